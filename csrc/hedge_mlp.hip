@@ -1,0 +1,596 @@
+// rphedge — fused hedge-MLP training step (K9), Adam/early-stop update (K10),
+// minibatch chunk permutation (K11) and the value/holdings/residual epilogue
+// (K12) for gfx950.
+//
+// Reference semantics (one backward-induction date):
+//   model(X1=[state_t, prices_{t+1}]) -> V = holdings(state_t) . prices_{t+1}
+//   fit MSE / 99% pinball, Adam(1e-3), batch 512, EarlyStopping(loss)
+//   (/root/reference/Replicating_Portfolio.py:149-221).
+//
+// Design (MI355X-first):
+//   * thread-per-path fp32 forward+backward; weights are wave-uniform and are
+//     read through the scalar unit (s_load -> SGPR operands of v_fma);
+//   * per-thread register accumulation of the full gradient (R = next pow2 of
+//     P+4 floats), one in-wave recursive-halving reduce-scatter (DPP/swizzle,
+//     ~4R VALU), one LDS cross-wave sum, one deterministic [num_wgs][R] slab;
+//   * the last-arriving workgroup (agent-scope release/acquire ticket) sums
+//     the slab and — for world_size == 1 — applies Keras-Adam, the epoch-end
+//     EarlyStopping/LR-schedule bookkeeping and the weight ping-pong in the
+//     same launch: ONE kernel per optimizer step, graph-capturable.
+//   * world_size > 1: the slab sum goes to grad_out, RCCL all-reduces it on
+//     the same stream and k_hedge_update applies the identical update on every
+//     rank (bitwise-identical decisions => identical early stopping).
+#include "rph_common.h"
+#include "rph_types.h"
+
+namespace rph {
+
+template <int NIN, int H, int NO, int HEAD>
+struct NetShape {
+  static constexpr int NHOLD = (HEAD == HEAD_COMPLEMENT) ? 2 : NO;
+  static constexpr int OW1 = 0;
+  static constexpr int OB1 = OW1 + NIN * H;
+  static constexpr int OW2 = OB1 + H;
+  static constexpr int OB2 = OW2 + H * H;
+  static constexpr int OW3 = OB2 + H;
+  static constexpr int OB3 = OW3 + H * NO;
+  static constexpr int P = OB3 + NO;
+  static constexpr int NSTAT = 4;  // loss, |e|, |e|/|y|, count
+  static constexpr int R = (P + NSTAT <= 128) ? 128 : 256;
+  static_assert(P <= PMAX, "network too large for PMAX");
+  static_assert(NHOLD <= MAXHOLD, "too many holdings");
+};
+
+// ---------------------------------------------------------------------------
+// K11: bijective chunk permutation for Keras-style per-epoch shuffling.  Paths
+// are permuted in chunks of 2^chunk_log2 (64 => one coalesced wave load); the
+// permutation is a keyed affine/xorshift bijection on the next power of two
+// with cycle-walking, so nothing is materialised.
+// ---------------------------------------------------------------------------
+struct Perm {
+  uint32_t mask, n, k1, a1, b1, a2, b2, sh;
+  bool on;
+  RPH_INLINE uint32_t f(uint32_t x) const {
+    x = (((x ^ k1) * a1) + b1) & mask;
+    x ^= x >> sh;
+    x = ((x * a2) + b2) & mask;
+    return x;
+  }
+  RPH_INLINE uint32_t operator()(uint32_t x) const {
+    if (!on) return x;
+    x = f(x);
+    while (x >= n) x = f(x);
+    return x;
+  }
+};
+
+RPH_INLINE Perm make_perm(uint32_t n_chunks, uint32_t seed, uint32_t epoch, bool on) {
+  Perm p;
+  uint32_t m = 1;
+  int bits = 0;
+  while (m < n_chunks) { m <<= 1; ++bits; }
+  p.mask = m - 1u;
+  p.n = n_chunks;
+  const u32x4 r = philox4x32_10({epoch, 0x5eedu, 0u, 0u}, seed, 0xC0FFEEu);
+  const u32x4 s = philox4x32_10({epoch, 0x5eedu, 1u, 0u}, seed, 0xC0FFEEu);
+  p.k1 = r.x & p.mask;
+  p.a1 = (r.y | 1u);
+  p.b1 = r.z;
+  p.a2 = (r.w | 1u);
+  p.b2 = s.x;
+  p.sh = bits > 1 ? (uint32_t)(bits / 2) : 1u;
+  p.on = on && n_chunks > 1;
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// Forward pass of one path (fp32).  W is wave-uniform.
+// ---------------------------------------------------------------------------
+template <int NIN, int H, int NO, int HEAD>
+RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], float alpha,
+                            float (&z1)[H], float (&a1)[H], float (&z2)[H], float (&a2)[H],
+                            float (&hold)[NetShape<NIN, H, NO, HEAD>::NHOLD]) {
+  using S = NetShape<NIN, H, NO, HEAD>;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    float acc = W[S::OB1 + j];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], W[S::OW1 + f * H + j], acc);
+    z1[j] = acc;
+    a1[j] = lrelu(acc, alpha);
+  }
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    float acc = W[S::OB2 + j];
+#pragma unroll
+    for (int i = 0; i < H; ++i) acc = fmaf(a1[i], W[S::OW2 + i * H + j], acc);
+    z2[j] = acc;
+    a2[j] = lrelu(acc, alpha);
+  }
+  float o[NO];
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    float acc = W[S::OB3 + k];
+#pragma unroll
+    for (int j = 0; j < H; ++j) acc = fmaf(a2[j], W[S::OW3 + j * NO + k], acc);
+    o[k] = acc;
+  }
+  if (HEAD == HEAD_COMPLEMENT) {  // EO: psi = 1 - phi  ("European Options.ipynb" cell 12)
+    hold[0] = o[0];
+    hold[1] = 1.0f - o[0];
+  } else {
+#pragma unroll
+    for (int k = 0; k < S::NHOLD; ++k) hold[k] = o[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Adam + EarlyStopping + LR schedule (K10).  Runs in ONE workgroup of 256
+// threads; gsum (LDS or global) holds the summed gradient [P] followed by the
+// 4 loss statistics.  Keras 2.x semantics:
+//   lr_t = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+//   w -= lr_t*m/(sqrt(v)+eps)
+// EarlyStopping.on_epoch_end: wait+=1; if loss<best: best=loss, save, wait=0;
+//   if wait>=patience and epoch>0: stop (+restore best).
+// ---------------------------------------------------------------------------
+template <int P>
+RPH_INLINE void apply_update(const float* gsum, NetWeights* wts, OptState* opt, FitState* fs,
+                             const float* lr_sched, int step, int steps_per_epoch, float* lds_scratch) {
+  const int tid = threadIdx.x;
+  const int cur = (int)wts->cur;
+  const int nxt = cur ^ 1;
+  // Epoch-begin LR schedule (Keras LearningRateScheduler.on_epoch_begin).
+  if (tid == 0) {
+    int ok = 1;
+    for (int i = 0; i < P; ++i) ok &= (int)__builtin_isfinite(gsum[i]);
+    lds_scratch[0] = (float)ok;
+    if (step == 0 && lr_sched != nullptr) {
+      const float l = lr_sched[(int)fs->epoch];
+      if (l == l) opt->lr = l;  // NaN => keep current
+    }
+  }
+  __syncthreads();
+  const bool finite = lds_scratch[0] != 0.f;
+  const float t = opt->t + (finite ? 1.f : 0.f);
+  const float b1 = opt->beta1, b2 = opt->beta2, eps = opt->eps, lr = opt->lr;
+  const float lr_t = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
+  for (int i = tid; i < P; i += blockDim.x) {
+    float w = wts->w[cur][i];
+    if (finite) {
+      const float g = gsum[i];
+      float m = opt->m[i], v = opt->v[i];
+      m = m + (g - m) * (1.f - b1);
+      v = v + (g * g - v) * (1.f - b2);
+      opt->m[i] = m;
+      opt->v[i] = v;
+      w = w - lr_t * m / (sqrtf(v) + eps);
+    }
+    wts->w[nxt][i] = w;
+  }
+  __syncthreads();
+  // Epoch bookkeeping: thread 0 decides, all threads copy.
+  __shared__ int s_act;  // 0 none, 1 save best, 2 restore best
+  if (tid == 0) {
+    if (finite) opt->t = t;
+    else opt->nan_steps += 1.f;
+    fs->loss_sum += gsum[P + 0];
+    fs->abs_sum += gsum[P + 1];
+    fs->ape_sum += gsum[P + 2];
+    fs->loss_cnt += gsum[P + 3];
+    int act = 0;
+    if (step == steps_per_epoch - 1) {
+      const float cnt = fmaxf(fs->loss_cnt, 1.f);
+      const float L = fs->loss_sum / cnt;
+      const int e = (int)fs->epoch;
+      if (e < MAXHIST) fs->hist[e] = L;
+      fs->last_loss = L;
+      fs->last_mae = fs->abs_sum / cnt;
+      fs->last_mape = 100.f * fs->ape_sum / cnt;
+      fs->loss_sum = fs->abs_sum = fs->ape_sum = fs->loss_cnt = 0.f;
+      fs->wait += 1.f;
+      const bool first = fs->has_best == 0.f;
+      if (L < fs->best_loss || first) {
+        if (L < fs->best_loss) { fs->best_loss = L; fs->wait = 0.f; }
+        fs->has_best = 1.f;
+        act = 1;
+      }
+      if (fs->wait >= fs->patience && e > 0) {
+        fs->stopped = 1.f;
+        if (fs->restore_best != 0.f) act = 2;
+      }
+      fs->epoch = (float)(e + 1);
+      if (fs->epoch >= fs->max_epochs && fs->stopped == 0.f) {
+        fs->stopped = 1.f;
+        if (fs->restore_best != 0.f && fs->restore_at_end != 0.f) act = 2;
+      }
+    }
+    s_act = act;
+  }
+  __syncthreads();
+  const int act = s_act;
+  if (act == 1) {
+    for (int i = tid; i < P; i += blockDim.x) fs->w_best[i] = wts->w[nxt][i];
+  } else if (act == 2) {
+    for (int i = tid; i < P; i += blockDim.x) wts->w[nxt][i] = fs->w_best[i];
+  }
+  __syncthreads();
+  if (tid == 0) wts->cur = (float)nxt;
+}
+
+// ---------------------------------------------------------------------------
+// K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
+// ---------------------------------------------------------------------------
+template <int NIN, int H, int NO, int HEAD>
+__global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, const int step) {
+  using S = NetShape<NIN, H, NO, HEAD>;
+  constexpr int R = S::R;
+  constexpr int P = S::P;
+  constexpr int NHOLD = S::NHOLD;
+  __shared__ __attribute__((aligned(16))) float lds[(4 * R > 1024 ? 4 * R : 1024) + 8];
+  __shared__ int s_last;
+
+  __shared__ __attribute__((aligned(16))) float wl[P + 4];
+
+  if (d.fit->stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
+  const int cur = (int)d.wts->cur;
+  // Weights are wave-uniform: stage them once in LDS and read them as
+  // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
+  for (int i = threadIdx.x; i < P; i += 256) wl[i] = d.wts->w[cur][i];
+  __syncthreads();
+  const float* __restrict__ W = wl;
+  const int epoch = (int)d.fit->epoch;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nwaves = gridDim.x * 4;
+  const int gw = blockIdx.x * 4 + wid;
+
+  const uint32_t n_chunks = (uint32_t)((d.n_local + (1 << d.chunk_log2) - 1) >> d.chunk_log2);
+  const Perm perm = make_perm(n_chunks, d.seed, (uint32_t)epoch, d.shuffle != 0);
+  const uint32_t cmask = (1u << d.chunk_log2) - 1u;
+
+  float g[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) g[i] = 0.f;
+
+  const float alpha = d.alpha;
+  const long long base = (long long)step * d.batch;
+  for (long long j0 = (long long)gw * 64; j0 < d.batch; j0 += (long long)nwaves * 64) {
+    const long long jl = j0 + lane;
+    const long long j = base + jl;
+    const bool valid = (jl < d.batch) && (j < d.n_local);
+    uint32_t p = 0;
+    if (valid) {
+      const uint32_t ju = (uint32_t)j;
+      p = (perm(ju >> d.chunk_log2) << d.chunk_log2) | (ju & cmask);
+      if (p >= (uint32_t)d.n_local) p = ju;  // (only when n_local is not chunk-aligned)
+    }
+    float x[NIN];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) x[f] = valid ? d.feat[f][p] : 0.f;
+    float pr[NHOLD];
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = valid ? d.price[k][p] : 0.f;
+    pr[NHOLD - 1] = d.bond;
+    const float y = valid ? d.target[p] : 0.f;
+
+    float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
+    net_forward<NIN, H, NO, HEAD>(W, x, alpha, z1, a1, z2, a2, hold);
+    float V = 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
+
+    // loss + dL/dV (mean over the global batch)
+    const float e = V - y;
+    float l, dV;
+    if (d.loss == LOSS_PINBALL) {
+      const float ep = -e;  // y - V
+      const float q = d.quantile;
+      const bool pos = q * ep >= (q - 1.f) * ep;
+      l = pos ? q * ep : (q - 1.f) * ep;
+      dV = pos ? -q : (1.f - q);
+    } else {
+      l = e * e;
+      dV = 2.f * e;
+    }
+    dV = valid ? dV * d.inv_batch : 0.f;
+    const float ae = fabsf(e);
+    g[P + 0] += valid ? l : 0.f;
+    g[P + 1] += valid ? ae : 0.f;
+    g[P + 2] += valid ? ae / fmaxf(fabsf(y), 1e-7f) : 0.f;
+    g[P + 3] += valid ? 1.f : 0.f;
+
+    // backward
+    float dout[NO];
+    if (HEAD == HEAD_COMPLEMENT) {
+      dout[0] = dV * (pr[0] - pr[1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k];
+    float dz2[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      float da = 0.f;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        g[S::OW3 + j * NO + k] = fmaf(a2[j], dout[k], g[S::OW3 + j * NO + k]);
+        da = fmaf(W[S::OW3 + j * NO + k], dout[k], da);
+      }
+      dz2[j] = da * lrelu_d(z2[j], alpha);
+      g[S::OB2 + j] += dz2[j];
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      float da = 0.f;
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
+        da = fmaf(W[S::OW2 + i * H + j], dz2[j], da);
+      }
+      const float dz1 = da * lrelu_d(z1[i], alpha);
+      g[S::OB1 + i] += dz1;
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
+    }
+  }
+
+  // ---- in-wave reduce-scatter, cross-wave LDS sum --------------------------
+  wave_reduce_scatter<R>(g, lane);
+  constexpr int PER = R / 64;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
+  __syncthreads();
+  float* red = lds;  // reuse: red[t] for t < R after the sum below
+  float val = 0.f;
+  if (threadIdx.x < R) val = lds[threadIdx.x] + lds[R + threadIdx.x] + lds[2 * R + threadIdx.x] + lds[3 * R + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x < R) red[threadIdx.x] = val;
+
+  if (gridDim.x > 1) {
+    // ---- publish partial, draw arrival ticket (Guideline 16 counter form) ----
+    if (threadIdx.x < R) d.slab[(size_t)blockIdx.x * R + threadIdx.x] = val;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t ticket = __hip_atomic_fetch_add(d.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = (ticket == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // ---- last arriver: deterministic slab sum (fixed row partition/order) ----
+    constexpr int Q = R / 4;                 // float4 columns
+    constexpr int GROUPS = 256 / Q;          // row groups
+    const int col = threadIdx.x % Q;
+    const int grp = threadIdx.x / Q;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* slab4 = reinterpret_cast<const float4*>(d.slab);
+    const int G = gridDim.x;
+#pragma unroll 8
+    for (int r = grp; r < G; r += GROUPS) {
+      const float4 v = slab4[(size_t)r * Q + col];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    __syncthreads();
+    reinterpret_cast<float4*>(lds)[grp * Q + col] = acc;
+    __syncthreads();
+    if (threadIdx.x < R) {
+      float s = 0.f;
+      for (int gi = 0; gi < GROUPS; ++gi) s += lds[gi * R + threadIdx.x];
+      val = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < R) red[threadIdx.x] = val;
+    if (threadIdx.x == 0) *d.counter = 0u;  // next launch starts from zero
+    __syncthreads();
+  } else {
+    __syncthreads();
+  }
+
+  if (d.fused_update) {
+    apply_update<P>(red, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch, lds + R);
+  } else if (threadIdx.x < R) {
+    d.grad_out[threadIdx.x] = red[threadIdx.x];
+  }
+}
+
+// K10 standalone (world_size > 1): one workgroup applies the all-reduced update.
+template <int NIN, int H, int NO, int HEAD>
+__global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const int step) {
+  using S = NetShape<NIN, H, NO, HEAD>;
+  __shared__ float gs[S::R + 8];
+  if (d.fit->stopped != 0.f) return;
+  for (int i = threadIdx.x; i < S::R; i += blockDim.x) gs[i] = d.grad_out[i];
+  __syncthreads();
+  apply_update<S::P>(gs, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch, gs + S::R);
+}
+
+// ---------------------------------------------------------------------------
+// K12: value / holdings / residual epilogue of a backward-induction date.
+//   V_t       = h(state_t) . p_t           (Keras predict(X0), RP:212)
+//   blend     = g + c (h - g)              (RP:221)
+//   residual  = V_{t+1} - h . p_{t+1}       ("VaR", RP:120; Q24)
+// Per-workgroup fp64 statistics go to a [num_wgs][EVAL_NSTAT] slab.
+// ---------------------------------------------------------------------------
+template <int NIN, int H, int NO, int HEAD>
+__global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
+  using S = NetShape<NIN, H, NO, HEAD>;
+  constexpr int NHOLD = S::NHOLD;
+  __shared__ double sst[4][EVAL_NSTAT];
+  __shared__ __attribute__((aligned(16))) float wl[2 * S::P + 8];
+  const bool has_b = d.wb != nullptr;
+  for (int i = threadIdx.x; i < S::P; i += 256) {
+    wl[i] = d.wa->w[(int)d.wa->cur][i];
+    if (has_b) wl[S::P + 4 + i] = d.wb->w[(int)d.wb->cur][i];
+  }
+  __syncthreads();
+  const float* __restrict__ WA = wl;
+  const float* __restrict__ WB = has_b ? wl + S::P + 4 : wl;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+
+  double st[EVAL_NSTAT];
+#pragma unroll
+  for (int i = 0; i < EVAL_NSTAT; ++i) st[i] = 0.0;
+  st[ES_RESMIN] = INFINITY;
+  st[ES_RESMAX] = -INFINITY;
+
+  for (int p0 = blockIdx.x * 256; p0 < d.n_local; p0 += gridDim.x * 256) {
+    const int p = p0 + threadIdx.x;
+    const bool valid = p < d.n_local;
+    const int pp = valid ? p : 0;
+    float x[NIN];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) x[f] = d.feat[f][pp];
+    float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], holdv[NHOLD];
+    net_forward<NIN, H, NO, HEAD>(WA, x, d.alpha, z1, a1, z2, a2, hold);
+#pragma unroll
+    for (int k = 0; k < NHOLD; ++k) holdv[k] = hold[k];
+    if (has_b) {
+      // V_t comes from net B (model2.predict, RP:218); reported holdings are
+      // the blend hA + hold_c (hB - hA) (get_phi_psi_VaR, RP:114-115).
+      net_forward<NIN, H, NO, HEAD>(WB, x, d.alpha, z1, a1, z2, a2, holdv);
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) hold[k] = hold[k] + d.hold_c * (holdv[k] - hold[k]);
+    }
+    float V = 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) V = fmaf(holdv[k], d.price_t[k][pp], V);
+    V = fmaf(holdv[NHOLD - 1], d.bond_t, V);
+    if (d.g_base) {
+      const float gb = d.g_base[pp];
+      V = gb + d.blend_c * (V - gb);
+    }
+    float res = 0.f, pred1 = 0.f;
+    const bool has1 = d.price_t1[0] != nullptr || NHOLD == 1;
+    if (has1) {
+#pragma unroll
+      for (int k = 0; k < NHOLD - 1; ++k) pred1 = fmaf(hold[k], d.price_t1[k][pp], pred1);
+      pred1 = fmaf(hold[NHOLD - 1], d.bond_t1, pred1);
+      if (d.target) res = d.target[pp] - pred1;
+    }
+    if (valid) {
+      if (d.v_out) d.v_out[p] = V;
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k)
+        if (d.hold_out[k]) d.hold_out[k][p] = hold[k];
+      if (d.resid_out) d.resid_out[p] = res;
+      if (d.pred1_out) d.pred1_out[p] = pred1;
+      st[ES_V] += V;
+      st[ES_V2] += (double)V * V;
+      st[ES_RES] += res;
+      st[ES_RES2] += (double)res * res;
+      st[ES_ABSRES] += fabs((double)res);
+      if (d.target) st[ES_APE] += fabs((double)res) / fmax(fabs((double)d.target[pp]), 1e-7);
+      st[ES_PRED1] += pred1;
+      st[ES_COUNT] += 1.0;
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) {
+        st[ES_HOLD + k] += hold[k];
+        st[ES_HOLD2 + k] += (double)hold[k] * hold[k];
+      }
+      st[ES_RESMIN] = fmin(st[ES_RESMIN], (double)res);
+      st[ES_RESMAX] = fmax(st[ES_RESMAX], (double)res);
+    }
+  }
+  // block reduce (fp64, only at the end)
+#pragma unroll
+  for (int i = 0; i < EVAL_NSTAT; ++i) {
+    double v = st[i];
+    if (i == ES_RESMIN) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    } else if (i == ES_RESMAX) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    } else {
+      v = wave_sum_d(v);
+    }
+    if (lane == 0) sst[wid][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < EVAL_NSTAT) {
+    const int i = threadIdx.x;
+    double v;
+    if (i == ES_RESMIN) v = fmin(fmin(sst[0][i], sst[1][i]), fmin(sst[2][i], sst[3][i]));
+    else if (i == ES_RESMAX) v = fmax(fmax(sst[0][i], sst[1][i]), fmax(sst[2][i], sst[3][i]));
+    else v = sst[0][i] + sst[1][i] + sst[2][i] + sst[3][i];
+    d.stats[(size_t)blockIdx.x * EVAL_NSTAT + i] = v;
+  }
+}
+
+}  // namespace rph
+
+// ---------------------------------------------------------------------------
+// Host dispatch over the supported network shapes.
+// ---------------------------------------------------------------------------
+using namespace rph;
+
+#define RPH_SHAPES(X)            \
+  X(1, 8, 1, HEAD_COMPLEMENT)    \
+  X(1, 8, 2, HEAD_FREE)          \
+  X(2, 8, 2, HEAD_FREE)          \
+  X(3, 8, 2, HEAD_FREE)          \
+  X(4, 8, 2, HEAD_FREE)          \
+  X(5, 8, 6, HEAD_FREE)          \
+  X(6, 8, 7, HEAD_FREE)
+
+static inline bool shape_is(int nin, int h, int nout, int head, int a, int b, int c, int e) {
+  return nin == a && h == b && nout == c && head == e;
+}
+
+extern "C" int rph_net_nparams(int nin, int h, int nout, int head, int* p_out, int* r_out) {
+#define X(A, B, C, E)                                  \
+  if (shape_is(nin, h, nout, head, A, B, C, E)) {      \
+    *p_out = NetShape<A, B, C, E>::P;                  \
+    *r_out = NetShape<A, B, C, E>::R;                  \
+    return 0;                                          \
+  }
+  RPH_SHAPES(X)
+#undef X
+  return -1;
+}
+
+extern "C" int rph_train_step(const TrainDesc* d, int step, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                        \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
+    hipLaunchKernelGGL((k_hedge_train_step<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d, step); \
+    return (int)hipGetLastError();                                                           \
+  }
+  RPH_SHAPES(X)
+#undef X
+  return -1;
+}
+
+extern "C" int rph_train_update(const TrainDesc* d, int step, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                        \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
+    hipLaunchKernelGGL((k_hedge_update<A, B, C, E>), dim3(1), dim3(256), 0, s, *d, step);   \
+    return (int)hipGetLastError();                                                           \
+  }
+  RPH_SHAPES(X)
+#undef X
+  return -1;
+}
+
+extern "C" int rph_eval(const EvalDesc* d, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                        \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
+    hipLaunchKernelGGL((k_hedge_eval<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d);  \
+    return (int)hipGetLastError();                                                           \
+  }
+  RPH_SHAPES(X)
+#undef X
+  return -1;
+}

@@ -1,0 +1,158 @@
+// rphedge — host/device shared plain-old-data structures.
+//
+// Every device-resident state block is a flat float32 array so the Python side
+// (rphedge/ops/native.py) can allocate it as a torch tensor and read fields by
+// index.  The field indices below are mirrored in rphedge/ops/layout.py and
+// checked by rph_layout_check() at import time.
+#pragma once
+#include <stdint.h>
+
+namespace rph {
+
+constexpr int PMAX = 256;      // max flat parameters per hedge network
+constexpr int MAXIN = 8;       // max input features
+constexpr int MAXHOLD = 8;     // max hedging instruments (assets + bond)
+constexpr int MAXHIST = 1024;  // per-fit epoch-loss history
+constexpr int EVAL_NSTAT = 32; // doubles per workgroup in the eval stats slab
+
+enum Head : int { HEAD_FREE = 0, HEAD_COMPLEMENT = 1 };
+enum Loss : int { LOSS_MSE = 0, LOSS_PINBALL = 1 };
+
+// Ping-pong weights: the step kernel reads w[cur] (never written in-launch) and
+// its last-arriving workgroup writes w[cur^1] then flips cur.
+struct NetWeights {
+  float w[2][PMAX];
+  float cur;
+  float pad[3];
+};
+
+// Keras-semantics Adam state (one per compiled optimizer; Q1 parity shares one
+// NetWeights between two OptStates — Replicating_Portfolio.py:172, :175-180).
+struct OptState {
+  float m[PMAX];
+  float v[PMAX];
+  float t;          // iteration counter (persists across fits like a Keras optimizer)
+  float lr;         // current learning rate (LearningRateScheduler writes it)
+  float beta1, beta2, eps;
+  float nan_steps;  // NaN/Inf guard: number of skipped updates
+  float pad0, pad1;
+};
+
+// EarlyStopping(monitor='loss') + epoch bookkeeping; reset by the host per fit
+// (Replicating_Portfolio.py:174, :203-209).
+struct FitState {
+  float w_best[PMAX];
+  float best_loss;     // +inf at fit start
+  float wait;
+  float stopped;       // 1 => remaining launched steps are no-ops
+  float epoch;         // epochs completed in this fit
+  float patience;
+  float max_epochs;
+  float restore_best;  // Keras restore_best_weights
+  float has_best;
+  float loss_sum, loss_cnt, abs_sum, ape_sum;  // running sums over the epoch
+  float last_loss, last_mae, last_mape;
+  float restore_at_end;  // Keras-3 semantics: also restore when max_epochs reached
+  float hist[MAXHIST];   // epoch loss history
+};
+
+constexpr int NETW_FLOATS = (int)(sizeof(NetWeights) / 4);
+constexpr int OPT_FLOATS = (int)(sizeof(OptState) / 4);
+constexpr int FIT_FLOATS = (int)(sizeof(FitState) / 4);
+
+// ---------------------------------------------------------------------------
+// Launch descriptors (passed by pointer from ctypes, by value to kernels).
+// ---------------------------------------------------------------------------
+struct TrainDesc {
+  const float* feat[MAXIN];      // features at t, [n_local] each
+  const float* price[MAXHOLD];   // traded-asset prices at t+1 (bond excluded)
+  const float* target;           // V_{t+1}, [n_local]
+  NetWeights* wts;
+  OptState* opt;
+  FitState* fit;
+  const float* lr_sched;         // [max_epochs] or null; NaN entry => keep lr
+  float* slab;                   // [max_wgs][R] partials
+  uint32_t* counter;             // arrival ticket (zeroed at alloc, reset by last arriver)
+  float* grad_out;               // [R] summed gradient (multi-rank path), may be null
+  float bond;                    // B_{t+1} (normalised), same for all paths
+  float alpha;                   // LeakyReLU slope
+  float quantile;                // pinball q
+  float inv_batch;               // 1 / global batch size
+  int loss;                      // Loss
+  int n_local;                   // local paths
+  int batch;                     // local batch per step
+  int steps_per_epoch;
+  int chunk_log2;                // shuffle granularity (0 = per path, 6 = 64-path chunks)
+  int shuffle;                   // Keras fit(shuffle=True)
+  uint32_t seed;
+  int fused_update;              // 1: last arriver applies Adam (world_size==1)
+  int num_wgs;
+  int nin, h, nout, head;        // network shape (dispatch)
+};
+
+struct EvalDesc {
+  const float* feat[MAXIN];      // features at t
+  const float* price_t[MAXHOLD]; // traded assets at t
+  const float* price_t1[MAXHOLD];// traded assets at t+1 (may be null => no residual)
+  const float* target;           // V_{t+1} (may be null)
+  const NetWeights* wa;
+  const NetWeights* wb;          // optional second network (holdings blend)
+  const float* g_base;           // optional: V_t = g + blend_c * (h - g)
+  float* v_out;                  // V_t (may be null)
+  float* hold_out[MAXHOLD];      // holdings (may be null)
+  float* resid_out;              // V_{t+1} - h . p_{t+1} (may be null)
+  float* pred1_out;              // h . p_{t+1} (may be null)
+  double* stats;                 // [num_wgs][EVAL_NSTAT]
+  float bond_t, bond_t1;
+  float alpha;
+  float blend_c;
+  float hold_c;                  // holdings = hA + hold_c * (hB - hA)
+  int n_local;
+  int num_wgs;
+  int nin, h, nout, head;
+};
+
+// Eval stats slab columns
+enum EvalStat : int {
+  ES_V = 0, ES_V2 = 1, ES_RES = 2, ES_RES2 = 3, ES_ABSRES = 4, ES_APE = 5, ES_PRED1 = 6,
+  ES_COUNT = 7, ES_HOLD = 8 /* 8 entries */, ES_HOLD2 = 16 /* 8 entries */, ES_RESMIN = 24,
+  ES_RESMAX = 25
+};
+
+struct SimDesc {
+  int model;                     // SimModel
+  int n_local;
+  long long path_offset;         // global index of local path 0 (Sobol index)
+  int n_fine;                    // fine grid points incl. t=0
+  int reduction;                 // store every `reduction` fine steps
+  int n_coarse;                  // stored points
+  int na;                        // assets (basket)
+  int fp64;                      // recursion in double
+  int parity;                    // reference quirks (SV sqrt of negative -> NaN, Q3 lambda index)
+  const uint32_t* sv1; const uint32_t* shift1; int dims1;   // Sobol table A
+  const uint32_t* sv2; const uint32_t* shift2; int dims2;   // Sobol table B (SV / mortality)
+  double s0[MAXIN], mu[MAXIN], sigma[MAXIN];
+  double chol[MAXIN * MAXIN];
+  double dt;
+  double inv_norm[MAXIN];
+  // SV / Heston
+  double v0, a, b, c, kappa, theta, xi, rho;
+  // mortality
+  double l0, lc, eta; int n0; uint32_t seed;
+  float* out;                    // [n_coarse][na][n_local]
+  float* out2;                   // second coarse output (vol / N-fraction)  [n_coarse][n_local]
+  float* out3;                   // third coarse output (lambda)             [n_coarse][n_local]
+  float* final_out;              // terminal fine value(s) [na][n_local]
+  float* final2_out;             // terminal fine N-fraction [n_local]
+};
+
+enum SimModel : int {
+  SIM_GBM_ARITH = 0,   // Y_t = Y_{t-1}(1 + mu dt + sigma sqrt(dt) Z)   (RP:64-65)
+  SIM_GBM_LOG = 1,     // log-Euler / exact GBM                          (EO:161-165)
+  SIM_SV_REF = 2,      // reference "CIR-on-sigma" SV                    (RP:282-289)
+  SIM_HESTON = 3,      // full-truncation Heston, rho-correlated
+  SIM_BASKET = 4,      // correlated log-GBM basket (Cholesky)
+  SIM_MORTALITY = 5,   // lambda Euler + binomial survivors             (RP:71-84)
+};
+
+}  // namespace rph

@@ -1,0 +1,403 @@
+"""Public API — same names, dict keys and return values as the reference.
+
+* ``Replicating_Portfolio(params) -> (phi, psi)``     (``Replicating_Portfolio.py:29-235``)
+* ``Replicating_Portfolio_SV(params) -> (phi, psi)``  (``Replicating_Portfolio.py:237-459``)
+* ``european_option(**kw) -> RunResult``              (``European Options.ipynb`` cells 3-20)
+
+plus :class:`HedgeRun`, the reusable pipeline (simulate -> payoff -> backward
+induction -> report) used by the CLI, the examples and ``bench.py``.  On a GPU
+the whole pipeline runs on device (HIP kernels, optional hipGraph capture and
+RCCL data parallelism); on CPU the torch reference backend runs the same
+algorithm.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import risk
+from .config import RunConfig, parse_params
+from .driver import BackwardInduction, InductionConfig, InductionResult, error_history, expected_value_trajectory
+from .engine import TrainConfig, make_backend, set_weights
+from .models import hedge_mlp as hm
+from .ops import layout as L
+from .ops import paths as P
+from .parallel import dist as D
+from .utils.logging import get_logger
+from .utils.profiling import PhaseTimer
+
+
+@dataclass
+class RunResult:
+    phi: float
+    psi: float
+    v0: float                              # scaled (EUR / option price)
+    scale: float
+    holdings0: np.ndarray
+    induction: InductionResult
+    errors: np.ndarray
+    p_e_values: np.ndarray
+    terminal_pnl: dict
+    var: dict = field(default_factory=dict)
+    summary: dict = field(default_factory=dict)
+    timings: dict = field(default_factory=dict)
+    config: dict = field(default_factory=dict)
+
+    def as_tuple(self):
+        return self.phi, self.psi
+
+
+class HedgeRun:
+    """One replicating-portfolio run, reusable for graph replay."""
+
+    def __init__(self, cfg: RunConfig, dist_info: D.DistInfo | None = None, stream=None):
+        self.cfg = cfg
+        self.log = get_logger()
+        if dist_info is None:
+            dist_info = D.init(device=cfg.device) if D.env_world() > 1 else D.DistInfo(
+                device=torch.device(cfg.device) if cfg.device else
+                (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else
+                 torch.device("cpu")))
+        self.di = dist_info
+        self.device = dist_info.device
+        self.backend_kind = cfg.backend or ("hip" if self.device.type == "cuda" else "torch")
+        if self.backend_kind == "hip" and self.device.type != "cuda":
+            raise ValueError("hip backend needs a GPU device")
+        self.stream = stream
+        self.grid = P.Grid(cfg.T, cfg.dt, cfg.rebalancing)
+        self.n_total = 2 ** int(cfg.n_paths)
+        self.offset, self.n_local = D.shard(self.n_total, dist_info.world, dist_info.rank)
+        self.timer = PhaseTimer(enabled=True, device=self.device)
+        self.kind = self._kind()
+        self.spec = self._spec()
+        self.paths = None
+        self.induction = None
+        self.graph = None
+
+    # ------------------------------------------------------------------ setup
+    def _kind(self) -> str:
+        c = self.cfg
+        if c.payoff in ("call", "put"):
+            return "european"
+        if c.payoff == "basket_call" or c.model == "basket":
+            return "basket"
+        return "pension"
+
+    def _spec(self) -> hm.NetSpec:
+        c = self.cfg
+        alpha = c.train.leaky_alpha
+        if self.kind == "european":
+            if c.model == "heston":
+                return hm.NetSpec(nin=2, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+            if c.parity.complement_head:
+                return hm.NetSpec(nin=1, hidden=8, nout=1, head=L.HEAD_COMPLEMENT, alpha=alpha,
+                                  layer_names=("LeakyReLU_1", "LeakyReLU_2", "Phi"))
+            return hm.NetSpec(nin=1, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+        if self.kind == "basket":
+            return hm.NetSpec(nin=c.n_assets, hidden=8, nout=c.n_assets + 1, head=L.HEAD_FREE, alpha=alpha)
+        if c.model in ("sv_ref", "heston") and not c.mortality:
+            return hm.NetSpec(nin=2, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+        return hm.NetSpec(nin=3, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+
+    @property
+    def scale(self) -> float:
+        c = self.cfg
+        return float(c.N * c.P) if self.kind == "pension" else float(c.Y if self.kind == "european" else 1.0)
+
+    def simulate(self):
+        """Paths (K1–K6) and terminal value V_T (K7) on the coarse grid."""
+        c, g, dev = self.cfg, self.grid, self.device
+        fp64 = c.dtype == "fp64"
+        kw = dict(device=dev, offset=self.offset, stream=self.stream)
+        with self.timer.phase("simulate"):
+            if self.kind == "european":
+                if c.model == "heston":
+                    p = P.simulate_sv(g, self.n_local, c.Y, c.r, c.v0, model="heston", kappa=c.kappa,
+                                      theta=c.theta, xi=c.xi, rho=c.rho, norm=c.Y, fp64=fp64, **kw)
+                else:
+                    scheme = "arith" if c.model == "gbm" else "log"
+                    p = P.simulate_gbm(g, self.n_local, c.Y, c.r, c.sigma, scheme=scheme, norm=c.Y, fp64=fp64,
+                                       **kw)
+                # EO normalises BOTH prices by S0 (cell 13: _B_t = B/S0, so psi counts
+                # unit bonds); the corrected default quotes the bond in S0 units.
+                p.bond = g.bond(c.r, norm=c.Y if c.parity.complement_head else 1.0)
+                v_t = P.payoff(c.option_type.lower(), p, c.K / c.Y, stream=self.stream)
+            elif self.kind == "basket":
+                na = c.n_assets
+                corr = np.full((na, na), c.basket_corr) + np.eye(na) * (1 - c.basket_corr)
+                s0 = [c.Y] * na
+                p = P.simulate_basket(g, self.n_local, s0, [c.r] * na, [c.sigma] * na, corr, norm=s0, **kw)
+                p.bond = g.bond(c.r)
+                w = c.basket_weights or tuple([1.0 / na] * na)
+                v_t = P.payoff("basket_call", p, c.K / c.Y, weights=w, stream=self.stream)
+            else:
+                if c.model in ("sv_ref", "heston"):
+                    sv_c = c.sv_c
+                    p = P.simulate_sv(g, self.n_local, c.Y, c.mu, c.s0, model=c.model, a=c.a, b=c.b, c=sv_c,
+                                      kappa=c.kappa, theta=c.theta, xi=c.xi, rho=c.rho, fp64=fp64,
+                                      parity_nan=c.parity.sv_sqrt_nan, **kw)
+                else:
+                    p = P.simulate_gbm(g, self.n_local, c.Y, c.mu, c.sigma, scheme=("log" if c.model == "gbm_log"
+                                                                                   else "arith"),
+                                       fp64=fp64, **kw)
+                if c.mortality:
+                    P.simulate_mortality(p, c.l0, c.c, c.ita, c.N, lambda_fine_index=c.parity.lambda_fine_index,
+                                         fp64=fp64, numpy_binomial=c.parity.numpy_binomial,
+                                         stream=self.stream)
+                else:
+                    p.kind = "pension_nomort"
+                p.bond = g.bond(c.r)
+                if not c.parity.fine_terminal_payoff:
+                    p.S_final = p.S[-1].clone()
+                    if p.nfrac is not None:
+                        p.nfrac_final = p.nfrac[-1].clone()
+                if p.nfrac is not None:
+                    # the coarse terminal survivors are what the liability is paid on (RP:184)
+                    p.nfrac_final = p.nfrac[-1]
+                v_t = P.payoff("guarantee", p, c.K, stream=self.stream)
+        self.paths, self.v_terminal = p, v_t
+        return p, v_t
+
+    def summary_stats(self) -> dict:
+        """E[N_T], P(out of the money), E[payoff] (C10; global over ranks)."""
+        c, p, w = self.cfg, self.paths, self.di.world
+        n = float(self.n_total)
+        yT = p.S_final if p.S_final.dim() == 1 else p.S_final[0]
+        if self.kind == "pension":
+            p_oom = D.all_reduce_scalar(float((yT < c.Y).double().sum()), device=self.device) / n if w > 1 else \
+                float((yT < c.Y).double().mean())
+        else:
+            strike = c.K / c.Y
+            p_oom = D.all_reduce_scalar(float((yT < strike).double().sum()), device=self.device) / n if w > 1 else \
+                float((yT < strike).double().mean())
+        e_pay = float(self.v_terminal.double().sum())
+        e_pay = (D.all_reduce_scalar(e_pay, device=self.device) if w > 1 else e_pay) / n
+        out = {"p_oom": p_oom, "E_payoff": e_pay}
+        if p.nfrac_final is not None:
+            en = float(p.nfrac_final.double().sum())
+            out["E_N_T"] = (D.all_reduce_scalar(en, device=self.device) if w > 1 else en) / n * c.N
+        out["mean_Y_T"] = (D.all_reduce_scalar(float(yT.double().sum()), device=self.device) if w > 1
+                           else float(yT.double().sum())) / n * (c.Y if self.kind != "pension" else 1.0)
+        return out
+
+    def init_weights(self, stats: dict) -> np.ndarray:
+        """Reference initialisers (RP:149-156): N(0,0.1) kernels + data-dependent output bias (Q11)."""
+        c, spec = self.cfg, self.spec
+        if self.kind == "pension":
+            bias = [1.0 - stats["p_oom"], stats["p_oom"]]
+        elif spec.head == L.HEAD_COMPLEMENT:
+            bias = [stats["E_payoff"]]                      # mean(payoff)/S0  (EO cell 12)
+        else:
+            p_itm = 1.0 - stats["p_oom"]
+            bias = [p_itm, stats["E_payoff"] - p_itm] + [0.0] * (spec.nout - 2)
+            if self.kind == "basket":
+                bias = [p_itm / c.n_assets] * c.n_assets + [stats["E_payoff"] - p_itm]
+        return hm.init_weights(spec, bias[: spec.nout], seed=c.train.seed)
+
+    def build(self, w0: np.ndarray | None = None):
+        c = self.cfg
+        if self.paths is None:
+            self.simulate()
+        self.stats0 = self.summary_stats()
+        self.w0 = self.init_weights(self.stats0) if w0 is None else w0
+        tr = c.train
+        tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
+                           lr=tr.lr)
+        self.backend = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
+                                    comm=self.di.comm, world=self.di.world, rank=self.di.rank, stream=self.stream)
+        pf = c.parity
+        icfg = InductionConfig(epochs_first=tr.epochs_first, epochs_rest=tr.epochs_rest,
+                               patience_first=tr.patience_first, patience_rest=tr.patience_rest,
+                               early_stopping=tr.early_stopping,
+                               lr_schedule_first=tr.lr_schedule_first and pf.lr_schedule_first_only,
+                               q99=tr.q99, quantile=tr.quantile, cost_of_capital=tr.cost_of_capital,
+                               shared_q99_model=pf.shared_q99_model,
+                               holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start,
+                               restore_best_at_end=pf.restore_best_at_end, keep_paths=c.keep_paths,
+                               poll_every=tr.poll_every, seed=tr.seed)
+        self.induction = BackwardInduction(self.paths, self.v_terminal, self.spec, self.w0, self.backend, icfg,
+                                           world=self.di.world, rank=self.di.rank)
+        return self
+
+    # ------------------------------------------------------------------ run
+    def enqueue(self, resimulate: bool = False):
+        """Enqueue the run (graph-capturable when ``poll_every == 0``)."""
+        ind = self.induction
+        if resimulate:
+            self.simulate()  # same buffers are re-created; only used outside capture
+        ind.values[-1].copy_(self.v_terminal)
+        ind.w_mse.copy_(ind.w_init)
+        ind.opt_mse.copy_(ind.opt_init)
+        if ind.cfg.q99:
+            if not ind.cfg.shared_q99_model:
+                ind.w_q.copy_(ind.w_init)
+            ind.opt_q.copy_(ind.opt_init)
+        with self.timer.phase("train"):
+            ind.enqueue()
+
+    def capture(self, include_simulation: bool = True):
+        """Capture simulation + full backward induction into ONE hipGraph."""
+        from .ops.native import Graph
+
+        if self.backend_kind != "hip":
+            raise RuntimeError("graph capture needs the hip backend")
+        assert self.cfg.train.poll_every == 0, "graph capture requires fully asynchronous early stopping"
+        s = self.stream or torch.cuda.current_stream(self.device)
+        # one eager pass first: populates every cached device constant (fit
+        # templates, LR tables, Sobol tables) so the capture allocates nothing
+        if include_simulation:
+            self._enqueue_sim_into_existing()
+        self.enqueue()
+        torch.cuda.synchronize(self.device)
+        g = Graph()
+        g.capture_begin(s)
+        try:
+            if include_simulation:
+                self._enqueue_sim_into_existing()
+            self.enqueue()
+        finally:
+            g.capture_end()
+        self.graph = g
+        return g
+
+    def _enqueue_sim_into_existing(self):
+        """Re-run the path kernels into the SAME buffers (graph-safe, no allocation)."""
+        c, g, p = self.cfg, self.grid, self.paths
+        from .ops import native
+        from .ops.sobol import device_table
+
+        if self.kind == "european" and c.model in ("gbm", "gbm_log"):
+            sv, sh, dims = device_table(g.n_fine, P.SEED_W1, self.device)
+            d = P._desc(L.SIM_GBM_LOG if c.model == "gbm_log" else L.SIM_GBM_ARITH, self.n_local, self.offset, g,
+                        c.dtype == "fp64", False)
+            d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), dims
+            d.s0[0], d.mu[0], d.sigma[0], d.inv_norm[0] = c.Y, c.r, c.sigma, 1.0 / c.Y
+            d.out, d.final_out = p.S.data_ptr(), p.S_final.data_ptr()
+            native.simulate(d, self.stream)
+            native.payoff({"call": 1, "put": 2}[c.option_type.lower()], p.S_final, self.v_terminal, c.K / c.Y,
+                          stream=self.stream)
+        else:
+            raise NotImplementedError("in-graph resimulation implemented for European GBM (bench config)")
+
+    def replay(self):
+        self.graph.replay(self.stream or torch.cuda.current_stream(self.device))
+
+    def run(self) -> RunResult:
+        t0 = time.perf_counter()
+        if self.induction is None:
+            self.build()
+        self.enqueue()
+        res = self.collect()
+        res.timings["wall_s"] = time.perf_counter() - t0
+        return res
+
+    def collect(self) -> RunResult:
+        c, w = self.cfg, self.di.world
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        ind = self.induction.collect()
+        scale = self.scale
+        h0 = ind.holdings0
+        if self.kind == "pension":
+            phi, psi = float(h0[0] * scale), float(h0[1] * scale)
+        else:
+            # psi in unit bonds (B_0 = 1): parity head already counts unit bonds
+            bond_unit = 1.0 if c.parity.complement_head else c.Y
+            phi, psi = float(h0[0]), float(h0[-1] * bond_unit)
+        term = ind.terminal
+        tp = {"mean": term.residual_mean * scale, "std": term.residual_std * scale,
+              "min": float(term.stats[L.ES_RESMIN]) * scale, "max": float(term.stats[L.ES_RESMAX]) * scale}
+        var = {}
+        if ind.residuals is not None and c.keep_paths:
+            var = risk.var_report(ind.residuals, scale=scale, world=w)
+        dtc = self.grid.dt_coarse
+        pe = expected_value_trajectory(ind, self.stats0["E_payoff"], c.mu if self.kind == "pension" else c.r, c.r,
+                                       dtc)
+        summary = dict(self.stats0)
+        summary.update({"V0": ind.v0 * scale, "phi0": phi, "psi0": psi, "n_paths": self.n_total,
+                        "n_dates": self.paths.n_coarse - 1, "reduction": self.grid.reduction,
+                        "epochs_mse": [d.fit_mse["epochs"] for d in ind.dates],
+                        "terminal_pnl_std": tp["std"]})
+        if self.kind == "european":
+            from .utils.reports import black_scholes
+
+            bs = black_scholes(c.Y, c.K, c.r, c.sigma, c.T, c.option_type)
+            summary["bs_price"], summary["bs_delta"] = bs
+        return RunResult(phi=phi, psi=psi, v0=ind.v0 * scale, scale=scale, holdings0=h0, induction=ind,
+                         errors=error_history(ind), p_e_values=pe, terminal_pnl=tp, var=var, summary=summary,
+                         timings=self.timer.summary(), config=c.to_dict())
+
+
+# ---------------------------------------------------------------------------
+# reference-compatible entry points
+# ---------------------------------------------------------------------------
+def _print_dates(run: HedgeRun, res: RunResult):
+    if not run.cfg.verbose or not run.di.is_main:
+        return
+    ind = res.induction
+    p = run.paths
+    dtc = run.grid.dt_coarse
+    for d in ind.dates:
+        t = d.index
+        y = float(p.asset(t + 1).double().mean()) * (1.0 if run.kind == "pension" else run.cfg.Y)
+        line = f">> Y_({(t + 1) * dtc:.2f}) = {y:.3f}"
+        if p.nfrac is not None:
+            line += f", N_({(t + 1) * dtc:.2f}) = {float(p.nfrac[t + 1].double().mean()):.3f}"
+        print(line)
+        if ind.residuals is not None:
+            q = risk.quantile(ind.residuals[t], (0.98, 0.99), run.di.world)
+            print(f"VaR: {q[0]:4f} (98%),  {q[1]:4f} (99%)  | epochs {d.fit_mse['epochs']}"
+                  f"{'/' + str(d.fit_q99['epochs']) if d.fit_q99 else ''}  loss {d.fit_mse['last_loss']:.3e}")
+
+
+def run_params(params: dict, sv: bool = False) -> RunResult:
+    cfg = parse_params(params, sv=sv)
+    run = HedgeRun(cfg)
+    if cfg.verbose and run.di.is_main:
+        print(f"reduction = {run.grid.reduction}")
+    res = run.run()
+    _print_dates(run, res)
+    if cfg.save_dir:
+        from .utils.model_io import save_run
+
+        save_run(cfg.save_dir, run, res)
+    return res
+
+
+def Replicating_Portfolio(params: dict):
+    """Pension-guarantee replicating portfolio; returns ``(phi, psi)`` at t=0
+    scaled by ``N*P`` (RP:29-235)."""
+    return run_params(params, sv=False).as_tuple()
+
+
+def Replicating_Portfolio_SV(params: dict):
+    """Stochastic-volatility variant (RP:237-459); returns ``(phi, psi)``."""
+    return run_params(params, sv=True).as_tuple()
+
+
+EO_DEFAULTS = dict(S0=100.0, K=100.0, r=0.08, sigma=0.15, T=1.0, N_paths=3000, dt=1 / 365,
+                   rebalancing_frequency=1 / 52, OPTION_TYPE="CALL")
+
+
+def european_option(S0=100.0, K=100.0, r=0.08, sigma=0.15, T=1.0, N_paths=3000, dt=1 / 365,
+                    rebalancing_frequency=1 / 52, OPTION_TYPE="CALL", parity: bool = False, model: str = "gbm_log",
+                    **extra) -> RunResult:
+    """European call/put replication (``European Options.ipynb``; C13, C16, C34).
+
+    Defaults are the notebook's (cell 3).  The reference driver trains the MSE
+    model only (the Q99 refit is commented out) and uses the ``psi = 1 - phi``
+    head (Q13) — reproduced with ``parity=True``; the default corrected head
+    learns (phi, psi) freely.
+    """
+    params = dict(Y=S0, K=K, T=T, mu=r, r=r, sigma=sigma, rebalancing=rebalancing_frequency, N=1, P=1.0, x=0.0,
+                  l0=0.0, c=0.0, ita=0.0, dt=dt, n_paths=int(math.ceil(math.log2(N_paths))), payoff="call" if
+                  OPTION_TYPE.upper() == "CALL" else "put", option_type=OPTION_TYPE.upper(), model=model,
+                  mortality=False, q99=False)
+    if parity:
+        params["parity"] = True
+    params.update(extra)
+    return run_params(params, sv=False)

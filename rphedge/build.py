@@ -1,0 +1,92 @@
+"""Build the native library ``rphedge/_lib/librphedge.so`` for gfx950.
+
+All HIP kernels (``csrc/*.hip``) and the C++ runtime (``csrc/*.cpp``) are
+compiled by ``hipcc --offload-arch=gfx950`` into ONE shared object with a C ABI
+(bound by ctypes in :mod:`rphedge.ops.native`).  The build is in-tree so the
+``.so`` travels with the repository snapshot to the GPU box.
+
+Usage::
+
+    python -m rphedge.build            # incremental (hash of sources)
+    python -m rphedge.build --force
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+LIBDIR = Path(__file__).resolve().parent / "_lib"
+LIB = LIBDIR / "librphedge.so"
+STAMP = LIBDIR / "librphedge.sha256"
+ARCH = os.environ.get("RPH_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build rphedge)")
+
+
+def sources() -> list[Path]:
+    return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.cpp")))
+
+
+def _digest(extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in sorted(sources() + list(CSRC.glob("*.h"))):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = False, debug: bool = False) -> Path:
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    flags = [
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-shared",
+        "-Wno-unused-result",
+        f"-I{CSRC}",
+        "-L/opt/rocm/lib",
+        "-lrccl",
+    ]
+    if debug:
+        flags += ["-g", "-DRPH_DEBUG=1"]
+    digest = _digest(" ".join(flags))
+    if not force and LIB.exists() and STAMP.exists() and STAMP.read_text().strip() == digest:
+        return LIB
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [_hipcc(), *flags, *[str(s) for s in sources()], "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+    os.replace(tmp, LIB)
+    STAMP.write_text(digest)
+    return LIB
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    lib = build(force=a.force, verbose=a.verbose, debug=a.debug)
+    print(lib)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

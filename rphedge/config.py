@@ -1,0 +1,193 @@
+"""Configuration: the reference dict API schema + extensions + parity flags.
+
+The reference configures everything through a plain ``params`` dict whose keys
+are read at ``Replicating_Portfolio.py:31-49`` (GBM) and ``:239-263`` (SV)
+(SURVEY §5.6).  :func:`parse_params` validates exactly those keys (``n_paths``
+is log2 of the path count, C03) and accepts optional extension keys with
+defaults.  Parity flags reproduce the reference quirks Q1–Q24;
+``parity=True`` switches all of them on, the default is corrected semantics.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import asdict, dataclass, field, fields
+
+GBM_KEYS = ("Y", "K", "T", "mu", "r", "sigma", "rebalancing", "N", "P", "x", "l0", "c", "ita", "dt", "n_paths")
+SV_KEYS = ("Y", "K", "T", "mu", "r", "s0", "a", "b", "c", "rebalancing", "N", "P", "x", "l0", "ita", "dt",
+           "n_paths")
+
+
+@dataclass
+class ParityFlags:
+    """Reference quirks.  True = reproduce the reference."""
+
+    shared_q99_model: bool = False      # Q1/Q2: "model2" aliases model1's layers, two Adam instances
+    holdings_blend_sign_rp: bool = False  # Q2: phi1 + c(phi1 - phi2) (RP) instead of phi1 + c(phi2 - phi1)
+    lambda_fine_index: bool = False     # Q3: lambda not subsampled (fine index t_i)
+    sv_c_overwrite: bool = False        # Q4: params['c'] is read twice (vol-of-vol := mortality c)
+    sv_reference_dynamics: bool = True  # Q5: reference SV recursion (no dt on mean reversion, vt as vol)
+    sv_sqrt_nan: bool = False           # numpy sqrt(negative) -> NaN propagation
+    fine_terminal_payoff: bool = True   # payoff from the last FINE point even if the coarse grid misses it
+    lr_schedule_first_only: bool = True  # Q17: LR schedule + patience 50 only on the first date
+    warm_start: bool = True             # Q18: one network refit at every date (weights + Adam persist)
+    restore_best_at_end: bool = False   # Keras-2: restore best weights only on early stop
+    numpy_binomial: bool = False        # Q20: numpy MT19937 reseeded 1234+t (CPU oracle only)
+    local_residual_pnl: bool = True     # Q24: "P&L at T" is the one-step residual
+    complement_head: bool = False       # Q13: European psi = 1 - phi head
+    eo_discount_artifact: bool = False  # Q14: report V0*e^{-rT} as "discounted E[V(T)]"
+
+    @classmethod
+    def reference(cls) -> "ParityFlags":
+        return cls(shared_q99_model=True, holdings_blend_sign_rp=True, lambda_fine_index=True,
+                   sv_c_overwrite=True, sv_reference_dynamics=True, sv_sqrt_nan=True,
+                   fine_terminal_payoff=True, lr_schedule_first_only=True, warm_start=True,
+                   restore_best_at_end=False, numpy_binomial=True, local_residual_pnl=True,
+                   complement_head=True, eo_discount_artifact=True)
+
+
+@dataclass
+class TrainingParams:
+    """Optimiser / schedule knobs (extension keys of the params dict)."""
+
+    batch_size: int = 512
+    epochs_first: int = 500
+    epochs_rest: int = 100
+    patience_first: int = 50
+    patience_rest: int = 7
+    lr: float = 1e-3
+    lr_schedule_first: bool = True
+    early_stopping: bool = True
+    cost_of_capital: float = 0.1
+    quantile: float = 0.99
+    q99: bool = True                 # second (pinball) fit per date
+    shuffle: bool = True
+    chunk_log2: int = 0              # 0 = per-path shuffle (Keras); 6 = 64-path chunks (throughput)
+    seed: int = 1234
+    leaky_alpha: float = 0.3
+    poll_every: int = 0              # host early-stop polling (0 = fully async / graph)
+
+
+@dataclass
+class RunConfig:
+    """Normalised configuration of one replicating-portfolio run."""
+
+    # financial (reference names kept in the dict API)
+    Y: float = 1.0
+    K: float = 1.0
+    T: float = 10.0
+    mu: float = 0.08
+    r: float = 0.03
+    sigma: float = 0.15
+    rebalancing: float = 0.25
+    N: int = 10_000
+    P: float = 100.0
+    x: float = 55.0                  # age (read but unused in the reference, Q19)
+    l0: float = 0.01
+    c: float = 0.075
+    ita: float = 0.000597
+    dt: float = 1 / 100
+    n_paths: int = 12                # log2 (C03)
+    # SV
+    s0: float = 0.15965
+    a: float = 0.0033566
+    b: float = 0.15431
+    sv_c: float = 0.015833
+    # Heston (corrected SV model)
+    kappa: float = 2.0
+    theta: float = 0.0256
+    xi: float = 0.3
+    rho: float = -0.7
+    v0: float = 0.0256
+    # extensions
+    model: str = "gbm"               # gbm | gbm_log | sv_ref | heston | basket
+    payoff: str = "guarantee"        # guarantee | call | put | basket_call
+    option_type: str = "CALL"
+    mortality: bool = True
+    n_assets: int = 1
+    basket_weights: tuple = ()
+    basket_corr: float = 0.5
+    device: str | None = None
+    backend: str | None = None       # hip | torch (default: hip when a GPU is present)
+    world_size: int | None = None
+    dtype: str = "fp32"              # recursion precision on device (fp32 | fp64)
+    verbose: bool = True
+    save_dir: str | None = None
+    keep_paths: bool = True          # keep per-date holdings/residuals for reports
+    train: TrainingParams = field(default_factory=TrainingParams)
+    parity: ParityFlags = field(default_factory=ParityFlags)
+
+    # derived grid (RP:51, :92-96)
+    @property
+    def n_fine(self) -> int:
+        return int(math.ceil(self.T / self.dt) + 1)
+
+    @property
+    def reduction(self) -> int:
+        return max(1, int(math.floor((self.n_fine - 1) / (self.T / self.rebalancing))))
+
+    @property
+    def n_coarse(self) -> int:
+        return int(math.ceil(self.n_fine / self.reduction))
+
+    @property
+    def dt_coarse(self) -> float:
+        return self.dt * self.reduction
+
+    @property
+    def paths(self) -> int:
+        return 2 ** int(self.n_paths)
+
+    def to_dict(self) -> dict:
+        d = asdict(self)
+        return d
+
+
+_TRAIN_KEYS = {f.name for f in fields(TrainingParams)}
+_PARITY_KEYS = {f.name for f in fields(ParityFlags)}
+_RUN_KEYS = {f.name for f in fields(RunConfig)} - {"train", "parity"}
+
+
+def parse_params(params: dict, sv: bool = False) -> RunConfig:
+    """Validate a reference-style params dict and build a :class:`RunConfig`.
+
+    Required keys are exactly the reference's (``GBM_KEYS``/``SV_KEYS``);
+    unknown keys raise.  Extension keys (``batch_size``, ``epochs_first`` …,
+    ``parity``/``parity_flags``, ``model``, ``payoff``, ``device`` …) are optional.
+    """
+    req = SV_KEYS if sv else GBM_KEYS
+    missing = [k for k in req if k not in params]
+    if missing:
+        raise KeyError(f"params missing required keys: {missing}")
+    cfg = RunConfig()
+    tr = TrainingParams()
+    pf = ParityFlags()
+    parity = params.get("parity", False)
+    if parity is True:
+        pf = ParityFlags.reference()
+    flags = params.get("parity_flags") or {}
+    for k, v in params.items():
+        if k in ("parity", "parity_flags"):
+            continue
+        if k in _TRAIN_KEYS:
+            setattr(tr, k, v)
+        elif k in _RUN_KEYS:
+            setattr(cfg, k, v)
+        elif k in _PARITY_KEYS:
+            setattr(pf, k, v)
+        else:
+            raise KeyError(f"unknown params key {k!r}")
+    for k, v in dict(flags).items():
+        if k not in _PARITY_KEYS:
+            raise KeyError(f"unknown parity flag {k!r}")
+        setattr(pf, k, v)
+    if sv:
+        # Q4: the reference reads params['c'] for BOTH the SV vol-of-vol and the
+        # mortality drift; the caller's dict (with its duplicate key) has c=0.075.
+        if "sv_c" not in params and pf.sv_c_overwrite:
+            cfg.sv_c = float(params["c"])
+        if "model" not in params:
+            cfg.model = "sv_ref"
+    cfg.train = tr
+    cfg.parity = pf
+    int(cfg.n_paths)
+    return cfg

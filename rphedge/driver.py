@@ -1,0 +1,210 @@
+"""Backward-induction replicating-portfolio driver (SURVEY C22–C27, L6).
+
+For every rebalancing date ``t = n-2 … 0`` (RP:193-227):
+
+1. fit the hedge MLP on ``X1 = [state_t, prices_{t+1}] -> V_{t+1}`` with MSE
+   (first date: 500 epochs, Keras LR schedule, patience 50; later: 100 epochs,
+   patience 7; warm start from date t+1 — Q17/Q18);
+2. ``g_t = predict(X0)``; ``Errors += evaluate(X1)`` (mae, mape);
+3. optionally refit with the 99% pinball loss (separate network by default,
+   the reference's shared-weights quirk Q1 with ``parity``);
+4. ``V_t = g_t + c (h_t - g_t)``; holdings, one-step residual ("VaR", Q24) and
+   per-date statistics in one fused epilogue kernel.
+
+Everything is enqueued on one stream without host synchronisation, so the
+whole scan (simulation included, see :mod:`rphedge.api`) can be captured into a
+single hipGraph and replayed (``bench.py``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .engine import DateData, FitConfig, TrainConfig, fit_seed, fit_summary, keras_lr_schedule, reduce_stats
+from .models.hedge_mlp import NetSpec
+from .ops import layout as L
+from .ops.paths import Paths
+
+
+@dataclass
+class InductionConfig:
+    epochs_first: int = 500
+    epochs_rest: int = 100
+    patience_first: int = 50
+    patience_rest: int = 7
+    early_stopping: bool = True
+    lr_schedule_first: bool = True
+    q99: bool = True
+    quantile: float = 0.99
+    cost_of_capital: float = 0.1
+    shared_q99_model: bool = False       # Q1
+    holdings_blend_sign_rp: bool = False  # Q2
+    warm_start: bool = True              # Q18
+    restore_best_at_end: bool = False
+    keep_paths: bool = True              # values / holdings / residual arrays
+    snapshot_weights: bool = True        # per-date weights for the saved-model format
+    poll_every: int = 0                  # host early-stop polling (0 = async)
+    seed: int = 1234
+
+
+@dataclass
+class DateResult:
+    index: int
+    time: float
+    fit_mse: dict | None = None
+    fit_q99: dict | None = None
+    stats: np.ndarray | None = None
+    stats_mse: np.ndarray | None = None
+
+    @property
+    def count(self) -> float:
+        return float(self.stats[L.ES_COUNT])
+
+    def mean_holdings(self, nhold: int) -> np.ndarray:
+        return self.stats[L.ES_HOLD:L.ES_HOLD + nhold] / self.count
+
+    @property
+    def mean_value(self) -> float:
+        return float(self.stats[L.ES_V] / self.count)
+
+    @property
+    def residual_mean(self) -> float:
+        return float(self.stats[L.ES_RES] / self.count)
+
+    @property
+    def residual_std(self) -> float:
+        n = self.count
+        m = self.stats[L.ES_RES] / n
+        return float(math.sqrt(max(self.stats[L.ES_RES2] / n - m * m, 0.0) * n / max(n - 1, 1)))
+
+    @property
+    def errors(self) -> tuple[float, float]:
+        """(mae, mape) of model1.evaluate(X1, V_{t+1}) after the MSE fit (RP:215)."""
+        s = self.stats_mse if self.stats_mse is not None else self.stats
+        n = s[L.ES_COUNT]
+        return float(s[L.ES_ABSRES] / n), float(100.0 * s[L.ES_APE] / n)
+
+
+@dataclass
+class InductionResult:
+    dates: list = field(default_factory=list)     # DateResult, ordered t = n-2 .. 0
+    values: torch.Tensor | None = None            # [n_coarse, n_local]
+    holdings: torch.Tensor | None = None          # [n_coarse-1, nhold, n_local]
+    residuals: torch.Tensor | None = None         # [n_coarse-1, n_local] (residual of date t at index t)
+    weights_snapshots: torch.Tensor | None = None  # [n_coarse-1, 2, NETW]
+    v0: float = float("nan")
+    holdings0: np.ndarray | None = None
+    terminal: DateResult | None = None
+
+
+class BackwardInduction:
+    """Owns device buffers for one run; ``enqueue()`` is graph-capturable."""
+
+    def __init__(self, paths: Paths, v_terminal: torch.Tensor, spec: NetSpec, w0: np.ndarray, backend,
+                 icfg: InductionConfig, world: int = 1, rank: int = 0):
+        self.paths, self.spec, self.backend, self.cfg = paths, spec, backend, icfg
+        self.world, self.rank = world, rank
+        n, nc = paths.n_local, paths.n_coarse
+        dev = paths.S.device
+        self.n_dates = nc - 1
+        self.values = torch.empty(nc, n, dtype=torch.float32, device=dev)
+        self.values[nc - 1].copy_(v_terminal)
+        self.v_terminal = v_terminal
+        self.gbuf = torch.empty(n, dtype=torch.float32, device=dev)
+        keep = icfg.keep_paths
+        self.holdings = torch.empty(nc - 1, spec.nhold, n, dtype=torch.float32, device=dev) if keep else None
+        self.residuals = torch.empty(nc - 1, n, dtype=torch.float32, device=dev) if keep else None
+        self.w_mse = backend.new_weights(w0)
+        self.opt_mse = backend.new_opt()
+        if icfg.q99:
+            self.w_q = self.w_mse if icfg.shared_q99_model else backend.new_weights(w0)
+            self.opt_q = backend.new_opt()
+        self.w_init = backend.new_weights(w0)
+        self.opt_init = backend.new_opt()
+        self.fits = [[backend.new_fit(), backend.new_fit()] for _ in range(self.n_dates)]
+        self.stats = [[backend.new_stats(), backend.new_stats()] for _ in range(self.n_dates)]
+        self.snap = torch.zeros(self.n_dates, 2, L.NETW_FLOATS, dtype=torch.float32, device=dev) \
+            if icfg.snapshot_weights else None
+        self.lr_first = tuple(keras_lr_schedule(icfg.epochs_first)) if icfg.lr_schedule_first else None
+
+    def _fcfg(self, first: bool, loss: int) -> FitConfig:
+        c = self.cfg
+        return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
+                         patience=c.patience_first if first else c.patience_rest,
+                         loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else None,
+                         restore_best=True, restore_at_end=c.restore_best_at_end, early_stopping=c.early_stopping)
+
+    def date_data(self, t: int) -> DateData:
+        p = self.paths
+        return DateData(feats=p.features(t), prices_next=p.prices(t + 1), bond_next=float(p.bond[t + 1]),
+                        target=self.values[t + 1], prices_now=p.prices(t), bond_now=float(p.bond[t]))
+
+    def enqueue(self):
+        c, be = self.cfg, self.backend
+        nc = self.paths.n_coarse
+        for t in range(nc - 2, -1, -1):
+            first = t == nc - 2
+            data = self.date_data(t)
+            if not c.warm_start and not first:
+                self.w_mse.copy_(self.w_init)
+                self.opt_mse.copy_(self.opt_init)
+                if c.q99:
+                    if not c.shared_q99_model:
+                        self.w_q.copy_(self.w_init)
+                    self.opt_q.copy_(self.opt_init)
+            f_m, f_q = self.fits[t]
+            s_m, s_q = self.stats[t]
+            be.fit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE),
+                   seed=fit_seed(c.seed, t, 0), poll_every=c.poll_every)
+            hold_out = [self.holdings[t, k] for k in range(self.spec.nhold)] if self.holdings is not None else None
+            resid_out = self.residuals[t] if self.residuals is not None else None
+            if c.q99:
+                be.eval(self.w_mse, data, s_m, v_out=self.gbuf)
+                be.fit(self.w_q, self.opt_q, f_q, data, self._fcfg(first, L.LOSS_PINBALL),
+                       seed=fit_seed(c.seed, t, 1), poll_every=c.poll_every)
+                hc = -c.cost_of_capital if c.holdings_blend_sign_rp else c.cost_of_capital
+                be.eval(self.w_mse, data, s_q, wts_b=self.w_q, g_base=self.gbuf, blend_c=c.cost_of_capital,
+                        hold_c=hc, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out)
+            else:
+                be.eval(self.w_mse, data, s_q, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out)
+            if self.snap is not None:
+                self.snap[t, 0].copy_(self.w_mse)
+                if c.q99:
+                    self.snap[t, 1].copy_(self.w_q)
+
+    def collect(self) -> InductionResult:
+        c = self.cfg
+        nc = self.paths.n_coarse
+        dtc = self.paths.grid.dt_coarse
+        res = InductionResult(values=self.values, holdings=self.holdings, residuals=self.residuals,
+                              weights_snapshots=self.snap)
+        for t in range(nc - 2, -1, -1):
+            f_m, f_q = self.fits[t]
+            s_m, s_q = self.stats[t]
+            d = DateResult(index=t, time=t * dtc, fit_mse=fit_summary(f_m),
+                           fit_q99=fit_summary(f_q) if c.q99 else None,
+                           stats=reduce_stats(s_q, self.world),
+                           stats_mse=reduce_stats(s_m, self.world) if c.q99 else None)
+            res.dates.append(d)
+        d0 = res.dates[-1]
+        res.terminal = res.dates[0]
+        res.v0 = d0.mean_value
+        res.holdings0 = d0.mean_holdings(self.spec.nhold)
+        return res
+
+
+def expected_value_trajectory(result: InductionResult, e_payoff: float, mu: float, r: float, dt: float) -> np.ndarray:
+    """P_E_Values (C27, RP:190, :227): [mean V_t, E_payoff e^{-mu dt its}, E_payoff e^{-r dt its}]."""
+    rows = [[e_payoff, e_payoff, e_payoff]]
+    for its, d in enumerate(result.dates, start=1):
+        rows.append([d.mean_value, e_payoff * math.exp(-mu * dt * its), e_payoff * math.exp(-r * dt * its)])
+    return np.asarray(rows)
+
+
+def error_history(result: InductionResult) -> np.ndarray:
+    """Errors (C26, RP:189, :215): rows [mae, mape], first row zeros like the reference."""
+    rows = [[0.0, 0.0]] + [list(d.errors) for d in result.dates]
+    return np.asarray(rows)

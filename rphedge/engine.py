@@ -1,0 +1,520 @@
+"""Training / evaluation engine: device-resident state + two backends.
+
+* :class:`HipBackend` — the MI355X path.  One fused HIP kernel per optimizer
+  step (``k_hedge_train_step``: forward + loss + backward + deterministic
+  gradient reduction + Keras-Adam + EarlyStopping/LR bookkeeping), optional
+  RCCL all-reduce of the 512-byte gradient packet on the same stream for DP,
+  and the ``k_hedge_eval`` epilogue.  Nothing synchronises with the host, so a
+  whole backward-induction run can be captured into ONE hipGraph
+  (:mod:`rphedge.driver`).
+* :class:`TorchBackend` — CPU (or any torch device) reference with identical
+  semantics: same chunk permutation (Philox), same Adam formula, same early
+  stopping; multi-process via ``torch.distributed`` (gloo).  It is the oracle
+  for GPU numerics tests and the "CPU plumbing" configuration of BASELINE.
+
+State blocks are flat float32 tensors (layout in :mod:`rphedge.ops.layout`).
+Reference semantics: ``Replicating_Portfolio.py:128-221`` (C17-C24).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .models.hedge_mlp import NetSpec, torch_forward
+from .ops import layout as L
+
+
+# ---------------------------------------------------------------------------
+# configuration
+# ---------------------------------------------------------------------------
+def keras_lr_schedule(epochs: int) -> list:
+    """``scheduler`` of RP:128-136 evaluated per epoch (NaN = keep current lr)."""
+    out = []
+    for e in range(epochs):
+        if e < 100:
+            out.append(1e-2)
+        elif e < 200:
+            out.append(1e-3)
+        elif e < 400:
+            out.append(5e-4)
+        else:
+            out.append(float("nan"))
+    return out
+
+
+@dataclass
+class FitConfig:
+    epochs: int = 100
+    patience: int = 7
+    loss: int = L.LOSS_MSE
+    quantile: float = 0.99
+    lr_schedule: tuple | None = None      # per-epoch learning rates (NaN keeps current)
+    restore_best: bool = True
+    restore_at_end: bool = False          # Keras-3 behaviour; Keras-2 restores only on early stop
+    early_stopping: bool = True
+
+    def key(self):
+        return (self.epochs, self.patience if self.early_stopping else 1 << 30, self.restore_best,
+                self.restore_at_end, tuple(self.lr_schedule) if self.lr_schedule is not None else None)
+
+
+@dataclass
+class TrainConfig:
+    batch_size: int = 512          # GLOBAL minibatch (reference: 512)
+    shuffle: bool = True           # Keras fit(shuffle=True)
+    chunk_log2: int = 0            # shuffle granularity: 0 = per path (Keras), 6 = 64-path chunks
+    seed: int = 1234
+    lr: float = 1e-3               # Adam(learning_rate=1e-3)
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-7              # Keras epsilon
+    max_wgs: int = 256             # workgroups per training step (deterministic slab rows)
+    paths_per_thread: int = 2      # target work per thread per step
+
+
+@dataclass
+class DateData:
+    """Inputs of one backward-induction fit (RP:200-201)."""
+
+    feats: list                    # state_t features, each [n_local]
+    prices_next: list              # traded assets at t+1 (bond excluded), each [n_local]
+    bond_next: float               # B_{t+1} (normalised)
+    target: torch.Tensor           # V_{t+1} [n_local]
+    prices_now: list = field(default_factory=list)   # assets at t (for V_t)
+    bond_now: float = 1.0
+
+
+def fit_seed(seed: int, date: int, net: int) -> int:
+    return (int(seed) * 1000003 + int(date) * 7919 + int(net) * 104729) & 0xFFFFFFFF
+
+
+# ---------------------------------------------------------------------------
+# state helpers (shared by both backends)
+# ---------------------------------------------------------------------------
+def make_weights(spec: NetSpec, w0: np.ndarray, device) -> torch.Tensor:
+    t = torch.zeros(L.NETW_FLOATS, dtype=torch.float32)
+    t[: spec.nparams] = torch.from_numpy(np.asarray(w0, np.float32))
+    t[L.PMAX: L.PMAX + spec.nparams] = t[: spec.nparams]
+    t[L.W_CUR] = 0.0
+    return t.to(device)
+
+
+def make_opt(tcfg: TrainConfig, device) -> torch.Tensor:
+    t = torch.zeros(L.OPT_FLOATS, dtype=torch.float32)
+    t[L.O_LR] = tcfg.lr
+    t[L.O_B1] = tcfg.beta1
+    t[L.O_B2] = tcfg.beta2
+    t[L.O_EPS] = tcfg.eps
+    return t.to(device)
+
+
+def fit_template(fcfg: FitConfig, device) -> torch.Tensor:
+    t = torch.zeros(L.FIT_FLOATS, dtype=torch.float32)
+    t[L.F_BEST] = float("inf")
+    t[L.F_PATIENCE] = float(fcfg.patience if fcfg.early_stopping else 1e30)
+    t[L.F_MAXEP] = float(fcfg.epochs)
+    t[L.F_RESTORE] = 1.0 if (fcfg.restore_best and fcfg.early_stopping) else 0.0
+    t[L.F_RESTORE_END] = 1.0 if fcfg.restore_at_end else 0.0
+    t[L.F_HIST:] = float("nan")
+    return t.to(device)
+
+
+def current_weights(spec: NetSpec, wts: torch.Tensor) -> np.ndarray:
+    w = wts.detach().cpu().numpy()
+    cur = int(w[L.W_CUR])
+    return w[cur * L.PMAX: cur * L.PMAX + spec.nparams].copy()
+
+
+def set_weights(spec: NetSpec, wts: torch.Tensor, w: np.ndarray):
+    t = torch.from_numpy(np.asarray(w, np.float32)).to(wts.device)
+    wts[: spec.nparams] = t
+    wts[L.PMAX: L.PMAX + spec.nparams] = t
+    wts[L.W_CUR] = 0.0
+
+
+def fit_summary(fit: torch.Tensor) -> dict:
+    f = fit.detach().cpu().numpy()
+    ep = int(f[L.F_EPOCH])
+    return {"epochs": ep, "stopped": bool(f[L.F_STOPPED]), "best_loss": float(f[L.F_BEST]),
+            "last_loss": float(f[L.F_LAST_LOSS]), "mae": float(f[L.F_LAST_MAE]),
+            "mape": float(f[L.F_LAST_MAPE]), "history": f[L.F_HIST:L.F_HIST + min(ep, L.MAXHIST)].tolist()}
+
+
+class _Cache:
+    def __init__(self):
+        self.d = {}
+
+    def get(self, key, make):
+        v = self.d.get(key)
+        if v is None:
+            v = make()
+            self.d[key] = v
+        return v
+
+
+def _steps(n_local: int, tcfg: TrainConfig, world: int) -> tuple[int, int]:
+    if tcfg.batch_size % world:
+        raise ValueError(f"global batch {tcfg.batch_size} not divisible by world size {world}")
+    bl = min(tcfg.batch_size // world, n_local)
+    steps = max(1, math.ceil(n_local / bl))
+    if n_local % bl:
+        raise ValueError(f"local paths {n_local} must be a multiple of the local batch {bl}")
+    return bl, steps
+
+
+# ---------------------------------------------------------------------------
+# HIP backend
+# ---------------------------------------------------------------------------
+class HipBackend:
+    name = "hip"
+
+    def __init__(self, spec: NetSpec, n_local: int, tcfg: TrainConfig, device=None, comm=None,
+                 world: int = 1, rank: int = 0, stream=None):
+        from .ops import native
+
+        self.native = native
+        native.load(required=True)
+        self.spec, self.n_local, self.tcfg = spec, int(n_local), tcfg
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.comm, self.world, self.rank = comm, world, rank
+        self.stream = stream
+        self.P, self.R = native.net_nparams(spec.nin, spec.hidden, spec.nout, spec.head)
+        assert self.P == spec.nparams
+        self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
+        work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
+        self.num_wgs = int(max(1, min(tcfg.max_wgs, work)))
+        dev = self.device
+        self.slab = torch.zeros(self.num_wgs, self.R, dtype=torch.float32, device=dev)
+        self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.grad = torch.zeros(self.R, dtype=torch.float32, device=dev)
+        self.eval_wgs = int(max(1, min(1024, (self.n_local + 255) // 256)))
+        self._cache = _Cache()
+
+    # -- state ---------------------------------------------------------------
+    def new_weights(self, w0):
+        return make_weights(self.spec, w0, self.device)
+
+    def new_opt(self):
+        return make_opt(self.tcfg, self.device)
+
+    def new_fit(self):
+        return torch.zeros(L.FIT_FLOATS, dtype=torch.float32, device=self.device)
+
+    def new_stats(self):
+        return torch.zeros(self.eval_wgs, L.EVAL_NSTAT, dtype=torch.float64, device=self.device)
+
+    def _template(self, fcfg: FitConfig):
+        return self._cache.get(("fit", fcfg.key()), lambda: fit_template(fcfg, self.device))
+
+    def _lr(self, fcfg: FitConfig):
+        if fcfg.lr_schedule is None:
+            return None
+        return self._cache.get(("lr", tuple(fcfg.lr_schedule)),
+                               lambda: torch.tensor(list(fcfg.lr_schedule), dtype=torch.float32, device=self.device))
+
+    # -- ops -----------------------------------------------------------------
+    def _train_desc(self, wts, opt, fit, data: DateData, fcfg: FitConfig, seed: int, lr_t):
+        n = self.native
+        d = n.TrainDesc()
+        for i, f in enumerate(data.feats):
+            d.feat[i] = f.data_ptr()
+        for i, p in enumerate(data.prices_next):
+            d.price[i] = p.data_ptr()
+        d.target = data.target.data_ptr()
+        d.wts, d.opt, d.fit = wts.data_ptr(), opt.data_ptr(), fit.data_ptr()
+        d.lr_sched = lr_t.data_ptr() if lr_t is not None else None
+        d.slab, d.counter, d.grad_out = self.slab.data_ptr(), self.counter.data_ptr(), self.grad.data_ptr()
+        d.bond = float(data.bond_next)
+        d.alpha = float(self.spec.alpha)
+        d.quantile = float(fcfg.quantile)
+        d.inv_batch = 1.0 / float(self.batch_local * self.world)
+        d.loss = int(fcfg.loss)
+        d.n_local = self.n_local
+        d.batch = self.batch_local
+        d.steps_per_epoch = self.steps_per_epoch
+        d.chunk_log2 = int(self.tcfg.chunk_log2)
+        d.shuffle = 1 if self.tcfg.shuffle else 0
+        d.seed = int(seed) & 0xFFFFFFFF
+        d.fused_update = 1 if self.world == 1 else 0
+        d.num_wgs = self.num_wgs
+        d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
+        return d
+
+    def fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig, seed: int, poll_every: int = 0):
+        """Enqueue a full Keras ``fit`` (epochs x steps).  With ``poll_every``>0 the
+        host checks the device early-stop flag every that many epochs and stops
+        enqueueing; otherwise everything is asynchronous (graph-capturable) and
+        surplus steps after an early stop are device-side no-ops."""
+        assert len(data.feats) == self.spec.nin and len(data.prices_next) == self.spec.nhold - 1
+        fit.copy_(self._template(fcfg), non_blocking=True)
+        lr_t = self._lr(fcfg)
+        d = self._train_desc(wts, opt, fit, data, fcfg, seed, lr_t)
+        n, S = self.native, self.steps_per_epoch
+        for e in range(fcfg.epochs):
+            for s in range(S):
+                n.train_step(d, s, self.stream)
+                if self.world > 1:
+                    self.comm.allreduce_(self.grad, self.stream)
+                    n.train_update(d, s, self.stream)
+            if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:
+                if float(fit[L.F_STOPPED].item()) != 0.0:
+                    break
+
+    def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
+             v_out=None, hold_out=None, resid_out=None, pred1_out=None):
+        n = self.native
+        d = n.EvalDesc()
+        for i, f in enumerate(data.feats):
+            d.feat[i] = f.data_ptr()
+        for i, p in enumerate(data.prices_now):
+            d.price_t[i] = p.data_ptr()
+        for i, p in enumerate(data.prices_next):
+            d.price_t1[i] = p.data_ptr()
+        d.target = data.target.data_ptr() if data.target is not None else None
+        d.wa = wts.data_ptr()
+        d.wb = wts_b.data_ptr() if wts_b is not None else None
+        d.g_base = g_base.data_ptr() if g_base is not None else None
+        d.v_out = v_out.data_ptr() if v_out is not None else None
+        if hold_out is not None:
+            for k, h in enumerate(hold_out):
+                d.hold_out[k] = h.data_ptr() if h is not None else None
+        d.resid_out = resid_out.data_ptr() if resid_out is not None else None
+        d.pred1_out = pred1_out.data_ptr() if pred1_out is not None else None
+        d.stats = stats.data_ptr()
+        d.bond_t, d.bond_t1 = float(data.bond_now), float(data.bond_next)
+        d.alpha = float(self.spec.alpha)
+        d.blend_c, d.hold_c = float(blend_c), float(hold_c)
+        d.n_local = self.n_local
+        d.num_wgs = self.eval_wgs
+        d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
+        n.eval_(d, self.stream)
+
+
+# ---------------------------------------------------------------------------
+# Torch reference backend (CPU oracle; gloo DP)
+# ---------------------------------------------------------------------------
+class TorchBackend:
+    name = "torch"
+
+    def __init__(self, spec: NetSpec, n_local: int, tcfg: TrainConfig, device="cpu", comm=None,
+                 world: int = 1, rank: int = 0, dtype=torch.float32, stream=None):
+        self.spec, self.n_local, self.tcfg = spec, int(n_local), tcfg
+        self.device = torch.device(device)
+        self.world, self.rank = world, rank
+        self.dtype = dtype
+        self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
+        self.eval_wgs = 1
+        self._order_cache = {}
+
+    new_weights = HipBackend.new_weights
+    new_opt = HipBackend.new_opt
+
+    def new_fit(self):
+        return torch.zeros(L.FIT_FLOATS, dtype=torch.float32, device=self.device)
+
+    def new_stats(self):
+        return torch.zeros(1, L.EVAL_NSTAT, dtype=torch.float64, device=self.device)
+
+    def _order(self, seed, epoch):
+        from .ops.philox import epoch_order
+
+        key = (seed, epoch)
+        o = self._order_cache.get(key)
+        if o is None:
+            o = torch.from_numpy(epoch_order(self.n_local, self.tcfg.chunk_log2, seed, epoch,
+                                             self.tcfg.shuffle)).to(self.device)
+            if len(self._order_cache) > 64:
+                self._order_cache.clear()
+            self._order_cache[key] = o
+        return o
+
+    def _allreduce(self, t: torch.Tensor):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(t)
+        return t
+
+    def fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig, seed: int, poll_every: int = 0):
+        spec, dt = self.spec, self.dtype
+        P = spec.nparams
+        fit.copy_(fit_template(fcfg, self.device))
+        X = torch.stack([f.to(dt) for f in data.feats], dim=1)
+        pr = torch.stack([p.to(dt) for p in data.prices_next] +
+                         [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
+        y = data.target.to(dt)
+        cur = int(wts[L.W_CUR].item())
+        w = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
+        m = opt[L.O_M:L.O_M + P].to(dt).clone()
+        v = opt[L.O_V:L.O_V + P].to(dt).clone()
+        t_it = float(opt[L.O_T].item())
+        lr = float(opt[L.O_LR].item())
+        b1, b2, eps = (float(opt[i].item()) for i in (L.O_B1, L.O_B2, L.O_EPS))
+        inv_b = 1.0 / float(self.batch_local * self.world)
+        best, wait, has_best = float("inf"), 0, False
+        w_best = w.clone()
+        patience = fcfg.patience if fcfg.early_stopping else 1 << 30
+        restore = fcfg.restore_best and fcfg.early_stopping
+        hist = []
+        sums = torch.zeros(4, dtype=torch.float64)
+        stopped = False
+        nan_steps = 0
+        epoch = 0
+        q = fcfg.quantile
+        for epoch in range(fcfg.epochs):
+            if fcfg.lr_schedule is not None:
+                l_ = fcfg.lr_schedule[epoch]
+                if l_ == l_:
+                    lr = float(l_)
+            order = self._order(seed, epoch)
+            for s in range(self.steps_per_epoch):
+                idx = order[s * self.batch_local:(s + 1) * self.batch_local]
+                wv = w.detach().requires_grad_(True)
+                V = (torch_forward(spec, wv, X[idx]) * pr[idx]).sum(dim=1)
+                e = V - y[idx]
+                if fcfg.loss == L.LOSS_PINBALL:
+                    ep = -e
+                    lvec = torch.maximum(q * ep, (q - 1.0) * ep)
+                else:
+                    lvec = e * e
+                (lvec.sum() * inv_b).backward()
+                pkt = torch.zeros(P + 4, dtype=torch.float64)
+                pkt[:P] = wv.grad.to(torch.float64)
+                with torch.no_grad():
+                    pkt[P] = lvec.sum().double()
+                    pkt[P + 1] = e.abs().sum().double()
+                    pkt[P + 2] = (e.abs() / y[idx].abs().clamp_min(1e-7)).sum().double()
+                    pkt[P + 3] = float(len(idx))
+                self._allreduce(pkt)
+                g = pkt[:P].to(dt)
+                if torch.isfinite(g).all():
+                    t_it += 1.0
+                    lr_t = lr * math.sqrt(1.0 - b2 ** t_it) / (1.0 - b1 ** t_it)
+                    m = m + (g - m) * (1.0 - b1)
+                    v = v + (g * g - v) * (1.0 - b2)
+                    w = (w - lr_t * m / (torch.sqrt(v) + eps)).detach()
+                else:
+                    nan_steps += 1
+                sums += pkt[P:P + 4]
+            cnt = max(float(sums[3]), 1.0)
+            Lval = float(sums[0]) / cnt
+            hist.append(Lval)
+            fit[L.F_LAST_MAE] = float(sums[1]) / cnt
+            fit[L.F_LAST_MAPE] = 100.0 * float(sums[2]) / cnt
+            sums.zero_()
+            wait += 1
+            if Lval < best or not has_best:
+                if Lval < best:
+                    best, wait = Lval, 0
+                has_best = True
+                w_best = w.clone()
+            if wait >= patience and epoch > 0:
+                stopped = True
+                if restore:
+                    w = w_best.clone()
+                break
+        else:
+            if restore and fcfg.restore_at_end:
+                w = w_best.clone()
+        n_ep = epoch + 1
+        wts[:P] = w.to(torch.float32)
+        wts[L.PMAX:L.PMAX + P] = w.to(torch.float32)
+        wts[L.W_CUR] = 0.0
+        opt[L.O_M:L.O_M + P] = m.to(torch.float32)
+        opt[L.O_V:L.O_V + P] = v.to(torch.float32)
+        opt[L.O_T] = t_it
+        opt[L.O_LR] = lr
+        opt[L.O_NAN] += nan_steps
+        fit[L.F_BEST] = best
+        fit[L.F_WAIT] = wait
+        fit[L.F_STOPPED] = 1.0
+        fit[L.F_EPOCH] = n_ep
+        fit[L.F_LAST_LOSS] = hist[-1] if hist else float("nan")
+        fit[L.F_WBEST:L.F_WBEST + P] = w_best.to(torch.float32)
+        k = min(len(hist), L.MAXHIST)
+        fit[L.F_HIST:L.F_HIST + k] = torch.tensor(hist[:k], dtype=torch.float32)
+        _ = stopped
+
+    def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
+             v_out=None, hold_out=None, resid_out=None, pred1_out=None):
+        spec, dt = self.spec, torch.float32
+        P = spec.nparams
+        X = torch.stack([f.to(dt) for f in data.feats], dim=1)
+
+        def cw(t):
+            cur = int(t[L.W_CUR].item())
+            return t[cur * L.PMAX: cur * L.PMAX + P].to(dt)
+
+        with torch.no_grad():
+            hold = torch_forward(spec, cw(wts), X)
+            holdv = hold
+            if wts_b is not None:
+                holdv = torch_forward(spec, cw(wts_b), X)
+                hold = hold + hold_c * (holdv - hold)
+            n = X.shape[0]
+            pr0 = torch.stack([p.to(dt) for p in data.prices_now] +
+                              [torch.full((n,), float(data.bond_now), dtype=dt, device=X.device)], dim=1)
+            V = (holdv * pr0).sum(dim=1)
+            if g_base is not None:
+                V = g_base + blend_c * (V - g_base)
+            if data.prices_next:
+                pr1 = torch.stack([p.to(dt) for p in data.prices_next] +
+                                  [torch.full((n,), float(data.bond_next), dtype=dt, device=X.device)], dim=1)
+                pred1 = (hold * pr1).sum(dim=1)
+            else:
+                pred1 = torch.zeros_like(V)
+            res = (data.target.to(dt) - pred1) if data.target is not None else torch.zeros_like(V)
+            if v_out is not None:
+                v_out.copy_(V)
+            if hold_out is not None:
+                for k, h in enumerate(hold_out):
+                    if h is not None:
+                        h.copy_(hold[:, k])
+            if resid_out is not None:
+                resid_out.copy_(res)
+            if pred1_out is not None:
+                pred1_out.copy_(pred1)
+            st = torch.zeros(L.EVAL_NSTAT, dtype=torch.float64)
+            Vd, rd, hd = V.double(), res.double(), hold.double()
+            st[L.ES_V] = Vd.sum()
+            st[L.ES_V2] = (Vd * Vd).sum()
+            st[L.ES_RES] = rd.sum()
+            st[L.ES_RES2] = (rd * rd).sum()
+            st[L.ES_ABSRES] = rd.abs().sum()
+            if data.target is not None:
+                st[L.ES_APE] = (rd.abs() / data.target.double().abs().clamp_min(1e-7)).sum()
+            st[L.ES_PRED1] = pred1.double().sum()
+            st[L.ES_COUNT] = n
+            for k in range(spec.nhold):
+                st[L.ES_HOLD + k] = hd[:, k].sum()
+                st[L.ES_HOLD2 + k] = (hd[:, k] ** 2).sum()
+            st[L.ES_RESMIN] = rd.min()
+            st[L.ES_RESMAX] = rd.max()
+            stats[0].copy_(st)
+
+
+def make_backend(kind: str, spec: NetSpec, n_local: int, tcfg: TrainConfig, **kw):
+    if kind == "hip":
+        return HipBackend(spec, n_local, tcfg, **kw)
+    kw.pop("stream", None)
+    return TorchBackend(spec, n_local, tcfg, **kw)
+
+
+def reduce_stats(stats: torch.Tensor, world: int = 1) -> np.ndarray:
+    """Sum per-workgroup eval partials (and across ranks) -> [EVAL_NSTAT] float64."""
+    s = stats.sum(dim=0)
+    mn = stats[:, L.ES_RESMIN].min()
+    mx = stats[:, L.ES_RESMAX].max()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(s)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    s = s.detach().cpu().numpy().copy()
+    s[L.ES_RESMIN] = float(mn)
+    s[L.ES_RESMAX] = float(mx)
+    return s

@@ -1,0 +1,54 @@
+"""Float-index layout of the device state blocks (mirror of csrc/rph_types.h).
+
+Checked against the native library at load time (``rph_layout``)."""
+PMAX = 256
+MAXHIST = 1024
+EVAL_NSTAT = 32
+
+# NetWeights: float w[2][PMAX]; float cur; pad[3]
+NETW_FLOATS = 2 * PMAX + 4
+W_CUR = 2 * PMAX
+
+# OptState: m[PMAX], v[PMAX], t, lr, beta1, beta2, eps, nan_steps, pad0, pad1
+OPT_FLOATS = 2 * PMAX + 8
+O_M = 0
+O_V = PMAX
+O_T = 2 * PMAX
+O_LR = O_T + 1
+O_B1 = O_T + 2
+O_B2 = O_T + 3
+O_EPS = O_T + 4
+O_NAN = O_T + 5
+
+# FitState
+F_WBEST = 0
+F_BEST = PMAX
+F_WAIT = PMAX + 1
+F_STOPPED = PMAX + 2
+F_EPOCH = PMAX + 3
+F_PATIENCE = PMAX + 4
+F_MAXEP = PMAX + 5
+F_RESTORE = PMAX + 6
+F_HASBEST = PMAX + 7
+F_LOSS_SUM = PMAX + 8
+F_LOSS_CNT = PMAX + 9
+F_ABS_SUM = PMAX + 10
+F_APE_SUM = PMAX + 11
+F_LAST_LOSS = PMAX + 12
+F_LAST_MAE = PMAX + 13
+F_LAST_MAPE = PMAX + 14
+F_RESTORE_END = PMAX + 15
+F_HIST = PMAX + 16
+FIT_FLOATS = F_HIST + MAXHIST
+
+# eval stats columns
+ES_V, ES_V2, ES_RES, ES_RES2, ES_ABSRES, ES_APE, ES_PRED1, ES_COUNT = range(8)
+ES_HOLD = 8
+ES_HOLD2 = 16
+ES_RESMIN = 24
+ES_RESMAX = 25
+
+HEAD_FREE, HEAD_COMPLEMENT = 0, 1
+LOSS_MSE, LOSS_PINBALL = 0, 1
+
+SIM_GBM_ARITH, SIM_GBM_LOG, SIM_SV_REF, SIM_HESTON, SIM_BASKET, SIM_MORTALITY = range(6)

@@ -1,0 +1,302 @@
+"""ctypes bindings to the in-tree native library ``rphedge/_lib/librphedge.so``.
+
+The library (HIP kernels for gfx950 + C++ runtime: hipGraph capture, RCCL
+communicator) exposes a plain C ABI.  ``torch`` is imported first so that the
+HIP runtime (``libamdhip64.so.7``) and RCCL (``librccl.so.1``) already loaded
+by torch are reused by the dynamic loader — one HIP runtime per process,
+device pointers from torch tensors are valid in our kernels.
+
+On a machine with a GPU the native library is mandatory: every op raises if it
+is missing (no silent eager fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded before librphedge.so)
+
+from . import layout as L
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / "librphedge.so"
+_lib = None
+_load_error: str | None = None
+
+MAXIN, MAXHOLD = 8, 8
+VP = C.c_void_p
+
+
+class TrainDesc(C.Structure):
+    _fields_ = [
+        ("feat", VP * MAXIN), ("price", VP * MAXHOLD), ("target", VP),
+        ("wts", VP), ("opt", VP), ("fit", VP), ("lr_sched", VP),
+        ("slab", VP), ("counter", VP), ("grad_out", VP),
+        ("bond", C.c_float), ("alpha", C.c_float), ("quantile", C.c_float), ("inv_batch", C.c_float),
+        ("loss", C.c_int), ("n_local", C.c_int), ("batch", C.c_int), ("steps_per_epoch", C.c_int),
+        ("chunk_log2", C.c_int), ("shuffle", C.c_int), ("seed", C.c_uint32), ("fused_update", C.c_int),
+        ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
+    ]
+
+
+class EvalDesc(C.Structure):
+    _fields_ = [
+        ("feat", VP * MAXIN), ("price_t", VP * MAXHOLD), ("price_t1", VP * MAXHOLD), ("target", VP),
+        ("wa", VP), ("wb", VP), ("g_base", VP), ("v_out", VP), ("hold_out", VP * MAXHOLD),
+        ("resid_out", VP), ("pred1_out", VP), ("stats", VP),
+        ("bond_t", C.c_float), ("bond_t1", C.c_float), ("alpha", C.c_float), ("blend_c", C.c_float),
+        ("hold_c", C.c_float),
+        ("n_local", C.c_int), ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int),
+        ("head", C.c_int),
+    ]
+
+
+class SimDesc(C.Structure):
+    _fields_ = [
+        ("model", C.c_int), ("n_local", C.c_int), ("path_offset", C.c_longlong),
+        ("n_fine", C.c_int), ("reduction", C.c_int), ("n_coarse", C.c_int), ("na", C.c_int),
+        ("fp64", C.c_int), ("parity", C.c_int),
+        ("sv1", VP), ("shift1", VP), ("dims1", C.c_int),
+        ("sv2", VP), ("shift2", VP), ("dims2", C.c_int),
+        ("s0", C.c_double * MAXIN), ("mu", C.c_double * MAXIN), ("sigma", C.c_double * MAXIN),
+        ("chol", C.c_double * (MAXIN * MAXIN)), ("dt", C.c_double), ("inv_norm", C.c_double * MAXIN),
+        ("v0", C.c_double), ("a", C.c_double), ("b", C.c_double), ("c", C.c_double),
+        ("kappa", C.c_double), ("theta", C.c_double), ("xi", C.c_double), ("rho", C.c_double),
+        ("l0", C.c_double), ("lc", C.c_double), ("eta", C.c_double), ("n0", C.c_int), ("seed", C.c_uint32),
+        ("out", VP), ("out2", VP), ("out3", VP), ("final_out", VP), ("final2_out", VP),
+    ]
+
+
+def _expected_layout() -> list[int]:
+    f = 4
+    T, E, S = TrainDesc, EvalDesc, SimDesc
+    return [
+        L.NETW_FLOATS * f, L.OPT_FLOATS * f, L.FIT_FLOATS * f,
+        L.W_CUR * f, L.O_T * f, L.O_LR * f, L.O_NAN * f,
+        L.F_BEST * f, L.F_STOPPED * f, L.F_EPOCH * f, L.F_LAST_LOSS * f, L.F_RESTORE_END * f, L.F_HIST * f,
+        C.sizeof(T), T.price.offset, T.target.offset, T.wts.offset, T.lr_sched.offset, T.slab.offset,
+        T.counter.offset, T.grad_out.offset, T.bond.offset, T.inv_batch.offset, T.loss.offset, T.seed.offset,
+        T.num_wgs.offset, T.head.offset,
+        C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
+        E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
+        E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset,
+        C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
+        S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
+        S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset,
+    ]
+
+
+def _bind(lib):
+    sig = {
+        "rph_last_error": (C.c_char_p, []),
+        "rph_layout": (C.c_int, [C.POINTER(C.c_longlong), C.c_int]),
+        "rph_device_info": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_longlong),
+                                      C.c_char_p, C.c_int]),
+        "rph_memset_async": (C.c_int, [VP, C.c_int, C.c_longlong, VP]),
+        "rph_stream_sync": (C.c_int, [VP]),
+        "rph_graph_begin": (C.c_int, [VP]),
+        "rph_graph_end": (C.c_int, [VP, C.POINTER(VP), C.POINTER(C.c_longlong)]),
+        "rph_graph_launch": (C.c_int, [VP, VP]),
+        "rph_graph_destroy": (C.c_int, [VP]),
+        "rph_nccl_unique_id": (C.c_int, [C.c_char_p]),
+        "rph_nccl_init": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(VP)]),
+        "rph_nccl_allreduce_f32": (C.c_int, [VP, VP, C.c_longlong, VP]),
+        "rph_nccl_allreduce_f64": (C.c_int, [VP, VP, C.c_longlong, VP]),
+        "rph_nccl_allreduce_u32": (C.c_int, [VP, VP, C.c_longlong, VP]),
+        "rph_nccl_destroy": (C.c_int, [VP]),
+        "rph_net_nparams": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "rph_train_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
+        "rph_train_update": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
+        "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
+        "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
+        "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
+        "rph_payoff": (C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP, C.c_float, VP, VP, VP]),
+        "rph_radix_hist": (C.c_int, [VP, C.c_longlong, C.c_uint32, C.c_uint32, C.c_int, C.c_int, VP, VP]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load(required: bool | None = None):
+    """Load (building if needed) the native library.  ``required`` defaults to
+    True whenever a GPU is visible."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if required is None:
+        required = torch.cuda.is_available()
+    try:
+        if not _LIB_PATH.exists() or os.environ.get("RPH_REBUILD"):
+            from .. import build as _build
+
+            _build.build()
+        lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
+        _bind(lib)
+        cap = 128
+        buf = (C.c_longlong * cap)()
+        n = lib.rph_layout(buf, cap)
+        got = list(buf[:n])
+        exp = _expected_layout()
+        if got != exp:
+            raise RuntimeError(f"native/ctypes layout mismatch:\n native={got}\n python={exp}")
+        _lib = lib
+        return lib
+    except Exception as e:  # pragma: no cover - exercised on broken installs only
+        _load_error = f"{type(e).__name__}: {e}"
+        if required:
+            raise RuntimeError(f"rphedge native library unavailable on a GPU machine: {_load_error}") from e
+        return None
+
+
+def available() -> bool:
+    return load(required=False) is not None
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.rph_last_error().decode() if _lib is not None else ""
+        raise RuntimeError(f"{what} failed with code {rc}: {msg}")
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+# ---------------------------------------------------------------------------
+# thin wrappers
+# ---------------------------------------------------------------------------
+def net_nparams(nin: int, h: int, nout: int, head: int) -> tuple[int, int]:
+    lib = load(required=True)
+    p, r = C.c_int(), C.c_int()
+    if lib.rph_net_nparams(nin, h, nout, head, C.byref(p), C.byref(r)) != 0:
+        raise ValueError(f"unsupported hedge network shape nin={nin} h={h} nout={nout} head={head}")
+    return p.value, r.value
+
+
+def sobol_normal(out: torch.Tensor, table, offset: int = 0, raw: bool = False, stream=None):
+    lib = load(required=True)
+    sv, sh, dims = table
+    n, d = out.shape
+    assert d <= dims
+    fp64 = 1 if out.dtype == torch.float64 else 0
+    _check(lib.rph_sobol_normal(ptr(out), n, d, ptr(sv), ptr(sh), int(offset), fp64, int(raw),
+                                stream_handle(stream)), "rph_sobol_normal")
+
+
+def simulate(desc: SimDesc, stream=None):
+    lib = load(required=True)
+    _check(lib.rph_simulate(C.byref(desc), stream_handle(stream)), "rph_simulate")
+
+
+def train_step(desc: TrainDesc, step: int, stream=None):
+    _check(_lib.rph_train_step(C.byref(desc), int(step), stream_handle(stream)), "rph_train_step")
+
+
+def train_update(desc: TrainDesc, step: int, stream=None):
+    _check(_lib.rph_train_update(C.byref(desc), int(step), stream_handle(stream)), "rph_train_update")
+
+
+def eval_(desc: EvalDesc, stream=None):
+    _check(_lib.rph_eval(C.byref(desc), stream_handle(stream)), "rph_eval")
+
+
+def payoff(kind: int, s: torch.Tensor, out: torch.Tensor, strike: float, nfrac=None, wts=None, na: int = 1,
+           stream=None):
+    lib = load(required=True)
+    n = out.numel()
+    _check(lib.rph_payoff(kind, n, na, ptr(s), ptr(nfrac), float(strike), ptr(wts), ptr(out),
+                          stream_handle(stream)), "rph_payoff")
+
+
+def radix_hist(x: torch.Tensor, pmask: int, prefix: int, shift: int, nbins: int, hist: torch.Tensor, stream=None):
+    lib = load(required=True)
+    _check(lib.rph_radix_hist(ptr(x), x.numel(), pmask & 0xFFFFFFFF, prefix & 0xFFFFFFFF, shift, nbins, ptr(hist),
+                              stream_handle(stream)), "rph_radix_hist")
+
+
+def memset_async(t: torch.Tensor, value: int = 0, stream=None):
+    lib = load(required=True)
+    _check(lib.rph_memset_async(ptr(t), value, t.numel() * t.element_size(), stream_handle(stream)),
+           "rph_memset_async")
+
+
+def device_info(dev: int = 0) -> dict:
+    lib = load(required=True)
+    cus, lds = C.c_int(), C.c_int()
+    hbm = C.c_longlong()
+    name = C.create_string_buffer(128)
+    _check(lib.rph_device_info(dev, C.byref(cus), C.byref(lds), C.byref(hbm), name, 128), "rph_device_info")
+    return {"cus": cus.value, "lds_per_cu": lds.value, "hbm_bytes": hbm.value, "arch": name.value.decode()}
+
+
+class Graph:
+    """hipGraph captured from a stream with the native runtime."""
+
+    def __init__(self):
+        self.exec = None
+        self.num_nodes = 0
+
+    def capture_begin(self, stream=None):
+        lib = load(required=True)
+        self._stream = stream_handle(stream)
+        _check(lib.rph_graph_begin(self._stream), "rph_graph_begin")
+
+    def capture_end(self):
+        ex = VP()
+        nn = C.c_longlong()
+        _check(_lib.rph_graph_end(self._stream, C.byref(ex), C.byref(nn)), "rph_graph_end")
+        self.exec = ex.value
+        self.num_nodes = nn.value
+
+    def replay(self, stream=None):
+        _check(_lib.rph_graph_launch(self.exec, stream_handle(stream)), "rph_graph_launch")
+
+    def __del__(self):
+        if self.exec is not None and _lib is not None:
+            try:
+                _lib.rph_graph_destroy(self.exec)
+            except Exception:
+                pass
+            self.exec = None
+
+
+class NcclComm:
+    """RCCL communicator owned by the native runtime (one per process/GPU).
+
+    The 128-byte unique id is created on rank 0 and broadcast via the
+    torch.distributed store, then every rank calls ``ncclCommInitRank``.
+    """
+
+    def __init__(self, rank: int, world: int, store, tag: str = "rph_nccl"):
+        lib = load(required=True)
+        key = f"{tag}_uid"
+        if rank == 0:
+            buf = C.create_string_buffer(128)
+            n = lib.rph_nccl_unique_id(buf)
+            if n <= 0:
+                _check(-1, "rph_nccl_unique_id")
+            store.set(key, bytes(buf.raw[:128]))
+        uid = store.get(key)
+        comm = VP()
+        _check(lib.rph_nccl_init(uid, world, rank, C.byref(comm)), "rph_nccl_init")
+        self.comm = comm.value
+        self.rank, self.world = rank, world
+
+    def allreduce_(self, t: torch.Tensor, stream=None):
+        fn = {torch.float32: _lib.rph_nccl_allreduce_f32, torch.float64: _lib.rph_nccl_allreduce_f64,
+              torch.int32: _lib.rph_nccl_allreduce_u32}[t.dtype]
+        _check(fn(self.comm, ptr(t), t.numel(), stream_handle(stream)), "rph_nccl_allreduce")
+
+    def close(self):
+        if self.comm is not None:
+            _lib.rph_nccl_destroy(self.comm)
+            self.comm = None

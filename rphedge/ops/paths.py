@@ -1,0 +1,381 @@
+"""Path simulation (K3–K7) on the device, plus a numpy oracle.
+
+Output is a :class:`Paths` object holding ONLY the coarse rebalancing grid,
+time-major ``[n_coarse, n_local]`` float32 (per asset for baskets), normalised
+prices, the deterministic bank account ``B_t`` (C07, RP:67-69) and the
+terminal fine-grid values used for the payoff (RP:88 computes the payoff
+before subsampling).
+
+Reference call sites: fund GBM RP:59-65 (C04), EO log-GBM (C05), SV RP:273-289
+(C06), mortality RP:71-84 (C08, C09), decimation RP:91-97 (C11).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import layout as L
+from .sobol import sobol_table, device_table
+from .ndtri import ndtri_u30_f64, ndtri_u30_f32
+from .philox import philox4x32_10, u01d
+
+SEED_W1 = 1235   # fund / stock shocks (RP:60)
+SEED_W2 = 1234   # mortality shocks (RP:72) — also W_SV in the SV model (Q7)
+
+
+@dataclass
+class Grid:
+    T: float
+    dt: float
+    rebalancing: float
+
+    @property
+    def n_fine(self) -> int:
+        return int(math.ceil(self.T / self.dt) + 1)
+
+    @property
+    def reduction(self) -> int:
+        return max(1, int(math.floor((self.n_fine - 1) / (self.T / self.rebalancing))))
+
+    @property
+    def n_coarse(self) -> int:
+        return int(math.ceil(self.n_fine / self.reduction))
+
+    @property
+    def dt_coarse(self) -> float:
+        return self.dt * self.reduction
+
+    def times(self) -> np.ndarray:
+        return np.arange(self.n_coarse) * self.dt * self.reduction
+
+    def bond(self, r: float, norm: float = 1.0) -> np.ndarray:
+        """B_t = exp(r t) on the fine linspace, subsampled (RP:68, :94)."""
+        fine = np.exp(r * np.linspace(0, self.T, self.n_fine))
+        return (fine[:: self.reduction] / norm).astype(np.float64)
+
+
+@dataclass
+class Paths:
+    kind: str
+    grid: Grid
+    n_local: int
+    path_offset: int
+    S: torch.Tensor                      # [n_coarse, n] or [n_coarse, na, n]
+    bond: np.ndarray                     # [n_coarse]
+    S_final: torch.Tensor                # [n] or [na, n]  terminal fine value
+    vol: torch.Tensor | None = None      # [n_coarse, n] (SV / Heston)
+    nfrac: torch.Tensor | None = None    # [n_coarse, n] N_t/N (pension)
+    lam: torch.Tensor | None = None      # [n_coarse, n]
+    nfrac_final: torch.Tensor | None = None
+    norm: float = 1.0
+    na: int = 1
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_coarse(self) -> int:
+        return self.S.shape[0]
+
+    def asset(self, t: int, a: int = 0) -> torch.Tensor:
+        return self.S[t, a] if self.S.dim() == 3 else self.S[t]
+
+    def prices(self, t: int) -> list:
+        return [self.asset(t, a) for a in range(self.na)]
+
+    def features(self, t: int) -> list:
+        if self.kind == "pension":
+            return [self.S[t], self.nfrac[t], self.lam[t]]
+        if self.kind in ("heston", "sv"):
+            return [self.S[t], self.vol[t]]
+        return self.prices(t)
+
+
+def _dev_is_gpu(device) -> bool:
+    return torch.device(device).type == "cuda"
+
+
+# ---------------------------------------------------------------------------
+# device simulation
+# ---------------------------------------------------------------------------
+def _desc(model, n_local, offset, grid: Grid, fp64, parity):
+    from . import native
+
+    d = native.SimDesc()
+    d.model = model
+    d.n_local = int(n_local)
+    d.path_offset = int(offset)
+    d.n_fine = grid.n_fine
+    d.reduction = grid.reduction
+    d.n_coarse = grid.n_coarse
+    d.na = 1
+    d.fp64 = 1 if fp64 else 0
+    d.parity = 1 if parity else 0
+    d.dt = float(grid.dt)
+    return d
+
+
+def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, scheme: str = "arith",
+                 norm: float = 1.0, device="cuda", offset: int = 0, fp64: bool = False, seed: int = SEED_W1,
+                 stream=None) -> Paths:
+    """Fund/stock GBM on the fine grid, stored on the coarse grid (K1+K2+K3)."""
+    dev = torch.device(device)
+    S = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    fin = torch.empty(n_local, dtype=torch.float32, device=dev)
+    if _dev_is_gpu(dev):
+        from . import native
+
+        sv, sh, dims = device_table(grid.n_fine, seed, dev)
+        d = _desc(L.SIM_GBM_LOG if scheme == "log" else L.SIM_GBM_ARITH, n_local, offset, grid, fp64, False)
+        d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), dims
+        d.s0[0], d.mu[0], d.sigma[0], d.inv_norm[0] = s0, mu, sigma, 1.0 / norm
+        d.out, d.final_out = S.data_ptr(), fin.data_ptr()
+        native.simulate(d, stream)
+    else:
+        s_np, f_np = _cpu_gbm(grid, n_local, s0, mu, sigma, scheme, offset, seed)
+        S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
+        fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
+    return Paths(kind="gbm", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
+                 S_final=fin, norm=norm)
+
+
+def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model: str = "sv_ref",
+                a=0.0, b=0.0, c=0.0, kappa=0.0, theta=0.0, xi=0.0, rho=0.0, norm: float = 1.0,
+                device="cuda", offset: int = 0, fp64: bool = False, parity_nan: bool = False,
+                seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None) -> Paths:
+    """Reference CIR-on-sigma SV (RP:282-289) or full-truncation Heston (K4)."""
+    dev = torch.device(device)
+    S = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    V = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    fin = torch.empty(n_local, dtype=torch.float32, device=dev)
+    mcode = L.SIM_SV_REF if model == "sv_ref" else L.SIM_HESTON
+    if _dev_is_gpu(dev):
+        from . import native
+
+        sv1, sh1, d1 = device_table(grid.n_fine, seed1, dev)
+        sv2, sh2, d2 = device_table(grid.n_fine, seed2, dev)
+        d = _desc(mcode, n_local, offset, grid, fp64, parity_nan)
+        d.sv1, d.shift1, d.dims1 = sv1.data_ptr(), sh1.data_ptr(), d1
+        d.sv2, d.shift2, d.dims2 = sv2.data_ptr(), sh2.data_ptr(), d2
+        d.s0[0], d.mu[0], d.inv_norm[0] = s0, mu, 1.0 / norm
+        d.v0, d.a, d.b, d.c = v0, a, b, c
+        d.kappa, d.theta, d.xi, d.rho = kappa, theta, xi, rho
+        d.out, d.out2, d.final_out = S.data_ptr(), V.data_ptr(), fin.data_ptr()
+        native.simulate(d, stream)
+    else:
+        s_np, v_np, f_np = _cpu_sv(grid, n_local, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset,
+                                   parity_nan, seed1, seed2)
+        S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
+        V.copy_(torch.from_numpy(v_np.astype(np.float32)))
+        fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
+    return Paths(kind="heston" if model == "heston" else "sv", grid=grid, n_local=n_local, path_offset=offset,
+                 S=S, vol=V, bond=grid.bond(0.0), S_final=fin, norm=norm)
+
+
+def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, device="cuda", offset: int = 0,
+                    seed: int = SEED_W1, stream=None) -> Paths:
+    """Correlated log-GBM basket (K3 basket variant)."""
+    na = len(s0)
+    norm = np.asarray(norm if norm is not None else s0, dtype=np.float64)
+    C = np.asarray(corr, dtype=np.float64)
+    chol = np.linalg.cholesky(C)
+    dev = torch.device(device)
+    S = torch.empty(grid.n_coarse, na, n_local, dtype=torch.float32, device=dev)
+    fin = torch.empty(na, n_local, dtype=torch.float32, device=dev)
+    if _dev_is_gpu(dev):
+        from . import native
+
+        sv, sh, dims = device_table(na * grid.n_fine, seed, dev)
+        d = _desc(L.SIM_BASKET, n_local, offset, grid, False, False)
+        d.na = na
+        d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), dims
+        for i in range(na):
+            d.s0[i], d.mu[i], d.sigma[i], d.inv_norm[i] = float(s0[i]), float(mu[i]), float(sigma[i]), 1.0 / norm[i]
+        for i in range(na):
+            for j in range(na):
+                d.chol[i * 8 + j] = float(chol[i, j])
+        d.out, d.final_out = S.data_ptr(), fin.data_ptr()
+        native.simulate(d, stream)
+    else:
+        s_np, f_np = _cpu_basket(grid, n_local, s0, mu, sigma, chol, offset, seed)
+        S.copy_(torch.from_numpy((s_np / norm[None, :, None]).astype(np.float32)))
+        fin.copy_(torch.from_numpy((f_np / norm[:, None]).astype(np.float32)))
+    p = Paths(kind="basket", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
+              S_final=fin, norm=float(norm[0]), na=na)
+    p.meta["norms"] = norm
+    return p
+
+
+def simulate_mortality(paths: Paths, l0: float, c: float, eta: float, n0: int, lambda_fine_index: bool = False,
+                       device=None, fp64: bool = False, seed: int = SEED_W2, philox_seed: int = 1234,
+                       numpy_binomial: bool = False, stream=None) -> Paths:
+    """Mortality intensity + binomial survivors (K5+K6); attaches nfrac/lam to ``paths``."""
+    grid, n_local, offset = paths.grid, paths.n_local, paths.path_offset
+    dev = paths.S.device if device is None else torch.device(device)
+    NF = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    LM = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    NT = torch.empty(n_local, dtype=torch.float32, device=dev)
+    if _dev_is_gpu(dev):
+        from . import native
+
+        sv, sh, dims = device_table(grid.n_fine, seed, dev)
+        d = _desc(L.SIM_MORTALITY, n_local, offset, grid, fp64, lambda_fine_index)
+        d.sv2, d.shift2, d.dims2 = sv.data_ptr(), sh.data_ptr(), dims
+        d.l0, d.lc, d.eta, d.n0, d.seed = l0, c, eta, int(n0), int(philox_seed)
+        d.out2, d.out3, d.final2_out = NF.data_ptr(), LM.data_ptr(), NT.data_ptr()
+        native.simulate(d, stream)
+    else:
+        nf, lm, nt = _cpu_mortality(grid, n_local, l0, c, eta, n0, lambda_fine_index, offset, seed, philox_seed,
+                                    numpy_binomial)
+        NF.copy_(torch.from_numpy(nf.astype(np.float32)))
+        LM.copy_(torch.from_numpy(lm.astype(np.float32)))
+        NT.copy_(torch.from_numpy(nt.astype(np.float32)))
+    paths.kind = "pension"
+    paths.nfrac, paths.lam, paths.nfrac_final = NF, LM, NT
+    return paths
+
+
+def payoff(kind: str, paths: Paths, strike: float, weights=None, stream=None) -> torch.Tensor:
+    """Terminal value V_T in normalised units (K7)."""
+    S = paths.S_final
+    n = paths.n_local
+    out = torch.empty(n, dtype=torch.float32, device=S.device)
+    code = {"guarantee": 0, "call": 1, "put": 2, "basket_call": 3}[kind]
+    if S.is_cuda:
+        from . import native
+
+        w = None
+        if code == 3:
+            w = torch.tensor(np.asarray(weights, np.float32), device=S.device)
+        native.payoff(code, S, out, strike, nfrac=paths.nfrac_final if code == 0 else None, wts=w, na=paths.na,
+                      stream=stream)
+        return out
+    if code == 0:
+        y = S
+        out.copy_(torch.where(y > strike, y, torch.full_like(y, strike)) *
+                  (paths.nfrac_final if paths.nfrac_final is not None else 1.0))
+    elif code == 1:
+        out.copy_((S - strike).clamp_min(0))
+    elif code == 2:
+        out.copy_((strike - S).clamp_min(0))
+    else:
+        w = torch.tensor(np.asarray(weights, np.float32))
+        out.copy_(((S * w[:, None]).sum(0) - strike).clamp_min(0))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# numpy oracles (same Sobol points; fp64 recursion)
+# ---------------------------------------------------------------------------
+def _normals(table_dims, seed, n_local, offset, dims, f32=False):
+    tab = sobol_table(table_dims, seed)
+    x = tab.points_u30(np.arange(offset, offset + n_local, dtype=np.uint64), dims=dims).astype(np.int64)
+    return ndtri_u30_f32(np.maximum(x, 1)).astype(np.float64) if f32 else ndtri_u30_f64(x)
+
+
+def _cpu_gbm(grid, n, s0, mu, sigma, scheme, offset, seed):
+    W = _normals(grid.n_fine, seed, n, offset, grid.n_fine)
+    dt = grid.dt
+    y = np.full(n, math.log(s0) if scheme == "log" else s0, dtype=np.float64)
+    out = np.empty((grid.n_coarse, n))
+    out[0] = s0
+    for t in range(1, grid.n_fine):
+        if scheme == "log":
+            y = y + (mu - 0.5 * sigma ** 2) * dt + sigma * math.sqrt(dt) * W[:, t]
+        else:
+            y = y + y * (mu * dt + sigma * math.sqrt(dt) * W[:, t])
+        if t % grid.reduction == 0 and t // grid.reduction < grid.n_coarse:
+            out[t // grid.reduction] = np.exp(y) if scheme == "log" else y
+    fin = np.exp(y) if scheme == "log" else y
+    return out, fin
+
+
+def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, parity_nan, seed1, seed2):
+    W1 = _normals(grid.n_fine, seed1, n, offset, grid.n_fine)
+    W2 = _normals(grid.n_fine, seed2, n, offset, grid.n_fine)
+    dt = grid.dt
+    ly = np.full(n, math.log(s0))
+    v = np.full(n, float(v0))
+    S = np.empty((grid.n_coarse, n))
+    V = np.empty((grid.n_coarse, n))
+    S[0], V[0] = s0, v0
+    rhoc = math.sqrt(1 - rho * rho)
+    with np.errstate(invalid="ignore"):
+        for t in range(1, grid.n_fine):
+            if model == "sv_ref":
+                arg = v * dt
+                sq = np.sqrt(arg) if parity_nan else np.sqrt(np.maximum(arg, 0.0))
+                v = v + a * (b - v) + c * sq * W2[:, t]
+                ly = ly + (mu - 0.5 * v * v) * dt + v * math.sqrt(dt) * W1[:, t]
+            else:
+                vp = np.maximum(v, 0.0)
+                sv = np.sqrt(vp * dt)
+                ly = ly + (mu - 0.5 * vp) * dt + sv * (rho * W2[:, t] + rhoc * W1[:, t])
+                v = v + kappa * (theta - vp) * dt + xi * sv * W2[:, t]
+            if t % grid.reduction == 0 and t // grid.reduction < grid.n_coarse:
+                S[t // grid.reduction] = np.exp(ly)
+                V[t // grid.reduction] = v
+    return S, V, np.exp(ly)
+
+
+def _cpu_basket(grid, n, s0, mu, sigma, chol, offset, seed):
+    na = len(s0)
+    dims = na * grid.n_fine
+    tab = sobol_table(dims, seed)
+    idx = np.arange(offset, offset + n, dtype=np.uint64)
+    x = tab.points_u30(idx, dims=dims).astype(np.int64)
+    Wall = ndtri_u30_f64(np.maximum(x, 1))
+    dt = grid.dt
+    ly = np.log(np.asarray(s0, dtype=np.float64))[:, None].repeat(n, 1)
+    out = np.empty((grid.n_coarse, na, n))
+    out[0] = np.asarray(s0)[:, None]
+    mu, sigma = np.asarray(mu), np.asarray(sigma)
+    for t in range(1, grid.n_fine):
+        w = np.stack([Wall[:, a * grid.n_fine + t] for a in range(na)])
+        z = chol @ w
+        ly = ly + ((mu - 0.5 * sigma ** 2) * dt)[:, None] + (sigma * math.sqrt(dt))[:, None] * z
+        if t % grid.reduction == 0 and t // grid.reduction < grid.n_coarse:
+            out[t // grid.reduction] = np.exp(ly)
+    return out, np.exp(ly)
+
+
+def _cpu_mortality(grid, n, l0, c, eta, n0, q3, offset, seed, philox_seed, numpy_binomial):
+    W2 = _normals(grid.n_fine, seed, n, offset, grid.n_fine)
+    dt = grid.dt
+    lam = np.full(n, float(l0))
+    N = np.full(n, int(n0), dtype=np.int64)
+    NF = np.empty((grid.n_coarse, n))
+    LM = np.empty((grid.n_coarse, n))
+    NF[0], LM[0] = 1.0, l0
+    gidx = np.arange(offset, offset + n, dtype=np.uint64)
+    for t in range(1, grid.n_fine):
+        lam = lam + (c * lam * dt + eta * math.sqrt(dt) * W2[:, t])
+        p = np.exp(-lam * dt)
+        if numpy_binomial:  # Q20: reference draw (MT19937 reseeded each fine step)
+            np.random.seed(1234 + t)
+            N = np.random.binomial(N, np.clip(p, 0, 1))
+        else:
+            q = np.clip(1.0 - p, 0.0, 1.0)
+            r = philox4x32_10((gidx & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+                              (gidx >> np.uint64(32)).astype(np.uint32), np.uint32(t), np.uint32(0xB1A0),
+                              philox_seed, 0x1234)
+            u = u01d(r[0], r[1])
+            D = np.zeros(n, dtype=np.int64)
+            f = np.exp(N * np.log1p(-np.minimum(q, 1 - 1e-16)))
+            F = f.copy()
+            ratio = q / np.maximum(1.0 - q, 1e-300)
+            active = (u > F) & (N > 0) & (q > 0)
+            while active.any():
+                f = np.where(active, f * (N - D) / (D + 1) * ratio, f)
+                D = np.where(active, D + 1, D)
+                F = np.where(active, F + f, F)
+                active = active & (u > F) & (D < N)
+            N = N - D
+        if q3 and t < grid.n_coarse:
+            LM[t] = lam
+        if t % grid.reduction == 0 and t // grid.reduction < grid.n_coarse:
+            NF[t // grid.reduction] = N / n0
+            if not q3:
+                LM[t // grid.reduction] = lam
+    return NF, LM, N / n0

@@ -1,0 +1,147 @@
+"""CPU tests: host twins of the device math, config/API plumbing, CPU engine."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+
+def test_philox_known_answer():
+    from rphedge.ops.philox import philox4x32_10
+
+    r = philox4x32_10(0, 0, 0, 0, 0, 0)
+    assert [int(v) for v in r] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    m = 0xFFFFFFFF
+    r = philox4x32_10(m, m, m, m, m, m)
+    assert [int(v) for v in r] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+@pytest.mark.parametrize("n", [1, 7, 64, 100, 4096])
+def test_chunk_perm_is_bijection(n):
+    from rphedge.ops.philox import ChunkPerm
+
+    p = ChunkPerm(n, seed=11, epoch=3)
+    y = p(np.arange(n))
+    assert sorted(y.tolist()) == list(range(n))
+
+
+def test_epoch_order_chunks():
+    from rphedge.ops.philox import epoch_order
+
+    o = epoch_order(4096, 6, 5, 0)
+    assert sorted(o.tolist()) == list(range(4096))
+    # chunks of 64 stay contiguous
+    assert np.all(np.diff(o.reshape(-1, 64), axis=1) == 1)
+
+
+def test_ndtri_twins_vs_scipy():
+    from scipy.special import ndtri
+
+    from rphedge.ops.ndtri import ndtri_u30_f32, ndtri_u30_f64
+
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.integers(1, 2 ** 30, 50000), np.arange(1, 500), 2 ** 30 - np.arange(1, 500)])
+    ref = ndtri(x * 2.0 ** -30)
+    np.testing.assert_allclose(ndtri_u30_f64(x), ref, rtol=1e-12, atol=1e-13)
+    core = np.abs(ref) < 5
+    np.testing.assert_allclose(ndtri_u30_f32(x)[core], ref[core], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("d,m,seed", [(5, 8, 1235), (40, 10, 1234)])
+def test_sobol_cpu_bit_exact(d, m, seed):
+    from scipy.stats import qmc
+
+    from rphedge.ops.sobol import sobol_uniform_cpu
+
+    ref = qmc.Sobol(d, scramble=True, seed=seed).random_base2(m)
+    assert np.array_equal(sobol_uniform_cpu(m, d, seed), ref)
+
+
+def test_sobol_norm_api_cpu():
+    from scipy.stats import norm, qmc
+
+    from rphedge import sobol_norm
+
+    z = sobol_norm(6, 3, 1235, device="cpu").numpy()
+    ref = norm.ppf(qmc.Sobol(3, scramble=True, seed=1235).random_base2(6))
+    np.testing.assert_allclose(z, ref, rtol=1e-12, atol=1e-13)
+
+
+def test_native_layout_loads_without_gpu():
+    from rphedge.ops import native
+
+    lib = native.load(required=False)
+    assert lib is not None
+    assert native.net_nparams(3, 8, 2, 0) == (122, 128)
+    assert native.net_nparams(1, 8, 1, 1) == (97, 128)
+
+
+def test_param_counts_match_reference():
+    from rphedge.models import EUROPEAN_REF, PENSION
+
+    assert PENSION.nparams == 122       # "Multi Time Step.ipynb":617
+    assert EUROPEAN_REF.nparams == 97   # "European Options.ipynb":451
+
+
+def test_grid_matches_reference():
+    from rphedge.ops.paths import Grid
+
+    g = Grid(10.0, 1 / 100, 0.25)
+    assert (g.n_fine, g.reduction, g.n_coarse) == (1001, 25, 41)
+    g = Grid(10.0, 1 / 365, 0.25)
+    assert (g.n_fine, g.reduction, g.n_coarse) == (3651, 91, 41)
+    g = Grid(1.0, 1 / 365, 1 / 52)
+    assert (g.n_fine, g.reduction, g.n_coarse) == (366, 7, 53)
+
+
+def test_parse_params_keys():
+    from rphedge.config import parse_params
+
+    base = dict(Y=1, K=1, T=10, mu=0.09464, r=0.03, sigma=0.15965, rebalancing=0.25, N=10000, P=100, x=55,
+                l0=0.01, c=0.075, ita=0.000597, dt=1 / 100, n_paths=12)
+    cfg = parse_params(base)
+    assert cfg.paths == 4096 and cfg.n_coarse == 41
+    with pytest.raises(KeyError):
+        parse_params({k: v for k, v in base.items() if k != "ita"})
+    with pytest.raises(KeyError):
+        parse_params(dict(base, bogus=1))
+    sv = dict(base)
+    sv.pop("sigma")
+    sv.update(s0=0.15965, a=0.0033566, b=0.15431)
+    cfg = parse_params(dict(sv, parity=True), sv=True)
+    assert cfg.sv_c == 0.075 and cfg.model == "sv_ref"   # Q4
+
+
+def test_gbm_cpu_moments():
+    from rphedge.ops import paths as P
+
+    g = P.Grid(10.0, 1 / 100, 0.25)
+    p = P.simulate_gbm(g, 4096, 1.0, 0.09464, 0.15965, device="cpu")
+    # MTS sanity check: mean Y_T ~ e^{mu T}
+    assert abs(float(p.S_final.double().mean()) - math.exp(0.9464)) < 0.03
+
+
+def test_black_scholes_reference_numbers():
+    from rphedge.utils.reports import black_scholes
+
+    price, delta = black_scholes(100, 100, 0.08, 0.15, 1.0)
+    assert price == pytest.approx(10.3896, abs=1e-3)
+    assert delta == pytest.approx(0.7285, abs=1e-3)
+
+
+def test_cpu_quantile_exact():
+    from rphedge import risk
+
+    x = torch.randn(5001, generator=torch.Generator().manual_seed(3))
+    qs = (0.0, 0.1, 0.5, 0.985, 1.0)
+    np.testing.assert_allclose(risk.quantile(x, qs), np.quantile(x.double().numpy(), qs), rtol=1e-6, atol=1e-7)
+
+
+def test_european_cpu_end_to_end():
+    import rphedge
+
+    res = rphedge.european_option(N_paths=4096, rebalancing_frequency=1 / 12, epochs_first=60, epochs_rest=15,
+                                  verbose=False, batch_size=512)
+    assert abs(res.v0 - 10.39) < 0.6
+    assert abs(res.phi - 0.7285) < 0.08
+    assert res.terminal_pnl["std"] < 3.5

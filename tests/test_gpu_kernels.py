@@ -1,0 +1,263 @@
+"""GPU numerics: every HIP kernel vs a plain fp32/fp64 PyTorch/numpy reference."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from rphedge.ops import native
+
+    native.load(required=True)
+    return torch.device("cuda", 0)
+
+
+def test_native_is_loaded(dev):
+    from rphedge.ops import native
+
+    assert native._lib is not None
+    info = native.device_info(0)
+    assert info["cus"] > 0
+    assert info["arch"].startswith("gfx9")
+
+
+@pytest.mark.parametrize("d,m,seed", [(7, 10, 1235), (31, 12, 1234), (3, 8, 42)])
+def test_sobol_fp64_matches_scipy(dev, d, m, seed):
+    from scipy.stats import norm, qmc
+
+    from rphedge.ops.sobol import sobol_norm
+
+    ref = norm.ppf(qmc.Sobol(d, scramble=True, seed=seed).random_base2(m))
+    got = sobol_norm(m, d, seed, device=dev, dtype=torch.float64).cpu().numpy()
+    fin = np.isfinite(ref)
+    assert np.array_equal(fin, np.isfinite(got))
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-12, atol=1e-13)
+
+
+def test_sobol_raw_bit_exact(dev):
+    from scipy.stats import qmc
+
+    from rphedge.ops import native
+    from rphedge.ops.sobol import device_table
+
+    d, m, seed = 9, 11, 1235
+    ref = qmc.Sobol(d, scramble=True, seed=seed).random_base2(m)
+    out = torch.empty(2 ** m, d, dtype=torch.float64, device=dev)
+    native.sobol_normal(out, device_table(d, seed, dev), raw=True)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_sobol_fp32_accuracy(dev):
+    from scipy.stats import norm, qmc
+
+    from rphedge.ops.sobol import sobol_norm
+
+    d, m = 5, 14
+    ref = norm.ppf(qmc.Sobol(d, scramble=True, seed=1235).random_base2(m))
+    got = sobol_norm(m, d, 1235, device=dev, dtype=torch.float32).cpu().numpy().astype(np.float64)
+    core = np.abs(ref) < 5
+    np.testing.assert_allclose(got[core], ref[core], rtol=2e-6, atol=2e-6)
+    assert np.max(np.abs(got[~core & np.isfinite(ref)] - ref[~core & np.isfinite(ref)]), initial=0) < 1e-3
+
+
+@pytest.mark.parametrize("scheme", ["arith", "log"])
+def test_gbm_paths_vs_numpy(dev, scheme):
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=1.0, dt=1 / 100, rebalancing=1 / 20)
+    n = 4096
+    gp = P.simulate_gbm(g, n, 1.0, 0.08, 0.15, scheme=scheme, device=dev, fp64=True)
+    cp = P.simulate_gbm(g, n, 1.0, 0.08, 0.15, scheme=scheme, device="cpu")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(gp.S.cpu().numpy(), cp.S.numpy(), rtol=2e-6)
+    np.testing.assert_allclose(gp.S_final.cpu().numpy(), cp.S_final.numpy(), rtol=2e-6)
+    g32 = P.simulate_gbm(g, n, 1.0, 0.08, 0.15, scheme=scheme, device=dev, fp64=False)
+    np.testing.assert_allclose(g32.S.cpu().numpy(), cp.S.numpy(), rtol=5e-5)
+
+
+def test_gbm_offset_shard_consistency(dev):
+    """Sharded generation (DP) reproduces the same global path set."""
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=1.0, dt=1 / 30, rebalancing=1 / 30)
+    full = P.simulate_gbm(g, 8192, 100.0, 0.08, 0.15, scheme="log", norm=100.0, device=dev)
+    a = P.simulate_gbm(g, 4096, 100.0, 0.08, 0.15, scheme="log", norm=100.0, device=dev, offset=0)
+    b = P.simulate_gbm(g, 4096, 100.0, 0.08, 0.15, scheme="log", norm=100.0, device=dev, offset=4096)
+    torch.testing.assert_close(torch.cat([a.S, b.S], 1), full.S)
+
+
+def test_gbm_moments(dev):
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=1.0, dt=1 / 30, rebalancing=1 / 30)
+    p = P.simulate_gbm(g, 1 << 20, 100.0, 0.08, 0.15, scheme="log", norm=100.0, device=dev)
+    m = float(p.S_final.double().mean()) * 100
+    assert abs(m - 100 * math.exp(0.08)) < 0.02
+
+
+def test_sv_and_heston_vs_numpy(dev):
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=2.0, dt=1 / 50, rebalancing=0.25)
+    for model, kw in [("sv_ref", dict(a=0.0034, b=0.154, c=0.0158)),
+                      ("heston", dict(kappa=2.0, theta=0.04, xi=0.3, rho=-0.7))]:
+        gp = P.simulate_sv(g, 2048, 1.0, 0.09, 0.16 if model == "sv_ref" else 0.04, model=model, device=dev,
+                           fp64=True, **kw)
+        cp = P.simulate_sv(g, 2048, 1.0, 0.09, 0.16 if model == "sv_ref" else 0.04, model=model, device="cpu",
+                           **kw)
+        np.testing.assert_allclose(gp.S.cpu().numpy(), cp.S.numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(gp.vol.cpu().numpy(), cp.vol.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_basket_vs_numpy(dev):
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=1.0, dt=1 / 20, rebalancing=1 / 10)
+    na = 5
+    corr = np.full((na, na), 0.5) + np.eye(na) * 0.5
+    gp = P.simulate_basket(g, 2048, [100.0] * na, [0.05] * na, [0.2] * na, corr, device=dev)
+    cp = P.simulate_basket(g, 2048, [100.0] * na, [0.05] * na, [0.2] * na, corr, device="cpu")
+    np.testing.assert_allclose(gp.S.cpu().numpy(), cp.S.numpy(), rtol=2e-4)
+
+
+def test_mortality_statistics(dev):
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=10.0, dt=1 / 100, rebalancing=0.25)
+    p = P.simulate_gbm(g, 8192, 1.0, 0.08, 0.15, device=dev)
+    P.simulate_mortality(p, 0.01, 0.075, 0.000597, 10000)
+    cp = P.simulate_gbm(g, 2048, 1.0, 0.08, 0.15, device="cpu")
+    P.simulate_mortality(cp, 0.01, 0.075, 0.000597, 10000)
+    # lambda is deterministic given the Sobol draws
+    np.testing.assert_allclose(p.lam[:, :2048].cpu().numpy(), cp.lam.numpy(), rtol=1e-5)
+    nT = p.nfrac_final.double().cpu().numpy() * 10000
+    # SURVEY: E[N_T] = 8615-8617, std 132-133
+    assert abs(nT.mean() - 8616) < 15
+    assert 110 < nT.std() < 160
+
+
+def _fit_pair(dev, spec, n, batch, epochs, loss, chunk_log2=0, lr=1e-2):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import init_weights
+    from rphedge.ops import layout as L
+
+    g = torch.Generator().manual_seed(0)
+    feats = [torch.rand(n, generator=g) * 0.5 + 0.75 for _ in range(spec.nin)]
+    prices = [f.clone() * (1 + 0.05 * torch.randn(n, generator=g)) for f in feats[: spec.nhold - 1]]
+    target = torch.relu(prices[0] - 1.0) if spec.nhold > 1 else torch.rand(n)
+    w0 = init_weights(spec, ([0.5] + [-0.4] * (spec.nout - 1)) if spec.head == 0 else [0.1])
+    tc = TrainConfig(batch_size=batch, chunk_log2=chunk_log2, lr=lr)
+    fc = FitConfig(epochs=epochs, patience=1000, loss=loss, early_stopping=False)
+    out = []
+    for be_cls, d in ((TorchBackend, torch.device("cpu")), (HipBackend, dev)):
+        be = be_cls(spec, n, tc, device=d)
+        data = DateData(feats=[f.to(d) for f in feats], prices_next=[p.to(d) for p in prices], bond_next=1.02,
+                        target=target.to(d), prices_now=[f.to(d) for f in feats[: spec.nhold - 1]], bond_now=1.0)
+        w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, fc, seed=7)
+        st = be.new_stats()
+        vo = torch.empty(n, device=d)
+        ro = torch.empty(n, device=d)
+        be.eval(w, data, st, v_out=vo, resid_out=ro)
+        if d.type == "cuda":
+            torch.cuda.synchronize()
+        out.append((current_weights(spec, w), o.cpu().numpy(), f.cpu().numpy(), vo.cpu().numpy(), ro.cpu().numpy(),
+                    st.sum(0).cpu().numpy()))
+    return out
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (5, 8, 6, 0)])
+def test_train_step_matches_torch(dev, shape):
+    """Fused HIP training (fwd+bwd+reduce+Adam, several steps) vs torch autograd + Keras-Adam."""
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    nin, h, nout, head = shape
+    spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE)
+    np.testing.assert_allclose(wg, wc, rtol=2e-3, atol=2e-4)
+    assert og[L.O_T] == oc[L.O_T] == 16
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
+    np.testing.assert_allclose(vg, vc, rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(rg, rc, rtol=1e-3, atol=1e-4)
+
+
+def test_train_pinball_multi_wg(dev):
+    """Large batch -> many workgroups + last-arriver slab reduction; pinball loss; 64-path chunk shuffle."""
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=3, hidden=8, nout=2, head=0)
+    (wc, oc, fc, *_), (wg, og, fg, *_) = _fit_pair(dev, spec, 1 << 17, 1 << 16, 3, L.LOSS_PINBALL, chunk_log2=6)
+    np.testing.assert_allclose(wg, wc, rtol=2e-3, atol=2e-4)
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 3], fc[L.F_HIST:L.F_HIST + 3], rtol=1e-3)
+
+
+def test_early_stopping_device_matches_torch(dev):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    n = 2048
+    x = torch.linspace(0.7, 1.3, n)
+    data_c = DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=torch.relu(x - 1), prices_now=[x])
+    data_g = DateData(feats=[x.to(dev)], prices_next=[(x * 1.01).to(dev)], bond_next=1.0,
+                      target=torch.relu(x - 1).to(dev), prices_now=[x.to(dev)])
+    fc = FitConfig(epochs=40, patience=3, loss=L.LOSS_MSE, lr_schedule=tuple([0.05] * 40))
+    res = []
+    for be, dd in ((TorchBackend(spec, n, TrainConfig(batch_size=512), device="cpu"), data_c),
+                   (HipBackend(spec, n, TrainConfig(batch_size=512), device=dev), data_g)):
+        w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, dd, fc, seed=3)
+        res.append((int(f[L.F_EPOCH].item()), current_weights(spec, w)))
+    assert res[0][0] == res[1][0]
+    np.testing.assert_allclose(res[1][1], res[0][1], rtol=5e-3, atol=5e-4)
+
+
+def test_radix_quantile_matches_numpy(dev):
+    from rphedge import risk
+
+    x = torch.randn(100_003, generator=torch.Generator().manual_seed(1)) ** 3
+    qs = (0.0, 0.01, 0.5, 0.98, 0.99, 0.995, 1.0)
+    got = risk.quantile(x.to(dev), qs)
+    ref = np.quantile(x.numpy().astype(np.float64), qs)
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_graph_replay_equals_eager(dev):
+    from rphedge.config import ParityFlags, RunConfig, TrainingParams
+    from rphedge.api import HedgeRun
+
+    tr = TrainingParams(batch_size=4096, epochs_first=4, epochs_rest=2, early_stopping=False, q99=False,
+                        lr_schedule_first=False, chunk_log2=6)
+    cfg = RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=0.1, dt=0.1, n_paths=14,
+                    payoff="call", option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0,
+                    keep_paths=False, verbose=False, train=tr, parity=ParityFlags())
+    run = HedgeRun(cfg)
+    run.build()
+    r_eager = run.run()
+    run.capture(include_simulation=True)
+    run.replay()
+    r_graph = run.collect()
+    assert r_graph.v0 == pytest.approx(r_eager.v0, rel=1e-6)
+    assert r_graph.terminal_pnl["std"] == pytest.approx(r_eager.terminal_pnl["std"], rel=1e-6)
+
+
+def test_european_converges_to_black_scholes(dev):
+    """Integration: corrected replication at 2^18 paths lands near BS 10.3896."""
+    from rphedge.config import ParityFlags, RunConfig, TrainingParams
+    from rphedge.api import HedgeRun
+
+    tr = TrainingParams(batch_size=1 << 14, epochs_first=60, epochs_rest=15, early_stopping=False, q99=False,
+                        lr_schedule_first=False, chunk_log2=6, lr=5e-3)
+    cfg = RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1 / 12, dt=1 / 12,
+                    n_paths=18, payoff="call", option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0,
+                    keep_paths=True, verbose=False, train=tr, parity=ParityFlags())
+    res = HedgeRun(cfg).run()
+    assert abs(res.v0 - 10.3896) < 0.35
+    assert abs(res.phi - 0.7285) < 0.06
