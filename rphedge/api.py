@@ -246,21 +246,28 @@ class HedgeRun:
         if self.backend_kind != "hip":
             raise RuntimeError("graph capture needs the hip backend")
         assert self.cfg.train.poll_every == 0, "graph capture requires fully asynchronous early stopping"
-        s = self.stream or torch.cuda.current_stream(self.device)
-        # one eager pass first: populates every cached device constant (fit
-        # templates, LR tables, Sobol tables) so the capture allocates nothing
-        if include_simulation:
-            self._enqueue_sim_into_existing()
-        self.enqueue()
-        torch.cuda.synchronize(self.device)
+        # Capture must run on a non-default stream; torch ops inside enqueue()
+        # follow torch's current stream, so make the side stream current.
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
         g = Graph()
-        g.capture_begin(s)
-        try:
+        timer_on, self.timer.enabled = self.timer.enabled, False  # no event records inside capture
+        with torch.cuda.stream(s):
+            # one eager pass first: populates every cached device constant (fit
+            # templates, LR tables, Sobol tables) so the capture allocates nothing
             if include_simulation:
                 self._enqueue_sim_into_existing()
             self.enqueue()
-        finally:
-            g.capture_end()
+            s.synchronize()
+            g.capture_begin(s)
+            try:
+                if include_simulation:
+                    self._enqueue_sim_into_existing()
+                self.enqueue()
+            finally:
+                g.capture_end()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.timer.enabled = timer_on
         self.graph = g
         return g
 
