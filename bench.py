@@ -49,6 +49,7 @@ def parse(argv=None):
     ap.add_argument("--batch-log2", type=int, default=16, help="per-GPU minibatch (global = N x this)")
     ap.add_argument("--lr", type=float, default=1e-2)
     ap.add_argument("--lr-rest", type=float, default=2e-3)
+    ap.add_argument("--lr-decay", type=float, default=1.0, help="per-date geometric LR decay factor (last/first epoch)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -89,8 +90,13 @@ def main(argv=None):
     gpu = run.device.type == "cuda"
     # lr schedule: first date a.lr, later dates a.lr_rest (constant per date; see FitConfig)
     run.build()
-    sched_first = tuple([a.lr] * a.epochs_first)
-    sched_rest = tuple([a.lr_rest] * a.epochs_rest)
+    def sched(lr0, n):
+        if n <= 1 or a.lr_decay == 1.0:
+            return tuple([lr0] * n)
+        return tuple(lr0 * a.lr_decay ** (e / (n - 1)) for e in range(n))
+
+    sched_first = sched(a.lr, a.epochs_first)
+    sched_rest = sched(a.lr_rest, a.epochs_rest)
     ind = run.induction
     orig = ind._fcfg
 

@@ -126,8 +126,10 @@ RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], 
 
 // ---------------------------------------------------------------------------
 // Adam + EarlyStopping + LR schedule (K10).  Runs in ONE workgroup of 256
-// threads; gsum (LDS or global) holds the summed gradient [P] followed by the
-// 4 loss statistics.  Keras 2.x semantics:
+// threads, weights updated IN PLACE (every other workgroup of the launch has
+// already passed the arrival ticket, i.e. finished reading them).  gsum (LDS)
+// holds the summed gradient [P] followed by the 4 loss statistics.
+// Keras 2.x semantics:
 //   lr_t = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 //   w -= lr_t*m/(sqrt(v)+eps)
 // EarlyStopping.on_epoch_end: wait+=1; if loss<best: best=loss, save, wait=0;
@@ -135,42 +137,38 @@ RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], 
 // ---------------------------------------------------------------------------
 template <int P>
 RPH_INLINE void apply_update(const float* gsum, NetWeights* wts, OptState* opt, FitState* fs,
-                             const float* lr_sched, int step, int steps_per_epoch, float* lds_scratch) {
+                             const float* lr_sched, int step, int steps_per_epoch) {
+  __shared__ int s_act;
   const int tid = threadIdx.x;
-  const int cur = (int)wts->cur;
-  const int nxt = cur ^ 1;
-  // Epoch-begin LR schedule (Keras LearningRateScheduler.on_epoch_begin).
-  if (tid == 0) {
-    int ok = 1;
-    for (int i = 0; i < P; ++i) ok &= (int)__builtin_isfinite(gsum[i]);
-    lds_scratch[0] = (float)ok;
-    if (step == 0 && lr_sched != nullptr) {
-      const float l = lr_sched[(int)fs->epoch];
-      if (l == l) opt->lr = l;  // NaN => keep current
-    }
+  const bool mine = tid < P;
+  const float g = mine ? gsum[tid] : 0.f;
+  // uniform scalars (read by every thread before thread 0 rewrites them below)
+  float lr = opt->lr;
+  if (step == 0 && lr_sched != nullptr) {  // Keras LearningRateScheduler.on_epoch_begin
+    const float l = lr_sched[(int)fs->epoch];
+    if (l == l) lr = l;                    // NaN => keep current
   }
-  __syncthreads();
-  const bool finite = lds_scratch[0] != 0.f;
-  const float t = opt->t + (finite ? 1.f : 0.f);
-  const float b1 = opt->beta1, b2 = opt->beta2, eps = opt->eps, lr = opt->lr;
+  const float t0 = opt->t;
+  const float b1 = opt->beta1, b2 = opt->beta2, eps = opt->eps;
+  const int finite = __syncthreads_and(mine ? (int)__builtin_isfinite(g) : 1);  // NaN/Inf guard
+  const float t = t0 + (finite ? 1.f : 0.f);
   const float lr_t = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
-  for (int i = tid; i < P; i += blockDim.x) {
-    float w = wts->w[cur][i];
+  float wnew = 0.f;
+  if (mine) {
+    wnew = wts->w[0][tid];
     if (finite) {
-      const float g = gsum[i];
-      float m = opt->m[i], v = opt->v[i];
+      float m = opt->m[tid], v = opt->v[tid];
       m = m + (g - m) * (1.f - b1);
       v = v + (g * g - v) * (1.f - b2);
-      opt->m[i] = m;
-      opt->v[i] = v;
-      w = w - lr_t * m / (sqrtf(v) + eps);
+      opt->m[tid] = m;
+      opt->v[tid] = v;
+      wnew = wnew - lr_t * m / (sqrtf(v) + eps);
+      wts->w[0][tid] = wnew;
     }
-    wts->w[nxt][i] = w;
   }
   __syncthreads();
-  // Epoch bookkeeping: thread 0 decides, all threads copy.
-  __shared__ int s_act;  // 0 none, 1 save best, 2 restore best
-  if (tid == 0) {
+  if (tid == 0) {  // epoch bookkeeping (thread 0 decides)
+    opt->lr = lr;
     if (finite) opt->t = t;
     else opt->nan_steps += 1.f;
     fs->loss_sum += gsum[P + 0];
@@ -208,14 +206,19 @@ RPH_INLINE void apply_update(const float* gsum, NetWeights* wts, OptState* opt, 
   }
   __syncthreads();
   const int act = s_act;
-  if (act == 1) {
-    for (int i = tid; i < P; i += blockDim.x) fs->w_best[i] = wts->w[nxt][i];
-  } else if (act == 2) {
-    for (int i = tid; i < P; i += blockDim.x) wts->w[nxt][i] = fs->w_best[i];
+  if (mine) {
+    if (act == 1) fs->w_best[tid] = wnew;
+    else if (act == 2) wts->w[0][tid] = fs->w_best[tid];
   }
-  __syncthreads();
-  if (tid == 0) wts->cur = (float)nxt;
 }
+
+// agent-scope (sc1) 4-byte accesses for the cross-workgroup hand-off
+RPH_INLINE void st_agent(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+RPH_INLINE float ld_agent(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contention / 8)
 
 // ---------------------------------------------------------------------------
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
@@ -227,18 +230,17 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   constexpr int P = S::P;
   constexpr int NHOLD = S::NHOLD;
   __shared__ __attribute__((aligned(16))) float lds[(4 * R > 1024 ? 4 * R : 1024) + 8];
+  __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ int s_last;
 
-  __shared__ __attribute__((aligned(16))) float wl[P + 4];
-
-  if (d.fit->stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
-  const int cur = (int)d.wts->cur;
+  // prologue: independent loads (early-stop flag, epoch, weights) in flight together
+  const float stopped = d.fit->stopped;
+  const int epoch = (int)d.fit->epoch;
+  const float wv = threadIdx.x < P ? d.wts->w[0][threadIdx.x] : 0.f;
+  if (stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
   // Weights are wave-uniform: stage them once in LDS and read them as
   // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
-  for (int i = threadIdx.x; i < P; i += 256) wl[i] = d.wts->w[cur][i];
-  __syncthreads();
-  const float* __restrict__ W = wl;
-  const int epoch = (int)d.fit->epoch;
+  if (threadIdx.x < P) wl[threadIdx.x] = wv;
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -248,6 +250,8 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   const uint32_t n_chunks = (uint32_t)((d.n_local + (1 << d.chunk_log2) - 1) >> d.chunk_log2);
   const Perm perm = make_perm(n_chunks, d.seed, (uint32_t)epoch, d.shuffle != 0);
   const uint32_t cmask = (1u << d.chunk_log2) - 1u;
+  __syncthreads();
+  const float* __restrict__ W = wl;
 
   float g[R];
 #pragma unroll
@@ -347,57 +351,61 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   float val = 0.f;
   if (threadIdx.x < R) val = lds[threadIdx.x] + lds[R + threadIdx.x] + lds[2 * R + threadIdx.x] + lds[3 * R + threadIdx.x];
   __syncthreads();
-  if (threadIdx.x < R) red[threadIdx.x] = val;
 
   if (gridDim.x > 1) {
-    // ---- publish partial, draw arrival ticket (Guideline 16 counter form) ----
-    if (threadIdx.x < R) d.slab[(size_t)blockIdx.x * R + threadIdx.x] = val;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- publish the partial write-through (sc1) / float-atomically, then draw
+    // the arrival ticket.  No release/acquire fences: every handed-off byte is
+    // stored sc1 (or added at the memory side) and every load of it by the last
+    // arriver is an sc1 load (MI355X_MICROARCH visibility table, row 1).
+    const int G = gridDim.x;
+    if (threadIdx.x < R) {
+      if (d.deterministic) st_agent(d.slab + (size_t)blockIdx.x * R + threadIdx.x, val);
+      else __hip_atomic_fetch_add(d.acc + (blockIdx.x % ACC_REPLICAS) * R + threadIdx.x, val, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t ticket = __hip_atomic_fetch_add(d.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = (ticket == gridDim.x - 1) ? 1 : 0;
+      s_last = (ticket == (uint32_t)G - 1u) ? 1 : 0;
     }
     __syncthreads();
     if (!s_last) return;
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    // ---- last arriver: deterministic slab sum (fixed row partition/order) ----
-    constexpr int Q = R / 4;                 // float4 columns
-    constexpr int GROUPS = 256 / Q;          // row groups
-    const int col = threadIdx.x % Q;
-    const int grp = threadIdx.x / Q;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* slab4 = reinterpret_cast<const float4*>(d.slab);
-    const int G = gridDim.x;
+    if (d.deterministic) {
+      // fixed row partition + fixed combine order => bitwise reproducible
+      constexpr int GROUPS = 256 / R;
+      const int col = threadIdx.x % R;
+      const int grp = threadIdx.x / R;
+      float a = 0.f;
 #pragma unroll 8
-    for (int r = grp; r < G; r += GROUPS) {
-      const float4 v = slab4[(size_t)r * Q + col];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      for (int r = grp; r < G; r += GROUPS) a += ld_agent(d.slab + (size_t)r * R + col);
+      lds[grp * R + col] = a;
+      __syncthreads();
+      if (threadIdx.x < R) {
+        float s2 = 0.f;
+        for (int gi = 0; gi < GROUPS; ++gi) s2 += lds[gi * R + threadIdx.x];
+        val = s2;
+      }
+      __syncthreads();
+    } else {
+      if (threadIdx.x < R) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int rp = 0; rp < ACC_REPLICAS; ++rp) {
+          float* a = d.acc + rp * R + threadIdx.x;
+          s2 += ld_agent(a);
+          st_agent(a, 0.f);  // re-arm for the next step
+        }
+        val = s2;
+      }
     }
-    __syncthreads();
-    reinterpret_cast<float4*>(lds)[grp * Q + col] = acc;
-    __syncthreads();
-    if (threadIdx.x < R) {
-      float s = 0.f;
-      for (int gi = 0; gi < GROUPS; ++gi) s += lds[gi * R + threadIdx.x];
-      val = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < R) red[threadIdx.x] = val;
-    if (threadIdx.x == 0) *d.counter = 0u;  // next launch starts from zero
-    __syncthreads();
-  } else {
-    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (threadIdx.x < R) red[threadIdx.x] = val;
+  __syncthreads();
 
   if (d.fused_update) {
-    apply_update<P>(red, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch, lds + R);
+    apply_update<P>(red, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch);
   } else if (threadIdx.x < R) {
     d.grad_out[threadIdx.x] = red[threadIdx.x];
   }
@@ -411,7 +419,7 @@ __global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const i
   if (d.fit->stopped != 0.f) return;
   for (int i = threadIdx.x; i < S::R; i += blockDim.x) gs[i] = d.grad_out[i];
   __syncthreads();
-  apply_update<S::P>(gs, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch, gs + S::R);
+  apply_update<S::P>(gs, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch);
 }
 
 // ---------------------------------------------------------------------------
@@ -429,8 +437,8 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   __shared__ __attribute__((aligned(16))) float wl[2 * S::P + 8];
   const bool has_b = d.wb != nullptr;
   for (int i = threadIdx.x; i < S::P; i += 256) {
-    wl[i] = d.wa->w[(int)d.wa->cur][i];
-    if (has_b) wl[S::P + 4 + i] = d.wb->w[(int)d.wb->cur][i];
+    wl[i] = d.wa->w[0][i];
+    if (has_b) wl[S::P + 4 + i] = d.wb->w[0][i];
   }
   __syncthreads();
   const float* __restrict__ WA = wl;

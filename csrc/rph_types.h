@@ -18,8 +18,8 @@ constexpr int EVAL_NSTAT = 32; // doubles per workgroup in the eval stats slab
 enum Head : int { HEAD_FREE = 0, HEAD_COMPLEMENT = 1 };
 enum Loss : int { LOSS_MSE = 0, LOSS_PINBALL = 1 };
 
-// Ping-pong weights: the step kernel reads w[cur] (never written in-launch) and
-// its last-arriving workgroup writes w[cur^1] then flips cur.
+// Network weights.  Updated in place by the last-arriving workgroup of a step
+// (all readers of the launch have finished by then); w[1]/cur are reserved.
 struct NetWeights {
   float w[2][PMAX];
   float cur;
@@ -88,6 +88,8 @@ struct TrainDesc {
   int fused_update;              // 1: last arriver applies Adam (world_size==1)
   int num_wgs;
   int nin, h, nout, head;        // network shape (dispatch)
+  float* acc;                    // [8][R] float-atomic accumulator (zeroed; re-armed by last arriver)
+  int deterministic;             // 1: fixed-order slab reduction (bitwise reproducible)
 };
 
 struct EvalDesc {

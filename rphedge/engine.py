@@ -71,8 +71,10 @@ class TrainConfig:
     beta1: float = 0.9
     beta2: float = 0.999
     eps: float = 1e-7              # Keras epsilon
-    max_wgs: int = 256             # workgroups per training step (deterministic slab rows)
-    paths_per_thread: int = 2      # target work per thread per step
+    max_wgs: int = 256             # workgroups per training step
+    paths_per_thread: int = 1      # target work per thread per step
+    deterministic: bool = False    # fixed-order slab reduction instead of float atomics
+    split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
 
 
 @dataclass
@@ -190,6 +192,7 @@ class HipBackend:
         self.slab = torch.zeros(self.num_wgs, self.R, dtype=torch.float32, device=dev)
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
         self.grad = torch.zeros(self.R, dtype=torch.float32, device=dev)
+        self.acc = torch.zeros(8, self.R, dtype=torch.float32, device=dev)
         self.eval_wgs = int(max(1, min(1024, (self.n_local + 255) // 256)))
         self._cache = _Cache()
 
@@ -238,7 +241,9 @@ class HipBackend:
         d.chunk_log2 = int(self.tcfg.chunk_log2)
         d.shuffle = 1 if self.tcfg.shuffle else 0
         d.seed = int(seed) & 0xFFFFFFFF
-        d.fused_update = 1 if self.world == 1 else 0
+        d.fused_update = 1 if (self.world == 1 and not self.tcfg.split_update) else 0
+        d.acc = self.acc.data_ptr()
+        d.deterministic = 1 if self.tcfg.deterministic else 0
         d.num_wgs = self.num_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
         return d
@@ -256,8 +261,9 @@ class HipBackend:
         for e in range(fcfg.epochs):
             for s in range(S):
                 n.train_step(d, s, self.stream)
-                if self.world > 1:
-                    self.comm.allreduce_(self.grad, self.stream)
+                if self.world > 1 or self.tcfg.split_update:
+                    if self.world > 1:
+                        self.comm.allreduce_(self.grad, self.stream)
                     n.train_update(d, s, self.stream)
             if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:
                 if float(fit[L.F_STOPPED].item()) != 0.0:

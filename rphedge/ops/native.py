@@ -36,6 +36,7 @@ class TrainDesc(C.Structure):
         ("loss", C.c_int), ("n_local", C.c_int), ("batch", C.c_int), ("steps_per_epoch", C.c_int),
         ("chunk_log2", C.c_int), ("shuffle", C.c_int), ("seed", C.c_uint32), ("fused_update", C.c_int),
         ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
+        ("acc", VP), ("deterministic", C.c_int),
     ]
 
 
@@ -76,7 +77,7 @@ def _expected_layout() -> list[int]:
         L.F_BEST * f, L.F_STOPPED * f, L.F_EPOCH * f, L.F_LAST_LOSS * f, L.F_RESTORE_END * f, L.F_HIST * f,
         C.sizeof(T), T.price.offset, T.target.offset, T.wts.offset, T.lr_sched.offset, T.slab.offset,
         T.counter.offset, T.grad_out.offset, T.bond.offset, T.inv_batch.offset, T.loss.offset, T.seed.offset,
-        T.num_wgs.offset, T.head.offset,
+        T.num_wgs.offset, T.head.offset, T.acc.offset, T.deterministic.offset,
         C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
         E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
         E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset,
