@@ -1,0 +1,112 @@
+"""Experiment drivers of the reference notebooks (C33, C35–C37, C44).
+
+* :func:`single_time_step` — ``Single Time Step.ipynb`` (C33): one fit pair
+  over [0, T] (8192 paths, reduction 120), MSE holdings (Res1) vs
+  cost-of-capital blended holdings (Res2); cost of capital ``0.1*dt`` = 1.0
+  after the reduction (Q12) under ``parity``.
+* :func:`volatility_sweep` — σ ∈ {.05,.10,.15,.20,.30} of full
+  ``Replicating_Portfolio`` runs (C36, "Multi Time Step.ipynb":2299-2306).
+* :func:`sv_experiment` — the SV parameter dict of "Multi Time Step.ipynb":2612-2646 (C37).
+* :func:`mts_parameters` / :func:`sv_parameters` — the notebooks' param dicts (C35).
+* :func:`sanity_checks` — the implicit acceptance checks printed by the
+  notebooks (C44): MC mean vs analytic, grid shape, survivors, param counts.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import risk
+from .api import HedgeRun, run_params
+from .config import parse_params
+from .ops import layout as L
+
+
+def mts_parameters(**over) -> dict:
+    """``parameters`` dict of "Multi Time Step.ipynb":1329-1351 (μ, σ from the SV cell, Q16)."""
+    p = dict(Y=1, K=1, T=10, mu=0.09464, r=0.03, sigma=0.15965, rebalancing=0.25, N=10_000, P=100, x=55,
+             l0=0.01, c=0.075, ita=0.000597, dt=1 / 100, n_paths=int(math.ceil(math.log2(3000))))
+    p.update(over)
+    return p
+
+
+def sv_parameters(**over) -> dict:
+    """``sv_parameters`` of "Multi Time Step.ipynb":2612-2639 (duplicate 'c' key: later value wins, Q4)."""
+    p = dict(Y=1, K=1, T=10, mu=0.09464, r=0.03, s0=0.15965, a=0.0033566, b=0.15431, c=0.075,
+             rebalancing=0.25, N=10_000, P=100, x=55, l0=0.01, ita=0.000597, dt=1 / 100,
+             n_paths=int(math.ceil(math.log2(3000))))
+    p.update(over)
+    return p
+
+
+def volatility_sweep(base: dict | None = None, sigmas=(0.05, 0.10, 0.15, 0.20, 0.30), **over) -> list[dict]:
+    """Rows [sigma, Phi, Psi, Phi+Psi] like "Multi Time Step.ipynb":2397-2403."""
+    base = dict(mts_parameters(**over) if base is None else base)
+    rows = []
+    for s in sigmas:
+        p = dict(base, sigma=s)
+        res = run_params(p)
+        rows.append({"sigma": s, "Phi": res.phi, "Psi": res.psi, "sum": res.phi + res.psi, "V0": res.v0})
+    return rows
+
+
+def sv_experiment(**over) -> tuple[float, float]:
+    from .api import Replicating_Portfolio_SV
+
+    return Replicating_Portfolio_SV(sv_parameters(**over))
+
+
+def single_time_step(parity: bool = True, **over) -> dict:
+    """One-step pension hedge (C33).  Returns VaRs of Res1 (MSE holdings) and
+    Res2 (blended), phi0/psi0 and V0 (all in EUR)."""
+    p = dict(Y=1, K=1, T=10, mu=0.08, r=0.03, sigma=0.15, rebalancing=10, N=10_000, P=100, x=55, l0=0.01,
+             c=0.075, ita=0.000597, dt=1 / 12, n_paths=int(math.ceil(math.log2(8000))), parity=parity)
+    p.update(over)
+    cfg = parse_params(p)
+    if parity and "cost_of_capital" not in over:
+        cfg.train.cost_of_capital = 0.1 * cfg.dt_coarse   # Q12: 0.1*dt after dt *= reduction -> 1.0
+    cfg.parity.shared_q99_model = parity and cfg.parity.shared_q99_model
+    run = HedgeRun(cfg)
+    run.build()
+    ind = run.induction
+    # STS evaluates the MSE holdings BEFORE the pinball fit (Res1) -> keep that residual too
+    res1 = torch.empty(run.n_local, dtype=torch.float32, device=run.device)
+    orig_eval = run.backend.eval
+
+    def eval_hook(wts, data, stats, **kw):
+        if kw.get("v_out") is ind.gbuf and kw.get("wts_b") is None:
+            kw["resid_out"] = res1
+        return orig_eval(wts, data, stats, **kw)
+
+    run.backend.eval = eval_hook
+    res = run.run()
+    scale = res.scale
+    r1 = risk.quantile(res1, (0.985, 0.99, 0.995), run.di.world)
+    r2 = risk.quantile(res.induction.residuals[0], (0.985, 0.99, 0.995), run.di.world)
+    return {"phi0": res.phi, "psi0": res.psi, "V0": res.v0, "VaR_Res1": (r1 * scale).tolist(),
+            "VaR_Res2": (r2 * scale).tolist(), "VaR_Res1_unit": r1.tolist(), "VaR_Res2_unit": r2.tolist(),
+            "result": res}
+
+
+def sanity_checks(cfg_or_params, sv: bool = False) -> dict:
+    """Implicit notebook checks on freshly simulated paths."""
+    cfg = parse_params(cfg_or_params, sv=sv) if isinstance(cfg_or_params, dict) else cfg_or_params
+    run = HedgeRun(cfg)
+    p, vt = run.simulate()
+    st = run.summary_stats()
+    out = {"grid": {"n_fine": run.grid.n_fine, "reduction": run.grid.reduction, "n_coarse": run.grid.n_coarse,
+                    "dt_coarse": run.grid.dt_coarse, "shape": [run.n_total, p.n_coarse]}}
+    drift = cfg.mu if run.kind == "pension" else cfg.r
+    analytic = cfg.Y * math.exp(drift * cfg.T)
+    out["mean_Y_T"] = st["mean_Y_T"] * (cfg.Y if run.kind == "pension" else 1.0)
+    out["analytic_Y_T"] = analytic
+    out["diff"] = out["mean_Y_T"] - analytic
+    if "E_N_T" in st:
+        nT = p.nfrac_final.double() * cfg.N
+        out["N_T"] = {"mean": float(nT.mean()), "std": float(nT.std())}
+    out["p_oom"] = st["p_oom"]
+    out["E_payoff"] = st["E_payoff"]
+    out["nparams"] = run.spec.nparams
+    return out
