@@ -25,6 +25,14 @@
 
 namespace rph {
 
+// Diagnostic phase stamps (s_memrealtime, 100 MHz): thread 0 of every
+// workgroup writes stamp k to d.stamps[blockIdx.x * 8 + k] when d.stamps is set.
+#define RPH_STAMP(k)                                                                    \
+  do {                                                                                  \
+    if (d.stamps != nullptr && threadIdx.x == 0)                                        \
+      d.stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+
 template <int NIN, int H, int NO, int HEAD>
 struct NetShape {
   static constexpr int NHOLD = (HEAD == HEAD_COMPLEMENT) ? 2 : NO;
@@ -135,80 +143,114 @@ RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], 
 // EarlyStopping.on_epoch_end: wait+=1; if loss<best: best=loss, save, wait=0;
 //   if wait>=patience and epoch>0: stop (+restore best).
 // ---------------------------------------------------------------------------
+// Optimizer/early-stop state prefetched by EVERY workgroup at kernel start, so
+// the last arriver can apply the update without another memory round trip.
+struct UpdPre {
+  float m, v, w, wbest;                 // this thread's parameter (tid < P)
+  float t, lr, b1, b2, eps, nan_steps;
+  float loss_sum, abs_sum, ape_sum, loss_cnt;
+  float wait, has_best, best_loss, patience, max_epochs, restore_best, restore_at_end;
+  float lr_sched_e;                     // lr_sched[epoch] (NaN if none)
+};
+
 template <int P>
-RPH_INLINE void apply_update(const float* gsum, NetWeights* wts, OptState* opt, FitState* fs,
-                             const float* lr_sched, int step, int steps_per_epoch) {
-  __shared__ int s_act;
+RPH_INLINE void prefetch_update(UpdPre& u, const NetWeights* wts, const OptState* opt, const FitState* fs,
+                                const float* lr_sched, int epoch, int step) {
+  const int tid = threadIdx.x;
+  if (tid < P) {
+    u.m = opt->m[tid];
+    u.v = opt->v[tid];
+    u.w = wts->w[0][tid];
+    u.wbest = fs->w_best[tid];
+  } else {
+    u.m = u.v = u.w = u.wbest = 0.f;
+  }
+  u.t = opt->t; u.lr = opt->lr; u.b1 = opt->beta1; u.b2 = opt->beta2; u.eps = opt->eps;
+  u.nan_steps = opt->nan_steps;
+  u.loss_sum = fs->loss_sum; u.abs_sum = fs->abs_sum; u.ape_sum = fs->ape_sum; u.loss_cnt = fs->loss_cnt;
+  u.wait = fs->wait; u.has_best = fs->has_best; u.best_loss = fs->best_loss; u.patience = fs->patience;
+  u.max_epochs = fs->max_epochs; u.restore_best = fs->restore_best; u.restore_at_end = fs->restore_at_end;
+  u.lr_sched_e = (step == 0 && lr_sched != nullptr) ? lr_sched[epoch] : __builtin_nanf("");
+}
+
+// ---------------------------------------------------------------------------
+// Adam + EarlyStopping + LR schedule (K10).  Runs in ONE workgroup of 256
+// threads, weights updated IN PLACE (every other workgroup of the launch has
+// already passed the arrival ticket, i.e. finished reading them).  gsum (LDS)
+// holds the summed gradient [P] followed by the 4 loss statistics.
+// Keras 2.x semantics:
+//   lr_t = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+//   w -= lr_t*m/(sqrt(v)+eps)
+// EarlyStopping.on_epoch_end: wait+=1; if loss<best: best=loss, save, wait=0;
+//   if wait>=patience and epoch>0: stop (+restore best).
+// ---------------------------------------------------------------------------
+template <int P>
+RPH_INLINE void apply_update(const float* gsum, const UpdPre& u, NetWeights* wts, OptState* opt, FitState* fs,
+                             int epoch, int step, int steps_per_epoch) {
   const int tid = threadIdx.x;
   const bool mine = tid < P;
   const float g = mine ? gsum[tid] : 0.f;
-  // uniform scalars (read by every thread before thread 0 rewrites them below)
-  float lr = opt->lr;
-  if (step == 0 && lr_sched != nullptr) {  // Keras LearningRateScheduler.on_epoch_begin
-    const float l = lr_sched[(int)fs->epoch];
-    if (l == l) lr = l;                    // NaN => keep current
-  }
-  const float t0 = opt->t;
-  const float b1 = opt->beta1, b2 = opt->beta2, eps = opt->eps;
+  const float lr = (u.lr_sched_e == u.lr_sched_e) ? u.lr_sched_e : u.lr;  // on_epoch_begin (NaN => keep)
   const int finite = __syncthreads_and(mine ? (int)__builtin_isfinite(g) : 1);  // NaN/Inf guard
-  const float t = t0 + (finite ? 1.f : 0.f);
-  const float lr_t = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
-  float wnew = 0.f;
-  if (mine) {
-    wnew = wts->w[0][tid];
-    if (finite) {
-      float m = opt->m[tid], v = opt->v[tid];
-      m = m + (g - m) * (1.f - b1);
-      v = v + (g * g - v) * (1.f - b2);
-      opt->m[tid] = m;
-      opt->v[tid] = v;
-      wnew = wnew - lr_t * m / (sqrtf(v) + eps);
-      wts->w[0][tid] = wnew;
-    }
+  const float t = u.t + (finite ? 1.f : 0.f);
+  const float lr_t = lr * sqrtf(1.f - powf(u.b2, t)) / (1.f - powf(u.b1, t));
+  float wnew = u.w;
+  if (mine && finite) {
+    const float m = u.m + (g - u.m) * (1.f - u.b1);
+    const float v = u.v + (g * g - u.v) * (1.f - u.b2);
+    opt->m[tid] = m;
+    opt->v[tid] = v;
+    wnew = u.w - lr_t * m / (sqrtf(v) + u.eps);
   }
-  __syncthreads();
-  if (tid == 0) {  // epoch bookkeeping (thread 0 decides)
-    opt->lr = lr;
-    if (finite) opt->t = t;
-    else opt->nan_steps += 1.f;
-    fs->loss_sum += gsum[P + 0];
-    fs->abs_sum += gsum[P + 1];
-    fs->ape_sum += gsum[P + 2];
-    fs->loss_cnt += gsum[P + 3];
-    int act = 0;
-    if (step == steps_per_epoch - 1) {
-      const float cnt = fmaxf(fs->loss_cnt, 1.f);
-      const float L = fs->loss_sum / cnt;
-      const int e = (int)fs->epoch;
-      if (e < MAXHIST) fs->hist[e] = L;
+  // epoch bookkeeping: computed redundantly by every thread from the prefetched
+  // (uniform) state — no extra barrier; thread 0 persists it.
+  const float loss_sum = u.loss_sum + gsum[P + 0];
+  const float abs_sum = u.abs_sum + gsum[P + 1];
+  const float ape_sum = u.ape_sum + gsum[P + 2];
+  const float loss_cnt = u.loss_cnt + gsum[P + 3];
+  int act = 0;
+  if (step == steps_per_epoch - 1) {
+    const float cnt = fmaxf(loss_cnt, 1.f);
+    const float L = loss_sum / cnt;
+    float wait = u.wait + 1.f, best = u.best_loss, stopped = 0.f;
+    if (L < best || u.has_best == 0.f) {
+      if (L < best) { best = L; wait = 0.f; }
+      act = 1;
+    }
+    if (wait >= u.patience && epoch > 0) {
+      stopped = 1.f;
+      if (u.restore_best != 0.f) act = 2;
+    }
+    if ((float)(epoch + 1) >= u.max_epochs && stopped == 0.f) {
+      stopped = 1.f;
+      if (u.restore_best != 0.f && u.restore_at_end != 0.f) act = 2;
+    }
+    if (tid == 0) {
+      if (epoch < MAXHIST) fs->hist[epoch] = L;
       fs->last_loss = L;
-      fs->last_mae = fs->abs_sum / cnt;
-      fs->last_mape = 100.f * fs->ape_sum / cnt;
+      fs->last_mae = abs_sum / cnt;
+      fs->last_mape = 100.f * ape_sum / cnt;
       fs->loss_sum = fs->abs_sum = fs->ape_sum = fs->loss_cnt = 0.f;
-      fs->wait += 1.f;
-      const bool first = fs->has_best == 0.f;
-      if (L < fs->best_loss || first) {
-        if (L < fs->best_loss) { fs->best_loss = L; fs->wait = 0.f; }
-        fs->has_best = 1.f;
-        act = 1;
-      }
-      if (fs->wait >= fs->patience && e > 0) {
-        fs->stopped = 1.f;
-        if (fs->restore_best != 0.f) act = 2;
-      }
-      fs->epoch = (float)(e + 1);
-      if (fs->epoch >= fs->max_epochs && fs->stopped == 0.f) {
-        fs->stopped = 1.f;
-        if (fs->restore_best != 0.f && fs->restore_at_end != 0.f) act = 2;
-      }
+      fs->wait = wait;
+      fs->best_loss = best;
+      fs->has_best = 1.f;
+      fs->epoch = (float)(epoch + 1);
+      fs->stopped = stopped;
     }
-    s_act = act;
+  } else if (tid == 0) {
+    fs->loss_sum = loss_sum;
+    fs->abs_sum = abs_sum;
+    fs->ape_sum = ape_sum;
+    fs->loss_cnt = loss_cnt;
   }
-  __syncthreads();
-  const int act = s_act;
+  if (tid == 0) {
+    opt->lr = lr;
+    opt->t = t;
+    if (!finite) opt->nan_steps = u.nan_steps + 1.f;
+  }
   if (mine) {
     if (act == 1) fs->w_best[tid] = wnew;
-    else if (act == 2) wts->w[0][tid] = fs->w_best[tid];
+    wts->w[0][tid] = (act == 2) ? u.wbest : wnew;
   }
 }
 
@@ -224,7 +266,7 @@ constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contentio
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
 // ---------------------------------------------------------------------------
 template <int NIN, int H, int NO, int HEAD>
-__global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, const int step) {
+__global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, const int step, const int epoch) {
   using S = NetShape<NIN, H, NO, HEAD>;
   constexpr int R = S::R;
   constexpr int P = S::P;
@@ -233,14 +275,15 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ int s_last;
 
-  // prologue: independent loads (early-stop flag, epoch, weights) in flight together
+  // prologue: every independent load is issued up front — early-stop flag,
+  // weights, the optimizer state for a possible last-arriver update, and the
+  // first path's data (epoch is a launch argument, so the permutation needs no
+  // device read).
+  RPH_STAMP(0);
   const float stopped = d.fit->stopped;
-  const int epoch = (int)d.fit->epoch;
   const float wv = threadIdx.x < P ? d.wts->w[0][threadIdx.x] : 0.f;
-  if (stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
-  // Weights are wave-uniform: stage them once in LDS and read them as
-  // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
-  if (threadIdx.x < P) wl[threadIdx.x] = wv;
+  UpdPre up;
+  if (d.fused_update) prefetch_update<P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -250,7 +293,37 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   const uint32_t n_chunks = (uint32_t)((d.n_local + (1 << d.chunk_log2) - 1) >> d.chunk_log2);
   const Perm perm = make_perm(n_chunks, d.seed, (uint32_t)epoch, d.shuffle != 0);
   const uint32_t cmask = (1u << d.chunk_log2) - 1u;
+  const long long base = (long long)step * d.batch;
+
+  // path data of iteration `it` (software-pipelined one iteration ahead)
+  auto load_path = [&](long long j0, float (&x)[NIN], float (&pr)[NHOLD], float& y, bool& valid) {
+    const long long jl = j0 + lane;
+    const long long j = base + jl;
+    valid = (jl < d.batch) && (j < d.n_local);
+    uint32_t p = 0;
+    if (valid) {
+      const uint32_t ju = (uint32_t)j;
+      p = (perm(ju >> d.chunk_log2) << d.chunk_log2) | (ju & cmask);
+      if (p >= (uint32_t)d.n_local) p = ju;  // (only when n_local is not chunk-aligned)
+    }
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) x[f] = valid ? d.feat[f][p] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = valid ? d.price[k][p] : 0.f;
+    pr[NHOLD - 1] = d.bond;
+    y = valid ? d.target[p] : 0.f;
+  };
+  long long j0 = (long long)gw * 64;
+  float xn[NIN], prn[NHOLD], yn = 0.f;
+  bool validn = false;
+  if (j0 < d.batch) load_path(j0, xn, prn, yn, validn);
+
+  if (stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
+  // Weights are wave-uniform: stage them once in LDS and read them as
+  // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
+  if (threadIdx.x < P) wl[threadIdx.x] = wv;
   __syncthreads();
+  RPH_STAMP(1);
   const float* __restrict__ W = wl;
 
   float g[R];
@@ -258,25 +331,16 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   for (int i = 0; i < R; ++i) g[i] = 0.f;
 
   const float alpha = d.alpha;
-  const long long base = (long long)step * d.batch;
-  for (long long j0 = (long long)gw * 64; j0 < d.batch; j0 += (long long)nwaves * 64) {
-    const long long jl = j0 + lane;
-    const long long j = base + jl;
-    const bool valid = (jl < d.batch) && (j < d.n_local);
-    uint32_t p = 0;
-    if (valid) {
-      const uint32_t ju = (uint32_t)j;
-      p = (perm(ju >> d.chunk_log2) << d.chunk_log2) | (ju & cmask);
-      if (p >= (uint32_t)d.n_local) p = ju;  // (only when n_local is not chunk-aligned)
-    }
-    float x[NIN];
+  for (; j0 < d.batch; j0 += (long long)nwaves * 64) {
+    float x[NIN], pr[NHOLD];
 #pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = valid ? d.feat[f][p] : 0.f;
-    float pr[NHOLD];
+    for (int f = 0; f < NIN; ++f) x[f] = xn[f];
 #pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = valid ? d.price[k][p] : 0.f;
-    pr[NHOLD - 1] = d.bond;
-    const float y = valid ? d.target[p] : 0.f;
+    for (int k = 0; k < NHOLD; ++k) pr[k] = prn[k];
+    const float y = yn;
+    const bool valid = validn;
+    const long long jnext = j0 + (long long)nwaves * 64;
+    if (jnext < d.batch) load_path(jnext, xn, prn, yn, validn);
 
     float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
     net_forward<NIN, H, NO, HEAD>(W, x, alpha, z1, a1, z2, a2, hold);
@@ -341,6 +405,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
     }
   }
 
+  RPH_STAMP(2);
   // ---- in-wave reduce-scatter, cross-wave LDS sum --------------------------
   wave_reduce_scatter<R>(g, lane);
   constexpr int PER = R / 64;
@@ -351,6 +416,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   float val = 0.f;
   if (threadIdx.x < R) val = lds[threadIdx.x] + lds[R + threadIdx.x] + lds[2 * R + threadIdx.x] + lds[3 * R + threadIdx.x];
   __syncthreads();
+  RPH_STAMP(3);
 
   if (gridDim.x > 1) {
     // ---- publish the partial write-through (sc1) / float-atomically, then draw
@@ -365,11 +431,13 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
     __syncthreads();
+    RPH_STAMP(4);
     if (threadIdx.x == 0) {
       const uint32_t ticket = __hip_atomic_fetch_add(d.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = (ticket == (uint32_t)G - 1u) ? 1 : 0;
     }
     __syncthreads();
+    RPH_STAMP(5);
     if (!s_last) return;
     if (d.deterministic) {
       // fixed row partition + fixed combine order => bitwise reproducible
@@ -403,23 +471,27 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   }
   if (threadIdx.x < R) red[threadIdx.x] = val;
   __syncthreads();
+  RPH_STAMP(6);
 
   if (d.fused_update) {
-    apply_update<P>(red, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch);
+    apply_update<P>(red, up, d.wts, d.opt, d.fit, epoch, step, d.steps_per_epoch);
   } else if (threadIdx.x < R) {
     d.grad_out[threadIdx.x] = red[threadIdx.x];
   }
+  RPH_STAMP(7);
 }
 
 // K10 standalone (world_size > 1): one workgroup applies the all-reduced update.
 template <int NIN, int H, int NO, int HEAD>
-__global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const int step) {
+__global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const int step, const int epoch) {
   using S = NetShape<NIN, H, NO, HEAD>;
   __shared__ float gs[S::R + 8];
   if (d.fit->stopped != 0.f) return;
+  UpdPre up;
+  prefetch_update<S::P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
   for (int i = threadIdx.x; i < S::R; i += blockDim.x) gs[i] = d.grad_out[i];
   __syncthreads();
-  apply_update<S::P>(gs, d.wts, d.opt, d.fit, d.lr_sched, step, d.steps_per_epoch);
+  apply_update<S::P>(gs, up, d.wts, d.opt, d.fit, epoch, step, d.steps_per_epoch);
 }
 
 // ---------------------------------------------------------------------------
@@ -567,11 +639,11 @@ extern "C" int rph_net_nparams(int nin, int h, int nout, int head, int* p_out, i
   return -1;
 }
 
-extern "C" int rph_train_step(const TrainDesc* d, int step, void* stream) {
+extern "C" int rph_train_step(const TrainDesc* d, int step, int epoch, void* stream) {
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
-    hipLaunchKernelGGL((k_hedge_train_step<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d, step); \
+    hipLaunchKernelGGL((k_hedge_train_step<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d, step, epoch); \
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)
@@ -579,11 +651,11 @@ extern "C" int rph_train_step(const TrainDesc* d, int step, void* stream) {
   return -1;
 }
 
-extern "C" int rph_train_update(const TrainDesc* d, int step, void* stream) {
+extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* stream) {
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
-    hipLaunchKernelGGL((k_hedge_update<A, B, C, E>), dim3(1), dim3(256), 0, s, *d, step);   \
+    hipLaunchKernelGGL((k_hedge_update<A, B, C, E>), dim3(1), dim3(256), 0, s, *d, step, epoch); \
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)

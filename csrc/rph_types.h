@@ -90,6 +90,7 @@ struct TrainDesc {
   int nin, h, nout, head;        // network shape (dispatch)
   float* acc;                    // [8][R] float-atomic accumulator (zeroed; re-armed by last arriver)
   int deterministic;             // 1: fixed-order slab reduction (bitwise reproducible)
+  unsigned long long* stamps;    // diagnostic phase stamps [num_wgs][8] (null in production)
 };
 
 struct EvalDesc {

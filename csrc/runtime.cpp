@@ -48,7 +48,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       (long long)sizeof(TrainDesc), OFF(TrainDesc, price), OFF(TrainDesc, target), OFF(TrainDesc, wts),
       OFF(TrainDesc, lr_sched), OFF(TrainDesc, slab), OFF(TrainDesc, counter), OFF(TrainDesc, grad_out),
       OFF(TrainDesc, bond), OFF(TrainDesc, inv_batch), OFF(TrainDesc, loss), OFF(TrainDesc, seed),
-      OFF(TrainDesc, num_wgs), OFF(TrainDesc, head), OFF(TrainDesc, acc), OFF(TrainDesc, deterministic),
+      OFF(TrainDesc, num_wgs), OFF(TrainDesc, head), OFF(TrainDesc, acc), OFF(TrainDesc, deterministic), OFF(TrainDesc, stamps),
       // EvalDesc
       (long long)sizeof(EvalDesc), OFF(EvalDesc, price_t), OFF(EvalDesc, price_t1), OFF(EvalDesc, target),
       OFF(EvalDesc, wa), OFF(EvalDesc, g_base), OFF(EvalDesc, v_out), OFF(EvalDesc, hold_out),

@@ -193,6 +193,7 @@ class HipBackend:
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
         self.grad = torch.zeros(self.R, dtype=torch.float32, device=dev)
         self.acc = torch.zeros(8, self.R, dtype=torch.float32, device=dev)
+        self.stamps = None  # set to an int64 [num_wgs, 8] tensor for phase diagnostics
         self.eval_wgs = int(max(1, min(1024, (self.n_local + 255) // 256)))
         self._cache = _Cache()
 
@@ -244,6 +245,7 @@ class HipBackend:
         d.fused_update = 1 if (self.world == 1 and not self.tcfg.split_update) else 0
         d.acc = self.acc.data_ptr()
         d.deterministic = 1 if self.tcfg.deterministic else 0
+        d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
         d.num_wgs = self.num_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
         return d
@@ -260,11 +262,11 @@ class HipBackend:
         n, S = self.native, self.steps_per_epoch
         for e in range(fcfg.epochs):
             for s in range(S):
-                n.train_step(d, s, self.stream)
+                n.train_step(d, s, e, self.stream)
                 if self.world > 1 or self.tcfg.split_update:
                     if self.world > 1:
                         self.comm.allreduce_(self.grad, self.stream)
-                    n.train_update(d, s, self.stream)
+                    n.train_update(d, s, e, self.stream)
             if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:
                 if float(fit[L.F_STOPPED].item()) != 0.0:
                     break

@@ -36,7 +36,7 @@ class TrainDesc(C.Structure):
         ("loss", C.c_int), ("n_local", C.c_int), ("batch", C.c_int), ("steps_per_epoch", C.c_int),
         ("chunk_log2", C.c_int), ("shuffle", C.c_int), ("seed", C.c_uint32), ("fused_update", C.c_int),
         ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
-        ("acc", VP), ("deterministic", C.c_int),
+        ("acc", VP), ("deterministic", C.c_int), ("stamps", VP),
     ]
 
 
@@ -77,7 +77,7 @@ def _expected_layout() -> list[int]:
         L.F_BEST * f, L.F_STOPPED * f, L.F_EPOCH * f, L.F_LAST_LOSS * f, L.F_RESTORE_END * f, L.F_HIST * f,
         C.sizeof(T), T.price.offset, T.target.offset, T.wts.offset, T.lr_sched.offset, T.slab.offset,
         T.counter.offset, T.grad_out.offset, T.bond.offset, T.inv_batch.offset, T.loss.offset, T.seed.offset,
-        T.num_wgs.offset, T.head.offset, T.acc.offset, T.deterministic.offset,
+        T.num_wgs.offset, T.head.offset, T.acc.offset, T.deterministic.offset, T.stamps.offset,
         C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
         E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
         E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset,
@@ -106,8 +106,8 @@ def _bind(lib):
         "rph_nccl_allreduce_u32": (C.c_int, [VP, VP, C.c_longlong, VP]),
         "rph_nccl_destroy": (C.c_int, [VP]),
         "rph_net_nparams": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
-        "rph_train_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
-        "rph_train_update": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
+        "rph_train_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
+        "rph_train_update": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
@@ -198,12 +198,12 @@ def simulate(desc: SimDesc, stream=None):
     _check(lib.rph_simulate(C.byref(desc), stream_handle(stream)), "rph_simulate")
 
 
-def train_step(desc: TrainDesc, step: int, stream=None):
-    _check(_lib.rph_train_step(C.byref(desc), int(step), stream_handle(stream)), "rph_train_step")
+def train_step(desc: TrainDesc, step: int, epoch: int, stream=None):
+    _check(_lib.rph_train_step(C.byref(desc), int(step), int(epoch), stream_handle(stream)), "rph_train_step")
 
 
-def train_update(desc: TrainDesc, step: int, stream=None):
-    _check(_lib.rph_train_update(C.byref(desc), int(step), stream_handle(stream)), "rph_train_update")
+def train_update(desc: TrainDesc, step: int, epoch: int, stream=None):
+    _check(_lib.rph_train_update(C.byref(desc), int(step), int(epoch), stream_handle(stream)), "rph_train_update")
 
 
 def eval_(desc: EvalDesc, stream=None):
