@@ -57,7 +57,7 @@ struct NetShape {
 // ---------------------------------------------------------------------------
 struct Perm {
   uint32_t mask, n, k1, a1, b1, a2, b2, sh;
-  bool on;
+  int on;
   RPH_INLINE uint32_t f(uint32_t x) const {
     x = (((x ^ k1) * a1) + b1) & mask;
     x ^= x >> sh;
@@ -72,7 +72,7 @@ struct Perm {
   }
 };
 
-RPH_INLINE Perm make_perm(uint32_t n_chunks, uint32_t seed, uint32_t epoch, bool on) {
+__host__ __device__ inline Perm make_perm(uint32_t n_chunks, uint32_t seed, uint32_t epoch, bool on) {
   Perm p;
   uint32_t m = 1;
   int bits = 0;
@@ -87,7 +87,7 @@ RPH_INLINE Perm make_perm(uint32_t n_chunks, uint32_t seed, uint32_t epoch, bool
   p.a2 = (r.w | 1u);
   p.b2 = s.x;
   p.sh = bits > 1 ? (uint32_t)(bits / 2) : 1u;
-  p.on = on && n_chunks > 1;
+  p.on = (on && n_chunks > 1) ? 1 : 0;
   return p;
 }
 
@@ -266,7 +266,8 @@ constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contentio
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
 // ---------------------------------------------------------------------------
 template <int NIN, int H, int NO, int HEAD>
-__global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, const int step, const int epoch) {
+__global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, const int step, const int epoch,
+                                                          const Perm perm) {
   using S = NetShape<NIN, H, NO, HEAD>;
   constexpr int R = S::R;
   constexpr int P = S::P;
@@ -290,9 +291,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   const int nwaves = gridDim.x * 4;
   const int gw = blockIdx.x * 4 + wid;
 
-  const uint32_t n_chunks = (uint32_t)((d.n_local + (1 << d.chunk_log2) - 1) >> d.chunk_log2);
-  const Perm perm = make_perm(n_chunks, d.seed, (uint32_t)epoch, d.shuffle != 0);
-  const uint32_t cmask = (1u << d.chunk_log2) - 1u;
+  const uint32_t cmask = (1u << d.chunk_log2) - 1u;  // perm keys come from the host (launch argument)
   const long long base = (long long)step * d.batch;
 
   // path data of iteration `it` (software-pipelined one iteration ahead)
@@ -322,6 +321,10 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   // Weights are wave-uniform: stage them once in LDS and read them as
   // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
   if (threadIdx.x < P) wl[threadIdx.x] = wv;
+  if (d.fused_update) {  // keep the prefetch here (the compiler would sink it into the last-arriver branch)
+    asm volatile("" ::"v"(up.m), "v"(up.v), "v"(up.w), "v"(up.wbest), "v"(up.t), "v"(up.lr), "v"(up.loss_sum),
+                 "v"(up.wait), "v"(up.best_loss), "v"(up.lr_sched_e));
+  }
   __syncthreads();
   RPH_STAMP(1);
   const float* __restrict__ W = wl;
@@ -457,14 +460,43 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
       __syncthreads();
     } else {
       if (threadIdx.x < R) {
-        float s2 = 0.f;
-#pragma unroll
-        for (int rp = 0; rp < ACC_REPLICAS; ++rp) {
-          float* a = d.acc + rp * R + threadIdx.x;
-          s2 += ld_agent(a);
-          st_agent(a, 0.f);  // re-arm for the next step
+        // all 8 replica loads in ONE asm statement with one wait (sc1: every load
+        // of the handed-off bytes bypasses the non-coherent L1), then re-arm.
+        float* a = d.acc + threadIdx.x;
+        float r0, r1, r2, r3, r4, r5, r6, r7;
+        if (R == 128) {
+          asm volatile(
+              "global_load_dword %0, %8, off sc1\n\t"
+              "global_load_dword %1, %8, off offset:512 sc1\n\t"
+              "global_load_dword %2, %8, off offset:1024 sc1\n\t"
+              "global_load_dword %3, %8, off offset:1536 sc1\n\t"
+              "global_load_dword %4, %8, off offset:2048 sc1\n\t"
+              "global_load_dword %5, %8, off offset:2560 sc1\n\t"
+              "global_load_dword %6, %8, off offset:3072 sc1\n\t"
+              "global_load_dword %7, %8, off offset:3584 sc1\n\t"
+              "s_waitcnt vmcnt(0)"
+              : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
+              : "v"(a)
+              : "memory");
+        } else {
+          float* b = a + 4 * R;
+          asm volatile(
+              "global_load_dword %0, %8, off sc1\n\t"
+              "global_load_dword %1, %8, off offset:1024 sc1\n\t"
+              "global_load_dword %2, %8, off offset:2048 sc1\n\t"
+              "global_load_dword %3, %8, off offset:3072 sc1\n\t"
+              "global_load_dword %4, %9, off sc1\n\t"
+              "global_load_dword %5, %9, off offset:1024 sc1\n\t"
+              "global_load_dword %6, %9, off offset:2048 sc1\n\t"
+              "global_load_dword %7, %9, off offset:3072 sc1\n\t"
+              "s_waitcnt vmcnt(0)"
+              : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
+              : "v"(a), "v"(b)
+              : "memory");
         }
-        val = s2;
+        val = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+#pragma unroll
+        for (int rp = 0; rp < ACC_REPLICAS; ++rp) st_agent(a + rp * R, 0.f);  // re-arm (completes by kernel end)
       }
     }
     if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -641,9 +673,11 @@ extern "C" int rph_net_nparams(int nin, int h, int nout, int head, int* p_out, i
 
 extern "C" int rph_train_step(const TrainDesc* d, int step, int epoch, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const uint32_t n_chunks = (uint32_t)((d->n_local + (1 << d->chunk_log2) - 1) >> d->chunk_log2);
+  const Perm perm = make_perm(n_chunks, d->seed, (uint32_t)epoch, d->shuffle != 0);
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
-    hipLaunchKernelGGL((k_hedge_train_step<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d, step, epoch); \
+    hipLaunchKernelGGL((k_hedge_train_step<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d, step, epoch, perm); \
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)

@@ -183,31 +183,50 @@ RPH_INLINE float xlane_bit0(float v) {  // quad_perm [1,0,3,2]
 
 // Recursive-halving ("reduce-scatter in a wave") of an R-vector held by every
 // lane.  After the call lane L holds the wave-total of entries
-// [L*(R/64), (L+1)*(R/64)) in v[0 .. R/64).  Cost ~ 4R VALU instead of 12R for
-// a naive butterfly per entry.  All indices are compile-time (no scratch).
+// [L*(R/64), (L+1)*(R/64)) in v[0 .. R/64).  All indices are compile-time (no
+// scratch).  Cross-lane moves, cheapest first on the largest arrays:
+//   bit 5: v_permlane32_swap (a HALF exchange: lanes 32-63 of the first operand
+//          swap with lanes 0-31 of the second) -> after swap(v[i], v[i+H])
+//          every lane's two registers hold exactly its own and its partner's
+//          share, so the step is ONE swap + ONE add per pair, no selects;
+//   bit 4: ds_swizzle xor-16 butterfly;
+//   bits 3..0: DPP (row_mirror / row_half_mirror / quad_perm) butterflies
+//          whose adds fold the DPP move (v_add_f32_dpp).
+template <int LEN>
+RPH_INLINE void halve_bit5(float* v) {
+  constexpr int H = LEN / 2;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + H]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+}
+
 template <int LEN, int BIT>
 RPH_INLINE void halve_step(float* v, int lane) {
   constexpr int H = LEN / 2;
   const bool up = (lane >> BIT) & 1;
 #pragma unroll
   for (int i = 0; i < H; ++i) {
-    const float keep = up ? v[i + H] : v[i];
-    const float send = up ? v[i] : v[i + H];
-    float got;
-    if (BIT == 5) got = xlane_bit5(send);
-    else if (BIT == 4) got = xlane_bit4(send);
-    else if (BIT == 3) got = xlane_bit3(send);
-    else if (BIT == 2) got = xlane_bit2(send);
-    else if (BIT == 1) got = xlane_bit1(send);
-    else got = xlane_bit0(send);
-    v[i] = keep + got;
+    if (BIT == 4) {
+      const float keep = up ? v[i + H] : v[i];
+      const float send = up ? v[i] : v[i + H];
+      v[i] = keep + xlane_bit4(send);
+    } else {
+      float lo, hi;
+      if (BIT == 3) { lo = v[i] + xlane_bit3(v[i]); hi = v[i + H] + xlane_bit3(v[i + H]); }
+      else if (BIT == 2) { lo = v[i] + xlane_bit2(v[i]); hi = v[i + H] + xlane_bit2(v[i + H]); }
+      else if (BIT == 1) { lo = v[i] + xlane_bit1(v[i]); hi = v[i + H] + xlane_bit1(v[i + H]); }
+      else { lo = v[i] + xlane_bit0(v[i]); hi = v[i + H] + xlane_bit0(v[i + H]); }
+      v[i] = up ? hi : lo;
+    }
   }
 }
 
 template <int R>
 RPH_INLINE void wave_reduce_scatter(float* v, int lane) {
   static_assert(R >= 64 && (R & (R - 1)) == 0, "R must be a power of two >= 64");
-  halve_step<R, 5>(v, lane);
+  halve_bit5<R>(v);
   halve_step<R / 2, 4>(v, lane);
   halve_step<R / 4, 3>(v, lane);
   halve_step<R / 8, 2>(v, lane);
