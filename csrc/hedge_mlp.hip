@@ -193,14 +193,17 @@ RPH_INLINE void apply_update(const float* gsum, const UpdPre& u, NetWeights* wts
   const float lr = (u.lr_sched_e == u.lr_sched_e) ? u.lr_sched_e : u.lr;  // on_epoch_begin (NaN => keep)
   const int finite = __syncthreads_and(mine ? (int)__builtin_isfinite(g) : 1);  // NaN/Inf guard
   const float t = u.t + (finite ? 1.f : 0.f);
-  const float lr_t = lr * sqrtf(1.f - powf(u.b2, t)) / (1.f - powf(u.b1, t));
+  // b^t = exp2(t log2 b) on the transcendental unit (v_log/v_exp, ~1 ulp)
+  const float bc1 = 1.f - __builtin_amdgcn_exp2f(t * __builtin_amdgcn_logf(u.b1));
+  const float bc2 = 1.f - __builtin_amdgcn_exp2f(t * __builtin_amdgcn_logf(u.b2));
+  const float lr_t = lr * sqrtf(bc2) * __frcp_rn(bc1);
   float wnew = u.w;
   if (mine && finite) {
     const float m = u.m + (g - u.m) * (1.f - u.b1);
     const float v = u.v + (g * g - u.v) * (1.f - u.b2);
     opt->m[tid] = m;
     opt->v[tid] = v;
-    wnew = u.w - lr_t * m / (sqrtf(v) + u.eps);
+    wnew = u.w - lr_t * m * __frcp_rn(sqrtf(v) + u.eps);
   }
   // epoch bookkeeping: computed redundantly by every thread from the prefetched
   // (uniform) state — no extra barrier; thread 0 persists it.
@@ -211,7 +214,7 @@ RPH_INLINE void apply_update(const float* gsum, const UpdPre& u, NetWeights* wts
   int act = 0;
   if (step == steps_per_epoch - 1) {
     const float cnt = fmaxf(loss_cnt, 1.f);
-    const float L = loss_sum / cnt;
+    const float L = loss_sum * __frcp_rn(cnt);
     float wait = u.wait + 1.f, best = u.best_loss, stopped = 0.f;
     if (L < best || u.has_best == 0.f) {
       if (L < best) { best = L; wait = 0.f; }
@@ -228,8 +231,8 @@ RPH_INLINE void apply_update(const float* gsum, const UpdPre& u, NetWeights* wts
     if (tid == 0) {
       if (epoch < MAXHIST) fs->hist[epoch] = L;
       fs->last_loss = L;
-      fs->last_mae = abs_sum / cnt;
-      fs->last_mape = 100.f * ape_sum / cnt;
+      fs->last_mae = abs_sum * __frcp_rn(cnt);
+      fs->last_mape = 100.f * ape_sum * __frcp_rn(cnt);
       fs->loss_sum = fs->abs_sum = fs->ape_sum = fs->loss_cnt = 0.f;
       fs->wait = wait;
       fs->best_loss = best;
