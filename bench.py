@@ -44,12 +44,12 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--paths-log2", type=int, default=20, help="paths PER GPU (weak scaling)")
     ap.add_argument("--dates", type=int, default=30)
-    ap.add_argument("--epochs-first", type=int, default=64)
+    ap.add_argument("--epochs-first", type=int, default=512)
     ap.add_argument("--epochs-rest", type=int, default=12)
-    ap.add_argument("--batch-log2", type=int, default=16, help="per-GPU minibatch (global = N x this)")
-    ap.add_argument("--lr", type=float, default=1e-2)
-    ap.add_argument("--lr-rest", type=float, default=2e-3)
-    ap.add_argument("--lr-decay", type=float, default=1.0, help="per-date geometric LR decay factor (last/first epoch)")
+    ap.add_argument("--batch-log2", type=int, default=18, help="per-GPU minibatch (global = N x this)")
+    ap.add_argument("--lr", type=float, default=2e-2)
+    ap.add_argument("--lr-rest", type=float, default=4e-3)
+    ap.add_argument("--lr-decay", type=float, default=0.02, help="per-date geometric LR decay factor (last/first epoch)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -106,9 +106,15 @@ def main(argv=None):
         return f
 
     ind._fcfg = fcfg
-    use_graph = gpu and not a.no_graph
+    use_graph = gpu and not a.no_graph and (world == 1 or os.environ.get("RPH_GRAPH_DP", "1") == "1")
     if use_graph:
-        run.capture(include_simulation=True)
+        try:
+            run.capture(include_simulation=True)
+        except Exception as e:  # e.g. a collective that refuses stream capture: run eagerly
+            if rank == 0:
+                print(f"bench.py: graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            torch.cuda.synchronize(run.device)
+            use_graph = False
 
     def one():
         if use_graph:

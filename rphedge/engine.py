@@ -243,6 +243,8 @@ class HipBackend:
         d.shuffle = 1 if self.tcfg.shuffle else 0
         d.seed = int(seed) & 0xFFFFFFFF
         d.fused_update = 1 if (self.world == 1 and not self.tcfg.split_update) else 0
+        if self.world > 1 and self.comm is None:
+            raise RuntimeError("HipBackend with world_size > 1 needs a native RCCL communicator")
         d.acc = self.acc.data_ptr()
         d.deterministic = 1 if self.tcfg.deterministic else 0
         d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
@@ -264,7 +266,7 @@ class HipBackend:
             for s in range(S):
                 n.train_step(d, s, e, self.stream)
                 if self.world > 1 or self.tcfg.split_update:
-                    if self.world > 1:
+                    if self.comm is not None:
                         self.comm.allreduce_(self.grad, self.stream)
                     n.train_update(d, s, e, self.stream)
             if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:

@@ -275,3 +275,68 @@ def test_deterministic_mode_is_bitwise_reproducible(dev):
     a = _fit_pair(dev, spec, 1 << 16, 1 << 15, 2, L.LOSS_MSE, chunk_log2=6, deterministic=True)[1]
     b = _fit_pair(dev, spec, 1 << 16, 1 << 15, 2, L.LOSS_MSE, chunk_log2=6, deterministic=True)[1]
     assert np.array_equal(a[0], b[0])
+
+
+def test_rccl_comm_split_update_and_graph_capture(dev):
+    """The DP hot path on one rank: step kernel -> native RCCL all-reduce ->
+    standalone update kernel, eager and captured in a hipGraph."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+    from torch.distributed import distributed_c10d as c10d
+
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops import layout as L
+    from rphedge.ops.native import Graph, NcclComm
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        comm = NcclComm(0, 1, c10d._get_default_store(), tag="test_rccl")
+        spec = NetSpec(nin=3, hidden=8, nout=2, head=0)
+        n = 1 << 15
+        gen = torch.Generator().manual_seed(5)
+        feats = [torch.rand(n, generator=gen) * 0.5 + 0.75 for _ in range(3)]
+        prices = [feats[0] * 1.02]
+        target = torch.relu(prices[0] - 1.0)
+        w0 = init_weights(spec, [0.5, -0.4])
+        tc = TrainConfig(batch_size=1 << 13, chunk_log2=6, lr=1e-2, split_update=True)
+        fc = FitConfig(epochs=3, patience=100, early_stopping=False)
+        out = {}
+        for name, be, d in (("cpu", TorchBackend(spec, n, tc, device="cpu"), torch.device("cpu")),
+                            ("gpu", HipBackend(spec, n, tc, device=dev, comm=comm, world=1), dev)):
+            data = DateData(feats=[f.to(d) for f in feats], prices_next=[p.to(d) for p in prices],
+                            bond_next=1.0, target=target.to(d), prices_now=[feats[0].to(d)])
+            w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+            be.fit(w, o, f, data, fc, seed=9)
+            out[name] = current_weights(spec, w)
+            if name == "gpu":
+                torch.cuda.synchronize()
+                # capture the same fit (RCCL all-reduce nodes included) and replay it
+                w2, o2, f2 = be.new_weights(w0), be.new_opt(), be.new_fit()
+                be.fit(w2, o2, f2, data, fc, seed=9)  # eager warm-up populates caches
+                torch.cuda.synchronize()
+                w2.copy_(be.new_weights(w0))
+                o2.copy_(be.new_opt())
+                st = torch.cuda.Stream(dev)
+                st.wait_stream(torch.cuda.current_stream())
+                g = Graph()
+                with torch.cuda.stream(st):
+                    g.capture_begin(st)
+                    be.fit(w2, o2, f2, data, fc, seed=9)
+                    g.capture_end()
+                    g.replay(st)
+                st.synchronize()
+                out["graph"] = current_weights(spec, w2)
+                assert float(f2[L.F_EPOCH].item()) == 3
+        np.testing.assert_allclose(out["gpu"], out["cpu"], rtol=2e-3, atol=2e-4)
+        np.testing.assert_allclose(out["graph"], out["gpu"], rtol=1e-4, atol=1e-5)
+        comm.close()
+    finally:
+        dist.destroy_process_group()
