@@ -552,11 +552,13 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   const float* __restrict__ WB = has_b ? wl + S::P + 4 : wl;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 
-  double st[EVAL_NSTAT];
+  // per-thread fp32 partials (a thread sees only a handful of paths), one
+  // in-wave reduce-scatter, fp64 only across waves / workgroups
+  constexpr int NS = 64;
+  float st[NS];
 #pragma unroll
-  for (int i = 0; i < EVAL_NSTAT; ++i) st[i] = 0.0;
-  st[ES_RESMIN] = INFINITY;
-  st[ES_RESMAX] = -INFINITY;
+  for (int i = 0; i < NS; ++i) st[i] = 0.f;
+  float rmin = INFINITY, rmax = -INFINITY;
 
   for (int p0 = blockIdx.x * 256; p0 < d.n_local; p0 += gridDim.x * 256) {
     const int p = p0 + threadIdx.x;
@@ -584,13 +586,16 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
       const float gb = d.g_base[pp];
       V = gb + d.blend_c * (V - gb);
     }
-    float res = 0.f, pred1 = 0.f;
-    const bool has1 = d.price_t1[0] != nullptr || NHOLD == 1;
+    float res = 0.f, pred1 = 0.f, tgt = 0.f;
+    const bool has1 = d.price_t1[0] != nullptr;
     if (has1) {
 #pragma unroll
       for (int k = 0; k < NHOLD - 1; ++k) pred1 = fmaf(hold[k], d.price_t1[k][pp], pred1);
       pred1 = fmaf(hold[NHOLD - 1], d.bond_t1, pred1);
-      if (d.target) res = d.target[pp] - pred1;
+      if (d.target) {
+        tgt = d.target[pp];
+        res = tgt - pred1;
+      }
     }
     if (valid) {
       if (d.v_out) d.v_out[p] = V;
@@ -600,36 +605,32 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
       if (d.resid_out) d.resid_out[p] = res;
       if (d.pred1_out) d.pred1_out[p] = pred1;
       st[ES_V] += V;
-      st[ES_V2] += (double)V * V;
+      st[ES_V2] += V * V;
       st[ES_RES] += res;
-      st[ES_RES2] += (double)res * res;
-      st[ES_ABSRES] += fabs((double)res);
-      if (d.target) st[ES_APE] += fabs((double)res) / fmax(fabs((double)d.target[pp]), 1e-7);
+      st[ES_RES2] += res * res;
+      st[ES_ABSRES] += fabsf(res);
+      st[ES_APE] += d.target ? fabsf(res) * __frcp_rn(fmaxf(fabsf(tgt), 1e-7f)) : 0.f;
       st[ES_PRED1] += pred1;
-      st[ES_COUNT] += 1.0;
+      st[ES_COUNT] += 1.f;
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) {
         st[ES_HOLD + k] += hold[k];
-        st[ES_HOLD2 + k] += (double)hold[k] * hold[k];
+        st[ES_HOLD2 + k] += hold[k] * hold[k];
       }
-      st[ES_RESMIN] = fmin(st[ES_RESMIN], (double)res);
-      st[ES_RESMAX] = fmax(st[ES_RESMAX], (double)res);
+      rmin = fminf(rmin, res);
+      rmax = fmaxf(rmax, res);
     }
   }
-  // block reduce (fp64, only at the end)
+  wave_reduce_scatter<NS>(st, lane);  // lane L now holds the wave total of stat L
 #pragma unroll
-  for (int i = 0; i < EVAL_NSTAT; ++i) {
-    double v = st[i];
-    if (i == ES_RESMIN) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    } else if (i == ES_RESMAX) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    } else {
-      v = wave_sum_d(v);
-    }
-    if (lane == 0) sst[wid][i] = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    rmin = fminf(rmin, __shfl_xor(rmin, o, 64));
+    rmax = fmaxf(rmax, __shfl_xor(rmax, o, 64));
+  }
+  if (lane < EVAL_NSTAT) sst[wid][lane] = (double)st[0];
+  if (lane == 0) {
+    sst[wid][ES_RESMIN] = rmin;
+    sst[wid][ES_RESMAX] = rmax;
   }
   __syncthreads();
   if (threadIdx.x < EVAL_NSTAT) {

@@ -13,7 +13,7 @@ from rphedge.ops import layout as L  # noqa: E402
 from rphedge.ops import native  # noqa: E402
 
 
-def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False):
+def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False, max_wgs=256, ppt=1):
     dev = torch.device("cuda", 0)
     spec = NetSpec(nin=nin, hidden=8, nout=nout, head=0)
     n = 1 << n_log2
@@ -21,7 +21,8 @@ def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False):
     feats = [(torch.rand(n, generator=g) * 0.5 + 0.75).to(dev) for _ in range(nin)]
     prices = [f * 1.01 for f in feats[: spec.nhold - 1]]
     target = torch.relu(prices[0] - 1.0)
-    be = HipBackend(spec, n, TrainConfig(batch_size=1 << batch_log2, chunk_log2=6, deterministic=det), device=dev)
+    be = HipBackend(spec, n, TrainConfig(batch_size=1 << batch_log2, chunk_log2=6, deterministic=det, max_wgs=max_wgs,
+                                         paths_per_thread=ppt), device=dev)
     data = DateData(feats=feats, prices_next=prices, bond_next=1.0, target=target, prices_now=feats[:1])
     w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
     fc = FitConfig(epochs=1000, patience=10 ** 6, early_stopping=False)
@@ -54,6 +55,8 @@ def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False):
 
 
 if __name__ == "__main__":
-    for bl in (14, 16, 18):
-        for det in (False, True):
-            print(json.dumps(run(batch_log2=bl, det=det)), flush=True)
+    grid = [dict(batch_log2=bl, det=False) for bl in (14, 16, 18)] + [dict(batch_log2=16, det=True)]
+    grid += [dict(batch_log2=18, max_wgs=mw) for mw in (512, 1024)] + [dict(batch_log2=17, max_wgs=512)]
+    grid += [dict(batch_log2=18, nin=3, nout=2), dict(batch_log2=18, nin=5, nout=6)]
+    for g in grid:
+        print(json.dumps(run(**g)), flush=True)
