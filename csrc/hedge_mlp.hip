@@ -325,8 +325,8 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
   if (threadIdx.x < P) wl[threadIdx.x] = wv;
   if (d.fused_update) {  // keep the prefetch here (the compiler would sink it into the last-arriver branch)
-    asm volatile("" ::"v"(up.m), "v"(up.v), "v"(up.w), "v"(up.wbest), "v"(up.t), "v"(up.lr), "v"(up.loss_sum),
-                 "v"(up.wait), "v"(up.best_loss), "v"(up.lr_sched_e));
+    asm volatile("" ::"v"(up.m), "v"(up.v), "v"(up.w), "v"(up.wbest), "s"(up.t), "s"(up.lr), "s"(up.loss_sum),
+                 "s"(up.wait), "s"(up.best_loss), "s"(up.lr_sched_e));
   }
   __syncthreads();
   RPH_STAMP(1);
@@ -338,6 +338,12 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
 
   const float alpha = d.alpha;
   for (; j0 < d.batch; j0 += (long long)nwaves * 64) {
+    // Re-read the (LDS-resident, broadcast) weights every iteration instead of
+    // letting the compiler hoist ~100 loop-invariant weights into VGPRs: the
+    // opaque zero offset keeps register pressure low enough for 2 waves/SIMD.
+    int zoff;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
+    const float* __restrict__ Wi = W + zoff;
     float x[NIN], pr[NHOLD];
 #pragma unroll
     for (int f = 0; f < NIN; ++f) x[f] = xn[f];
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
     if (jnext < d.batch) load_path(jnext, xn, prn, yn, validn);
 
     float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
-    net_forward<NIN, H, NO, HEAD>(W, x, alpha, z1, a1, z2, a2, hold);
+    net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold);
     float V = 0.f;
 #pragma unroll
     for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
 #pragma unroll
       for (int k = 0; k < NO; ++k) {
         g[S::OW3 + j * NO + k] = fmaf(a2[j], dout[k], g[S::OW3 + j * NO + k]);
-        da = fmaf(W[S::OW3 + j * NO + k], dout[k], da);
+        da = fmaf(Wi[S::OW3 + j * NO + k], dout[k], da);
       }
       dz2[j] = da * lrelu_d(z2[j], alpha);
       g[S::OB2 + j] += dz2[j];
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
 #pragma unroll
       for (int j = 0; j < H; ++j) {
         g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
-        da = fmaf(W[S::OW2 + i * H + j], dz2[j], da);
+        da = fmaf(Wi[S::OW2 + i * H + j], dz2[j], da);
       }
       const float dz1 = da * lrelu_d(z1[i], alpha);
       g[S::OB1 + i] += dz1;

@@ -24,7 +24,7 @@ def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False, max_wgs=256
     be = HipBackend(spec, n, TrainConfig(batch_size=1 << batch_log2, chunk_log2=6, deterministic=det, max_wgs=max_wgs,
                                          paths_per_thread=ppt), device=dev)
     data = DateData(feats=feats, prices_next=prices, bond_next=1.0, target=target, prices_now=feats[:1])
-    w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+    w, o, f = be.new_weights(init_weights(spec, [0.5] + [0.0] * (nout - 1))), be.new_opt(), be.new_fit()
     fc = FitConfig(epochs=1000, patience=10 ** 6, early_stopping=False)
     be.fit(w, o, f, data, fc, seed=1)  # warm
     torch.cuda.synchronize()
@@ -55,8 +55,9 @@ def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False, max_wgs=256
 
 
 if __name__ == "__main__":
-    grid = [dict(batch_log2=bl, det=False) for bl in (14, 16, 18)] + [dict(batch_log2=16, det=True)]
-    grid += [dict(batch_log2=18, max_wgs=mw) for mw in (512, 1024)] + [dict(batch_log2=17, max_wgs=512)]
-    grid += [dict(batch_log2=18, nin=3, nout=2), dict(batch_log2=18, nin=5, nout=6)]
+    import sys as _s
+    grid = json.loads(_s.argv[1]) if len(_s.argv) > 1 else (
+        [dict(batch_log2=bl) for bl in (14, 16, 18)] + [dict(batch_log2=18, max_wgs=512), dict(batch_log2=17, max_wgs=512),
+                                                       dict(batch_log2=18, max_wgs=1024)])
     for g in grid:
         print(json.dumps(run(**g)), flush=True)
