@@ -338,12 +338,9 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
 
   const float alpha = d.alpha;
   for (; j0 < d.batch; j0 += (long long)nwaves * 64) {
-    // Re-read the (LDS-resident, broadcast) weights every iteration instead of
-    // letting the compiler hoist ~100 loop-invariant weights into VGPRs: the
-    // opaque zero offset keeps register pressure low enough for 2 waves/SIMD.
-    int zoff;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
-    const float* __restrict__ Wi = W + zoff;
+    // (loop-invariant LDS weights are hoisted into registers by the compiler;
+    // re-reading them per iteration to reach 2 waves/SIMD measured slower)
+    const float* __restrict__ Wi = W;
     float x[NIN], pr[NHOLD];
 #pragma unroll
     for (int f = 0; f < NIN; ++f) x[f] = xn[f];
