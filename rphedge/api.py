@@ -206,7 +206,7 @@ class HedgeRun:
         self.w0 = self.init_weights(self.stats0) if w0 is None else w0
         tr = c.train
         tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
-                           lr=tr.lr)
+                           lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs)
         self.backend = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
                                     comm=self.di.comm, world=self.di.world, rank=self.di.rank, stream=self.stream)
         pf = c.parity

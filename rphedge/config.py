@@ -65,6 +65,8 @@ class TrainingParams:
     seed: int = 1234
     leaky_alpha: float = 0.3
     poll_every: int = 0              # host early-stop polling (0 = fully async / graph)
+    deterministic: bool = False      # fixed-order gradient reduction (bitwise reproducible)
+    max_wgs: int = 256               # workgroups per training step
 
 
 @dataclass

@@ -1,0 +1,191 @@
+"""API / feature coverage on CPU: pension + SV dict API, parity flags, saved-model
+format, CLI, experiments, calibration, Brownian helpers, reports."""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _small(**kw):
+    from rphedge.experiments import mts_parameters
+
+    p = mts_parameters(n_paths=9, dt=0.1, rebalancing=1.0, epochs_first=20, epochs_rest=5, verbose=False,
+                       device="cpu")
+    p.update(kw)
+    return p
+
+
+def test_replicating_portfolio_returns_two_floats():
+    from rphedge import Replicating_Portfolio
+
+    phi, psi = Replicating_Portfolio(_small())
+    assert isinstance(phi, float) and isinstance(psi, float)
+    # holdings of a N*P=1e6 guarantee: phi + psi of the order of the liability value
+    assert 4e5 < phi + psi < 1.6e6
+
+
+def test_replicating_portfolio_sv_parity():
+    from rphedge import Replicating_Portfolio_SV
+    from rphedge.experiments import sv_parameters
+
+    p = sv_parameters(n_paths=9, dt=0.1, rebalancing=1.0, epochs_first=20, epochs_rest=5, verbose=False,
+                      device="cpu", parity=True)
+    phi, psi = Replicating_Portfolio_SV(p)
+    assert math.isfinite(phi) and math.isfinite(psi)
+
+
+def test_parity_shared_model_has_identical_nets():
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+
+    cfg = parse_params(_small(parity=True))
+    run = HedgeRun(cfg)
+    run.build()
+    assert run.induction.w_q is run.induction.w_mse           # Q1 alias
+    assert run.induction.opt_q is not run.induction.opt_mse   # two Adam instances
+    cfg2 = parse_params(_small())
+    run2 = HedgeRun(cfg2)
+    run2.build()
+    assert run2.induction.w_q is not run2.induction.w_mse
+
+
+def test_lambda_fine_index_quirk():
+    """Q3: with parity the lambda feature at coarse index i is lambda on the fine grid at i."""
+    from rphedge.ops import paths as P
+
+    g = P.Grid(10.0, 0.1, 1.0)
+    a = P.simulate_gbm(g, 512, 1.0, 0.08, 0.15, device="cpu")
+    P.simulate_mortality(a, 0.01, 0.075, 0.000597, 10000, lambda_fine_index=True)
+    b = P.simulate_gbm(g, 512, 1.0, 0.08, 0.15, device="cpu")
+    P.simulate_mortality(b, 0.01, 0.075, 0.000597, 10000, lambda_fine_index=False)
+    # fine index 1 vs coarse index 1 (= fine 10)
+    assert not torch.allclose(a.lam[1], b.lam[1])
+    assert torch.allclose(a.lam[0], b.lam[0])
+
+
+def test_saved_model_roundtrip(tmp_path):
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.engine import current_weights
+    from rphedge.utils.model_io import load_date, save_run
+
+    cfg = parse_params(_small())
+    run = HedgeRun(cfg)
+    res = run.run()
+    save_run(str(tmp_path), run, res)
+    files = sorted(os.listdir(tmp_path))
+    assert "config.json" in files and "report.json" in files and "values.npy" in files
+    assert sum(f.startswith("weights_t") for f in files) == run.paths.n_coarse - 1
+    meta, spec, w, wq, vals = load_date(str(tmp_path), 0)
+    np.testing.assert_allclose(w, current_weights(spec, res.induction.weights_snapshots[0, 0]))
+    assert wq is not None and vals.shape == (run.n_local,)
+    from safetensors.numpy import load_file
+
+    t = load_file(str(tmp_path / "weights_t0000.safetensors"))
+    assert t["LeakyReLU_1/kernel"].shape == (3, 8) and t["Phi_Psi/bias"].shape == (2,)
+    rep = json.load(open(tmp_path / "report.json"))
+    assert abs(rep["phi0"] - res.phi) < 1e-6
+
+
+def test_single_time_step_cpu():
+    from rphedge.experiments import single_time_step
+
+    out = single_time_step(parity=True, n_paths=9, epochs_first=30, device="cpu", verbose=False)
+    assert len(out["VaR_Res1"]) == 3 and len(out["VaR_Res2"]) == 3
+    # Q12: cost of capital 0.1*dt = 1.0 -> the blended (Res2) holdings are the Q99 holdings,
+    # whose 99% VaR is below the MSE holdings' (the hedge sign condition of the notebook)
+    assert out["VaR_Res2_unit"][1] <= out["VaR_Res1_unit"][1] + 1e-3
+
+
+def test_volatility_sweep_rows():
+    from rphedge.experiments import volatility_sweep
+
+    rows = volatility_sweep(sigmas=(0.1, 0.3), n_paths=8, dt=0.1, rebalancing=2.0, epochs_first=10, epochs_rest=3,
+                            verbose=False, device="cpu")
+    assert [r["sigma"] for r in rows] == [0.1, 0.3]
+    assert all(math.isfinite(r["Phi"]) and math.isfinite(r["Psi"]) for r in rows)
+
+
+def test_sanity_checks_match_notebook_values():
+    from rphedge.experiments import mts_parameters, sanity_checks
+
+    out = sanity_checks(mts_parameters(device="cpu", verbose=False))
+    assert out["grid"]["shape"] == [4096, 41]
+    assert abs(out["diff"]) < 0.03                  # "Multi Time Step.ipynb":122-124 (diff 0.0016)
+    assert 8550 < out["N_T"]["mean"] < 8680         # mean 8,615-8,617
+    assert 110 < out["N_T"]["std"] < 160            # std 132-133
+    assert out["nparams"] == 122
+
+
+def test_cir_calibration_recovers_parameters():
+    from rphedge import calib
+
+    rng = np.random.default_rng(3)
+    a, b, c = 0.02, 0.16, 0.01
+    v = [b]
+    for _ in range(20000):
+        v.append(max(v[-1] + a * (b - v[-1]) + c * math.sqrt(v[-1]) * rng.standard_normal(), 1e-4))
+    est = calib.estimate_CIR_params(np.asarray(v))
+    assert est.a == pytest.approx(a, rel=0.3) and est.b == pytest.approx(b, rel=0.05)
+    assert est.c == pytest.approx(c, rel=0.05)
+    with pytest.raises(ValueError):
+        calib.CIRParams(0.001, 0.1, 0.5)     # Feller violated (Q22: message corrected)
+    out = calib.calibrate(calib.synthetic_prices(1500))
+    assert set(out) >= {"mu", "vol0", "a", "b", "c"}
+    assert len(calib.acf(np.random.default_rng(0).standard_normal(500), 10)) == 11
+
+
+def test_brownian_helpers():
+    from rphedge.brownian_motion import get_W, get_dW
+
+    dW = get_dW(50, 1)
+    W = get_W(50, 1)
+    assert dW.shape == (50,) and W[0] == 0.0
+    np.testing.assert_allclose(W[1:], np.cumsum(dW)[:-1])
+
+
+def test_cli_calibrate_and_info():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "rphedge", "calibrate", "--synthetic"], capture_output=True,
+                         text=True, cwd=ROOT, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "vol0" in json.loads(out.stdout)
+    out = subprocess.run([sys.executable, "-m", "rphedge", "info"], capture_output=True, text=True, cwd=ROOT,
+                         env=env, timeout=120)
+    assert out.returncode == 0 and json.loads(out.stdout)["native_loaded"]
+
+
+def test_cli_run_config(tmp_path):
+    cfg = dict(json.load(open(os.path.join(ROOT, "examples", "pension_mts.json"))), n_paths=8, dt=0.1,
+               rebalancing=2.0, epochs_first=5, epochs_rest=2, device="cpu", verbose=False)
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(cfg))
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "rphedge", "run", "--config", str(p), "--out", str(tmp_path / "o")],
+                         capture_output=True, text=True, cwd=ROOT, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr
+    res = json.loads(out.stdout)
+    assert math.isfinite(res["phi0"]) and (tmp_path / "o" / "report.json").exists()
+
+
+def test_reports():
+    import rphedge
+    from rphedge.utils import reports
+
+    res = rphedge.european_option(N_paths=512, rebalancing_frequency=0.25, epochs_first=10, epochs_rest=3,
+                                  verbose=False, device="cpu")
+    v = reports.valuation_report(res, 0.08, 1.0)
+    assert set(v) == {"V0", "discounted_E_payoff", "difference", "difference_pct"}
+    h = reports.holdings_over_time(res)
+    assert len(h) == 4
+    fan = reports.value_fan(res.induction.values)
+    assert fan.shape == (6, 5)
+    cf = reports.pension_closed_form(10000, 100, 10, 0.03, 0.15, 0.8617)
+    assert 8.5e5 < cf[0] < 1.0e6  # SURVEY: ~917,112 EUR
