@@ -106,7 +106,7 @@ class HedgeRun:
     @property
     def scale(self) -> float:
         c = self.cfg
-        return float(c.N * c.P) if self.kind == "pension" else float(c.Y if self.kind == "european" else 1.0)
+        return float(c.N * c.P) if self.kind == "pension" else float(c.Y)
 
     def simulate(self):
         """Paths (K1–K6) and terminal value V_T (K7) on the coarse grid."""
