@@ -266,6 +266,61 @@ RPH_INLINE float ld_agent(const float* p) {
 constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contention / 8)
 
 // ---------------------------------------------------------------------------
+// Fused one-shot all-reduce of the gradient packet over xGMI (data parallel).
+// Runs in the last-arriving workgroup of every rank: push the local packet to
+// every rank's mailbox (IPC-mapped peer HBM, system-scope write-through
+// stores), raise one flag per peer after every storing wave has drained,
+// wait for all peers' flags, then sum the W packets from local HBM in fixed
+// rank order — every rank computes the bitwise-identical sum, so the Adam
+// update and the early-stopping decision are identical everywhere.  The tag is
+// a per-rank device step counter (not a launch argument), so graph replays
+// never see stale flags; DP_SLOTS-deep mailboxes let a fast rank run ahead.
+// Spins are bounded; a timeout sets dp_error (checked by the host).
+// ---------------------------------------------------------------------------
+template <int R>
+RPH_INLINE void dp_allreduce(const TrainDesc& d, float* red) {
+  __shared__ uint32_t s_seq;
+  const int tid = threadIdx.x;
+  const int W = d.dp_world, me = d.dp_rank;
+  if (tid == 0) s_seq = __hip_atomic_load(d.dp_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t seq = s_seq;
+  const int slot = (int)(seq % DP_SLOTS);
+  if (tid < R) {
+    const float v = red[tid];
+    for (int p = 0; p < W; ++p)
+      __hip_atomic_store(d.dp_mbox[p] + ((size_t)slot * W + me) * R + tid, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (tid < W) {
+    __hip_atomic_store(d.dp_flags[tid] + slot * W + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // wait for rank `tid`'s packet in MY mailbox
+    uint32_t* f = d.dp_flags[me] + slot * W + tid;
+    unsigned it = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 23)) {  // ~seconds: a peer never arrived
+        __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < R) {
+    float s = 0.f;
+    for (int p = 0; p < W; ++p)
+      s += __hip_atomic_load(d.dp_mbox[me] + ((size_t)slot * W + p) * R + tid, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    red[tid] = s;
+  }
+  if (tid == 0) __hip_atomic_store(d.dp_counter, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+}
+
+
+// ---------------------------------------------------------------------------
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
 // ---------------------------------------------------------------------------
 template <int NIN, int H, int NO, int HEAD>
@@ -511,12 +566,16 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   __syncthreads();
   RPH_STAMP(6);
 
+  if (d.dp_world > 1) {
+    dp_allreduce<R>(d, red);
+    RPH_STAMP(7);
+  }
   if (d.fused_update) {
     apply_update<P>(red, up, d.wts, d.opt, d.fit, epoch, step, d.steps_per_epoch);
   } else if (threadIdx.x < R) {
     d.grad_out[threadIdx.x] = red[threadIdx.x];
   }
-  RPH_STAMP(7);
+  if (d.dp_world <= 1) RPH_STAMP(7);
 }
 
 // K10 standalone (world_size > 1): one workgroup applies the all-reduced update.

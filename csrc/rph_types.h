@@ -91,7 +91,18 @@ struct TrainDesc {
   float* acc;                    // [8][R] float-atomic accumulator (zeroed; re-armed by last arriver)
   int deterministic;             // 1: fixed-order slab reduction (bitwise reproducible)
   unsigned long long* stamps;    // diagnostic phase stamps [num_wgs][8] (null in production)
+  // Fused data-parallel all-reduce over xGMI peer memory (dp_world > 1):
+  // mailbox of rank p = dp_mbox[p]: [DP_SLOTS][dp_world][R] floats, flags
+  // dp_flags[p]: [DP_SLOTS][dp_world] u32 (IPC-mapped, system-scope accesses).
+  int dp_world;
+  int dp_rank;
+  float* dp_mbox[8];
+  uint32_t* dp_flags[8];
+  uint32_t* dp_counter;          // this rank's step sequence counter (device)
+  uint32_t* dp_error;            // set on a peer timeout (host checks after the run)
 };
+
+constexpr int DP_SLOTS = 4;
 
 struct EvalDesc {
   const float* feat[MAXIN];      // features at t

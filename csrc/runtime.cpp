@@ -49,6 +49,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(TrainDesc, lr_sched), OFF(TrainDesc, slab), OFF(TrainDesc, counter), OFF(TrainDesc, grad_out),
       OFF(TrainDesc, bond), OFF(TrainDesc, inv_batch), OFF(TrainDesc, loss), OFF(TrainDesc, seed),
       OFF(TrainDesc, num_wgs), OFF(TrainDesc, head), OFF(TrainDesc, acc), OFF(TrainDesc, deterministic), OFF(TrainDesc, stamps),
+      OFF(TrainDesc, dp_world), OFF(TrainDesc, dp_mbox), OFF(TrainDesc, dp_flags), OFF(TrainDesc, dp_counter), OFF(TrainDesc, dp_error),
       // EvalDesc
       (long long)sizeof(EvalDesc), OFF(EvalDesc, price_t), OFF(EvalDesc, price_t1), OFF(EvalDesc, target),
       OFF(EvalDesc, wa), OFF(EvalDesc, g_base), OFF(EvalDesc, v_out), OFF(EvalDesc, hold_out),
@@ -160,3 +161,39 @@ extern "C" int rph_nccl_destroy(void* comm) {
   NCCL_TRY(ncclCommDestroy((ncclComm_t)comm));
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// IPC mailboxes for the fused xGMI all-reduce (one allocation per rank,
+// exported with hipIpcGetMemHandle and opened by every peer process).
+// ---------------------------------------------------------------------------
+extern "C" int rph_ipc_alloc(long long bytes, void** ptr_out, char* handle_out /*64 B*/) {
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, (size_t)bytes));
+  HIP_TRY(hipMemset(p, 0, (size_t)bytes));
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, p));
+  memcpy(handle_out, &h, sizeof(h));
+  *ptr_out = p;
+  return (int)sizeof(h);
+}
+
+extern "C" int rph_ipc_open(const char* handle /*64 B*/, void** ptr_out) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  void* p = nullptr;
+  HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  *ptr_out = p;
+  return 0;
+}
+
+extern "C" int rph_ipc_close(void* p) {
+  HIP_TRY(hipIpcCloseMemHandle(p));
+  return 0;
+}
+
+extern "C" int rph_free(void* p) {
+  HIP_TRY(hipFree(p));
+  return 0;
+}
+
+extern "C" int rph_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }

@@ -207,8 +207,13 @@ class HedgeRun:
         tr = c.train
         tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
                            lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs)
+        kw = {}
+        if self.backend_kind == "hip" and self.di.world > 1:
+            self.mailbox = D.make_mailbox(self.di, self.spec.red_width)
+            kw["mailbox"] = self.mailbox
         self.backend = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
-                                    comm=self.di.comm, world=self.di.world, rank=self.di.rank, stream=self.stream)
+                                    comm=self.di.comm, world=self.di.world, rank=self.di.rank, stream=self.stream,
+                                    **kw)
         pf = c.parity
         icfg = InductionConfig(epochs_first=tr.epochs_first, epochs_rest=tr.epochs_rest,
                                patience_first=tr.patience_first, patience_rest=tr.patience_rest,
@@ -306,6 +311,8 @@ class HedgeRun:
         c, w = self.cfg, self.di.world
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+        if getattr(self, "mailbox", None) is not None:
+            self.mailbox.check()
         ind = self.induction.collect()
         scale = self.scale
         h0 = ind.holdings0

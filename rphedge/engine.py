@@ -174,9 +174,10 @@ class HipBackend:
     name = "hip"
 
     def __init__(self, spec: NetSpec, n_local: int, tcfg: TrainConfig, device=None, comm=None,
-                 world: int = 1, rank: int = 0, stream=None):
+                 world: int = 1, rank: int = 0, stream=None, mailbox=None):
         from .ops import native
 
+        self.mailbox = mailbox  # native.IpcMailbox: fused xGMI all-reduce inside the step kernel
         self.native = native
         native.load(required=True)
         self.spec, self.n_local, self.tcfg = spec, int(n_local), tcfg
@@ -242,9 +243,14 @@ class HipBackend:
         d.chunk_log2 = int(self.tcfg.chunk_log2)
         d.shuffle = 1 if self.tcfg.shuffle else 0
         d.seed = int(seed) & 0xFFFFFFFF
-        d.fused_update = 1 if (self.world == 1 and not self.tcfg.split_update) else 0
-        if self.world > 1 and self.comm is None:
-            raise RuntimeError("HipBackend with world_size > 1 needs a native RCCL communicator")
+        fused_dp = self.mailbox is not None and self.world > 1
+        d.fused_update = 1 if ((self.world == 1 or fused_dp) and not self.tcfg.split_update) else 0
+        if self.world > 1 and self.comm is None and not fused_dp:
+            raise RuntimeError("HipBackend with world_size > 1 needs an RCCL communicator or an IPC mailbox")
+        if fused_dp:
+            self.mailbox.fill(d)
+        else:
+            d.dp_world, d.dp_rank = 1, 0
         d.acc = self.acc.data_ptr()
         d.deterministic = 1 if self.tcfg.deterministic else 0
         d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
@@ -265,7 +271,7 @@ class HipBackend:
         for e in range(fcfg.epochs):
             for s in range(S):
                 n.train_step(d, s, e, self.stream)
-                if self.world > 1 or self.tcfg.split_update:
+                if (self.world > 1 and d.fused_update == 0) or self.tcfg.split_update:
                     if self.comm is not None:
                         self.comm.allreduce_(self.grad, self.stream)
                     n.train_update(d, s, e, self.stream)
@@ -510,6 +516,7 @@ def make_backend(kind: str, spec: NetSpec, n_local: int, tcfg: TrainConfig, **kw
     if kind == "hip":
         return HipBackend(spec, n_local, tcfg, **kw)
     kw.pop("stream", None)
+    kw.pop("mailbox", None)
     return TorchBackend(spec, n_local, tcfg, **kw)
 
 

@@ -37,6 +37,8 @@ class TrainDesc(C.Structure):
         ("chunk_log2", C.c_int), ("shuffle", C.c_int), ("seed", C.c_uint32), ("fused_update", C.c_int),
         ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
         ("acc", VP), ("deterministic", C.c_int), ("stamps", VP),
+        ("dp_world", C.c_int), ("dp_rank", C.c_int), ("dp_mbox", VP * 8), ("dp_flags", VP * 8),
+        ("dp_counter", VP), ("dp_error", VP),
     ]
 
 
@@ -78,6 +80,7 @@ def _expected_layout() -> list[int]:
         C.sizeof(T), T.price.offset, T.target.offset, T.wts.offset, T.lr_sched.offset, T.slab.offset,
         T.counter.offset, T.grad_out.offset, T.bond.offset, T.inv_batch.offset, T.loss.offset, T.seed.offset,
         T.num_wgs.offset, T.head.offset, T.acc.offset, T.deterministic.offset, T.stamps.offset,
+        T.dp_world.offset, T.dp_mbox.offset, T.dp_flags.offset, T.dp_counter.offset, T.dp_error.offset,
         C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
         E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
         E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset,
@@ -113,6 +116,11 @@ def _bind(lib):
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
         "rph_payoff": (C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP, C.c_float, VP, VP, VP]),
         "rph_radix_hist": (C.c_int, [VP, C.c_longlong, C.c_uint32, C.c_uint32, C.c_int, C.c_int, VP, VP]),
+        "rph_ipc_alloc": (C.c_int, [C.c_longlong, C.POINTER(VP), C.c_char_p]),
+        "rph_ipc_open": (C.c_int, [C.c_char_p, C.POINTER(VP)]),
+        "rph_ipc_close": (C.c_int, [VP]),
+        "rph_free": (C.c_int, [VP]),
+        "rph_ipc_handle_size": (C.c_int, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -301,3 +309,63 @@ class NcclComm:
         if self.comm is not None:
             _lib.rph_nccl_destroy(self.comm)
             self.comm = None
+
+
+DP_SLOTS = 4
+
+
+class IpcMailbox:
+    """Peer-mapped mailboxes for the fused xGMI gradient all-reduce.
+
+    Every rank hipMallocs ``[DP_SLOTS][W][R]`` floats + ``[DP_SLOTS][W]`` flags,
+    exports an IPC handle through the torch.distributed store and opens every
+    peer's handle.  The step kernel's last-arriving workgroup then writes its
+    packet straight into each peer's HBM over xGMI (no RCCL launch, no extra
+    kernel per step)."""
+
+    def __init__(self, rank: int, world: int, R: int, store, device, tag: str = "rph_mbox"):
+        lib = load(required=True)
+        if world > 8:
+            raise ValueError("fused xGMI all-reduce supports up to 8 ranks (one node)")
+        self.rank, self.world, self.R = rank, world, R
+        data_bytes = DP_SLOTS * world * R * 4
+        self.flag_off = (data_bytes + 255) // 256 * 256
+        nbytes = self.flag_off + DP_SLOTS * world * 4 + 256
+        hs = lib.rph_ipc_handle_size()
+        buf = C.create_string_buffer(hs)
+        p = VP()
+        _check(lib.rph_ipc_alloc(nbytes, C.byref(p), buf), "rph_ipc_alloc")
+        self.own = p.value
+        store.set(f"{tag}_{rank}", bytes(buf.raw[:hs]))
+        self.ptrs, self.opened = [], []
+        for q in range(world):
+            if q == rank:
+                self.ptrs.append(self.own)
+                continue
+            h = store.get(f"{tag}_{q}")
+            pq = VP()
+            _check(lib.rph_ipc_open(h, C.byref(pq)), "rph_ipc_open")
+            self.ptrs.append(pq.value)
+            self.opened.append(pq.value)
+        self.counter = torch.zeros(4, dtype=torch.int32, device=device)
+        self.error = torch.zeros(4, dtype=torch.int32, device=device)
+
+    def fill(self, d: TrainDesc):
+        d.dp_world, d.dp_rank = self.world, self.rank
+        for q in range(self.world):
+            d.dp_mbox[q] = self.ptrs[q]
+            d.dp_flags[q] = self.ptrs[q] + self.flag_off
+        d.dp_counter = self.counter.data_ptr()
+        d.dp_error = self.error.data_ptr()
+
+    def check(self):
+        if int(self.error[0].item()) != 0:
+            raise RuntimeError("fused xGMI all-reduce: a peer rank did not arrive (timeout)")
+
+    def close(self):
+        for p in self.opened:
+            _lib.rph_ipc_close(p)
+        self.opened = []
+        if self.own is not None:
+            _lib.rph_free(self.own)
+            self.own = None

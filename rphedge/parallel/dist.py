@@ -29,6 +29,7 @@ class DistInfo:
     device: torch.device = torch.device("cpu")
     comm: object = None          # native RCCL communicator (HIP path)
     initialized_here: bool = False
+    dp_mode: str = "xgmi"        # xgmi: fused IPC all-reduce in the step kernel; rccl: RCCL + update kernel
 
     @property
     def is_main(self) -> bool:
@@ -63,7 +64,8 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(dev)
-    info = DistInfo(rank=rank, world=world, local_rank=local, device=dev)
+    info = DistInfo(rank=rank, world=world, local_rank=local, device=dev,
+                    dp_mode=os.environ.get("RPH_DP", "xgmi" if world <= 8 else "rccl"))
     if world > 1:
         be = backend or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
@@ -90,6 +92,15 @@ def _store():
     from torch.distributed import distributed_c10d as c10d
 
     return c10d._get_default_store() if hasattr(c10d, "_get_default_store") else dist.distributed_c10d._get_default_store()
+
+
+def make_mailbox(info: DistInfo, R: int, tag: str = "rph_mbox"):
+    """IPC mailbox for the fused xGMI all-reduce (None on 1 rank / CPU / rccl mode)."""
+    if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
+        return None
+    from ..ops.native import IpcMailbox
+
+    return IpcMailbox(info.rank, info.world, R, _store(), info.device, tag=tag)
 
 
 def shard(n_total: int, world: int, rank: int) -> tuple[int, int]:

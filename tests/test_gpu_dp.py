@@ -1,0 +1,83 @@
+"""Data parallelism on ONE MI355X: two processes share the card and run the
+fused xGMI/IPC all-reduce inside the step kernel (the 8-GPU path minus the
+links).  Full-batch GD makes the DP result comparable with one process."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n, dev, lo=0, cnt=None):
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(n, generator=g) * 0.6 + 0.7
+    cnt = n if cnt is None else cnt
+    f = x[lo:lo + cnt].to(dev)
+    return f, f * 1.01, torch.relu(f * 1.01 - 1.0)
+
+
+def _fit(rank, world, n, epochs, dev, mailbox=None, deterministic=True):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    per = n // world
+    f, p1, y = _data(n, dev, rank * per, per)
+    tc = TrainConfig(batch_size=n, chunk_log2=6, lr=1e-2, shuffle=False, deterministic=deterministic)
+    be = HipBackend(spec, per, tc, device=dev, world=world, rank=rank, mailbox=mailbox)
+    data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f])
+    w, o, fs = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+    be.fit(w, o, fs, data, FitConfig(epochs=epochs, patience=10 ** 6, early_stopping=False), seed=3)
+    torch.cuda.synchronize()
+    return current_weights(spec, w), fs.cpu().numpy()
+
+
+def _worker(rank, world, port, n, epochs, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from torch.distributed import distributed_c10d as c10d
+
+    from rphedge.ops.native import IpcMailbox
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mb = IpcMailbox(rank, world, 128, c10d._get_default_store(), dev, tag="t_dp")
+    dist.barrier()
+    w, fs = _fit(rank, world, n, epochs, dev, mailbox=mb)
+    mb.check()
+    np.save(out + f".{rank}.npy", w)
+    dist.barrier()
+    mb.close()
+    dist.destroy_process_group()
+
+
+def test_fused_xgmi_allreduce_two_ranks_one_gpu():
+    n, epochs, world = 1 << 15, 6, 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "w")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, n, epochs, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    assert np.array_equal(w0, w1)                      # bitwise-identical replicas
+    ref, _ = _fit(0, 1, n, epochs, torch.device("cuda", 0))
+    np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-5)
