@@ -174,7 +174,7 @@ extern "C" int rph_ipc_alloc(long long bytes, void** ptr_out, char* handle_out /
   HIP_TRY(hipIpcGetMemHandle(&h, p));
   memcpy(handle_out, &h, sizeof(h));
   *ptr_out = p;
-  return (int)sizeof(h);
+  return 0;
 }
 
 extern "C" int rph_ipc_open(const char* handle /*64 B*/, void** ptr_out) {
