@@ -526,11 +526,11 @@ def reduce_stats(stats: torch.Tensor, world: int = 1) -> np.ndarray:
     mn = stats[:, L.ES_RESMIN].min()
     mx = stats[:, L.ES_RESMAX].max()
     if world > 1:
-        import torch.distributed as dist
+        from .parallel.dist import all_reduce_
 
-        dist.all_reduce(s)
-        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        all_reduce_(s)
+        all_reduce_(mn, "min")
+        all_reduce_(mx, "max")
     s = s.detach().cpu().numpy().copy()
     s[L.ES_RESMIN] = float(mn)
     s[L.ES_RESMAX] = float(mx)

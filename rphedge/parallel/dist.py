@@ -67,7 +67,7 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
     info = DistInfo(rank=rank, world=world, local_rank=local, device=dev,
                     dp_mode=os.environ.get("RPH_DP", "xgmi" if world <= 8 else "rccl"))
     if world > 1:
-        be = backend or ("nccl" if use_gpu else "gloo")
+        be = backend or os.environ.get("RPH_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {}
@@ -76,7 +76,7 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
             dist.init_process_group(be, timeout=datetime.timedelta(seconds=timeout_s), **kw)
             info.initialized_here = True
         info.backend = be
-        if use_gpu and native_comm:
+        if use_gpu and native_comm and info.dp_mode == "rccl":
             from ..ops.native import NcclComm
 
             store = _store()
@@ -119,11 +119,18 @@ def barrier():
 
 
 def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """In-place all-reduce; device tensors go through the host when the
+    process group is gloo (single-GPU multi-rank rehearsals)."""
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-        dist.all_reduce(t, op=o)
+        if t.is_cuda and dist.get_backend() == "gloo":
+            h = t.detach().cpu()
+            dist.all_reduce(h, op=o)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=o)
     return t
 
 

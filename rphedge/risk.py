@@ -37,9 +37,9 @@ def _hist_pass(x: torch.Tensor, pmask: int, prefix: int, shift: int, nbins: int,
         h = torch.from_numpy(np.bincount(((k[sel] >> np.uint32(shift)) & np.uint32(nbins - 1)).astype(np.int64),
                                          minlength=nbins).astype(np.int32))
     if world > 1:
-        import torch.distributed as dist
+        from .parallel.dist import all_reduce_
 
-        dist.all_reduce(h)
+        all_reduce_(h)
     return h.cpu().numpy().astype(np.int64)
 
 
@@ -86,12 +86,12 @@ def describe(x: torch.Tensor, scale: float = 1.0, world: int = 1) -> dict:
     s = torch.stack([xd.sum(), (xd * xd).sum()])
     mn, mx = xd.min().reshape(1), xd.max().reshape(1)
     if world > 1:
-        import torch.distributed as dist
+        from .parallel.dist import all_reduce_
 
-        dist.all_reduce(n)
-        dist.all_reduce(s)
-        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        all_reduce_(n)
+        all_reduce_(s)
+        all_reduce_(mn, "min")
+        all_reduce_(mx, "max")
     N = float(n.item())
     mean = float(s[0].item()) / N
     var = max(float(s[1].item()) / N - mean * mean, 0.0) * N / max(N - 1, 1)
