@@ -298,6 +298,43 @@ class HedgeRun:
     def replay(self):
         self.graph.replay(self.stream or torch.cuda.current_stream(self.device))
 
+    def resume(self, out_dir: str, date: int) -> RunResult:
+        """Restart the backward scan at ``date-1`` from a saved run directory
+        (weights of ``date`` as the warm start, Q18, and ``values[date]``).
+        Adam moments restart from zero (Keras does not persist them either)."""
+        from .utils.model_io import load_date
+
+        if self.induction is None:
+            self.build()
+        ind = self.induction
+        _, spec, w, wq, vals = load_date(out_dir, date)
+        assert spec.nparams == self.spec.nparams, "saved network shape differs from this configuration"
+        set_weights(self.spec, ind.w_init, w)
+        if wq is not None and ind.cfg.q99 and not ind.cfg.shared_q99_model:
+            self._wq_resume = wq
+        if vals is None:
+            raise ValueError("values.npy missing: cannot resume the backward induction")
+        t0 = time.perf_counter()
+        ind.values[date].copy_(torch.from_numpy(vals).to(ind.values.device))
+        ind.w_mse.copy_(ind.w_init)
+        ind.opt_mse.copy_(ind.opt_init)
+        if ind.cfg.q99:
+            if not ind.cfg.shared_q99_model:
+                ind.w_q.copy_(ind.w_init)
+                if getattr(self, "_wq_resume", None) is not None:
+                    set_weights(self.spec, ind.w_q, self._wq_resume)
+            ind.opt_q.copy_(ind.opt_init)
+        # the first resumed date is NOT the reference's "first" date (no LR schedule)
+        orig = ind._fcfg
+        ind._fcfg = lambda first, loss: orig(False, loss)
+        try:
+            ind.enqueue(start=date - 1)
+        finally:
+            ind._fcfg = orig
+        res = self.collect()
+        res.timings["wall_s"] = time.perf_counter() - t0
+        return res
+
     def run(self) -> RunResult:
         t0 = time.perf_counter()
         if self.induction is None:

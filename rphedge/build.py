@@ -47,7 +47,10 @@ def _digest(extra: str) -> str:
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = False, debug: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, debug: bool = False, asan: bool = False) -> Path:
+    """Compile csrc/ for gfx950.  ``asan`` builds a host-AddressSanitizer variant
+    (``librphedge_asan.so``; device code is not instrumented — GPU ASan is not
+    available on this pool) for host-side race/memory debugging."""
     LIBDIR.mkdir(parents=True, exist_ok=True)
     flags = [
         f"--offload-arch={ARCH}",
@@ -62,28 +65,33 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False) -> Pa
     ]
     if debug:
         flags += ["-g", "-DRPH_DEBUG=1"]
+    lib, stamp = LIB, STAMP
+    if asan:
+        flags += ["-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+        lib, stamp = LIBDIR / "librphedge_asan.so", LIBDIR / "librphedge_asan.sha256"
     digest = _digest(" ".join(flags))
-    if not force and LIB.exists() and STAMP.exists() and STAMP.read_text().strip() == digest:
-        return LIB
-    tmp = LIB.with_suffix(".so.tmp")
+    if not force and lib.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return lib
+    tmp = lib.with_suffix(".so.tmp")
     cmd = [_hipcc(), *flags, *[str(s) for s in sources()], "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
-    os.replace(tmp, LIB)
-    STAMP.write_text(digest)
-    return LIB
+    os.replace(tmp, lib)
+    stamp.write_text(digest)
+    return lib
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host AddressSanitizer variant")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
-    lib = build(force=a.force, verbose=a.verbose, debug=a.debug)
+    lib = build(force=a.force, verbose=a.verbose, debug=a.debug, asan=a.asan)
     print(lib)
     return 0
 

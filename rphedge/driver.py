@@ -142,10 +142,15 @@ class BackwardInduction:
         return DateData(feats=p.features(t), prices_next=p.prices(t + 1), bond_next=float(p.bond[t + 1]),
                         target=self.values[t + 1], prices_now=p.prices(t), bond_now=float(p.bond[t]))
 
-    def enqueue(self):
+    def enqueue(self, start: int | None = None):
+        """Enqueue dates ``start, start-1, ..., 0`` (default: all, from n-2).
+        Resume restarts at ``start = i-1`` after loading the
+        weights and ``values[i]`` of a saved date i."""
         c, be = self.cfg, self.backend
         nc = self.paths.n_coarse
-        for t in range(nc - 2, -1, -1):
+        start = nc - 2 if start is None else int(start)
+        self.ran = list(range(start, -1, -1))
+        for t in self.ran:
             first = t == nc - 2
             data = self.date_data(t)
             if not c.warm_start and not first:
@@ -181,7 +186,7 @@ class BackwardInduction:
         dtc = self.paths.grid.dt_coarse
         res = InductionResult(values=self.values, holdings=self.holdings, residuals=self.residuals,
                               weights_snapshots=self.snap)
-        for t in range(nc - 2, -1, -1):
+        for t in getattr(self, "ran", range(nc - 2, -1, -1)):
             f_m, f_q = self.fits[t]
             s_m, s_q = self.stats[t]
             d = DateResult(index=t, time=t * dtc, fit_mse=fit_summary(f_m),

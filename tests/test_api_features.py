@@ -189,3 +189,43 @@ def test_reports():
     assert fan.shape == (6, 5)
     cf = reports.pension_closed_form(10000, 100, 10, 0.03, 0.15, 0.8617)
     assert 8.5e5 < cf[0] < 1.0e6  # SURVEY: ~917,112 EUR
+
+
+def test_resume_from_saved_date(tmp_path):
+    """Checkpoint/resume: a run restarted at date i from the saved weights and
+    values reproduces the dates < i of the uninterrupted run (CPU backend is
+    deterministic)."""
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.utils.model_io import save_run
+
+    p = _small(rebalancing=2.0, shuffle=False, q99=False)
+    run = HedgeRun(parse_params(p))
+    full = run.run()
+    save_run(str(tmp_path), run, full)
+    i = 3
+    run2 = HedgeRun(parse_params(p))
+    res = run2.resume(str(tmp_path), i)
+    assert [d.index for d in res.induction.dates] == list(range(i - 1, -1, -1))
+    assert math.isfinite(res.phi) and math.isfinite(res.v0)
+    assert res.v0 == pytest.approx(full.v0, rel=0.05)
+
+
+def test_nan_gradient_guard_cpu():
+    """Fault injection: a NaN target poisons the gradient -> the update is
+    skipped and counted, weights stay finite."""
+    from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    n = 1024
+    x = torch.linspace(0.8, 1.2, n)
+    y = torch.relu(x - 1)
+    y[5] = float("nan")
+    be = TorchBackend(spec, n, TrainConfig(batch_size=256, shuffle=False))
+    w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, DateData(feats=[x], prices_next=[x], bond_next=1.0, target=y, prices_now=[x]),
+           FitConfig(epochs=3, patience=100, early_stopping=False), seed=1)
+    assert np.all(np.isfinite(current_weights(spec, w)))
+    assert float(o[L.O_NAN]) == 3.0   # one poisoned batch per epoch

@@ -340,3 +340,24 @@ def test_rccl_comm_split_update_and_graph_capture(dev):
         comm.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_nan_gradient_guard_gpu(dev):
+    """Fault injection on device: NaN gradients -> update skipped + counted."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    n = 1 << 14
+    x = torch.linspace(0.8, 1.2, n, device=dev)
+    y = torch.relu(x - 1)
+    y[5] = float("nan")
+    be = HipBackend(spec, n, TrainConfig(batch_size=4096, shuffle=False), device=dev)
+    w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, DateData(feats=[x], prices_next=[x], bond_next=1.0, target=y, prices_now=[x]),
+           FitConfig(epochs=3, patience=100, early_stopping=False), seed=1)
+    torch.cuda.synchronize()
+    assert np.all(np.isfinite(current_weights(spec, w)))
+    assert float(o[L.O_NAN].item()) == 3.0
+    assert float(o[L.O_T].item()) == 9.0   # 12 steps, 3 skipped
