@@ -50,6 +50,8 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=2e-2)
     ap.add_argument("--lr-rest", type=float, default=4e-3)
     ap.add_argument("--lr-decay", type=float, default=0.02, help="per-date geometric LR decay factor (last/first epoch)")
+    ap.add_argument("--hidden", type=int, default=8, help="hidden width (8 = reference net; 32 = MFMA kernel)")
+    ap.add_argument("--mfma-precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -63,7 +65,7 @@ def build_run(a, world: int):
     tr = TrainingParams(batch_size=(1 << a.batch_log2) * world, epochs_first=a.epochs_first,
                         epochs_rest=a.epochs_rest, patience_first=10 ** 6, patience_rest=10 ** 6,
                         lr=a.lr, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
-                        chunk_log2=6, seed=1234)
+                        chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision)
     cfg = RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
                     dt=1.0 / a.dates, n_paths=a.paths_log2 + int(math.log2(world)), payoff="call",
                     option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0, keep_paths=False,
@@ -160,9 +162,9 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": value / BASELINE_SAMPLES_PER_S,
-        "dtype": "fp32",
+        "dtype": "fp32" if (a.hidden == 8 or a.mfma_precision == "fp32") else "bf16",
         "data": "synthetic (Sobol-QMC GBM paths generated on device; random-init N(0,0.1) weights)",
-        "config": {"model": "hedge-MLP 1-8-8-2 (LeakyReLU 0.3), European call S0=K=100 r=0.08 sigma=0.15 T=1",
+        "config": {"model": f"hedge-MLP 1-{a.hidden}-{a.hidden}-2 (LeakyReLU 0.3), European call S0=K=100 r=0.08 sigma=0.15 T=1",
                    "global_batch": cfg.train.batch_size, "seq_len": n_dates,
                    "parallelism": f"dp{world}", "paths_global": n_total, "paths_per_gpu": run.n_local,
                    "epochs_first": a.epochs_first, "epochs_rest": a.epochs_rest,

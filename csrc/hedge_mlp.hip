@@ -20,305 +20,9 @@
 //   * world_size > 1: the slab sum goes to grad_out, RCCL all-reduces it on
 //     the same stream and k_hedge_update applies the identical update on every
 //     rank (bitwise-identical decisions => identical early stopping).
-#include "rph_common.h"
-#include "rph_types.h"
+#include "hedge_core.h"
 
 namespace rph {
-
-// Diagnostic phase stamps (s_memrealtime, 100 MHz): thread 0 of every
-// workgroup writes stamp k to d.stamps[blockIdx.x * 8 + k] when d.stamps is set.
-#define RPH_STAMP(k)                                                                    \
-  do {                                                                                  \
-    if (d.stamps != nullptr && threadIdx.x == 0)                                        \
-      d.stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
-  } while (0)
-
-template <int NIN, int H, int NO, int HEAD>
-struct NetShape {
-  static constexpr int NHOLD = (HEAD == HEAD_COMPLEMENT) ? 2 : NO;
-  static constexpr int OW1 = 0;
-  static constexpr int OB1 = OW1 + NIN * H;
-  static constexpr int OW2 = OB1 + H;
-  static constexpr int OB2 = OW2 + H * H;
-  static constexpr int OW3 = OB2 + H;
-  static constexpr int OB3 = OW3 + H * NO;
-  static constexpr int P = OB3 + NO;
-  static constexpr int NSTAT = 4;  // loss, |e|, |e|/|y|, count
-  static constexpr int R = (P + NSTAT <= 128) ? 128 : 256;
-  static_assert(P <= PMAX, "network too large for PMAX");
-  static_assert(NHOLD <= MAXHOLD, "too many holdings");
-};
-
-// ---------------------------------------------------------------------------
-// K11: bijective chunk permutation for Keras-style per-epoch shuffling.  Paths
-// are permuted in chunks of 2^chunk_log2 (64 => one coalesced wave load); the
-// permutation is a keyed affine/xorshift bijection on the next power of two
-// with cycle-walking, so nothing is materialised.
-// ---------------------------------------------------------------------------
-struct Perm {
-  uint32_t mask, n, k1, a1, b1, a2, b2, sh;
-  int on;
-  RPH_INLINE uint32_t f(uint32_t x) const {
-    x = (((x ^ k1) * a1) + b1) & mask;
-    x ^= x >> sh;
-    x = ((x * a2) + b2) & mask;
-    return x;
-  }
-  RPH_INLINE uint32_t operator()(uint32_t x) const {
-    if (!on) return x;
-    x = f(x);
-    while (x >= n) x = f(x);
-    return x;
-  }
-};
-
-__host__ __device__ inline Perm make_perm(uint32_t n_chunks, uint32_t seed, uint32_t epoch, bool on) {
-  Perm p;
-  uint32_t m = 1;
-  int bits = 0;
-  while (m < n_chunks) { m <<= 1; ++bits; }
-  p.mask = m - 1u;
-  p.n = n_chunks;
-  const u32x4 r = philox4x32_10({epoch, 0x5eedu, 0u, 0u}, seed, 0xC0FFEEu);
-  const u32x4 s = philox4x32_10({epoch, 0x5eedu, 1u, 0u}, seed, 0xC0FFEEu);
-  p.k1 = r.x & p.mask;
-  p.a1 = (r.y | 1u);
-  p.b1 = r.z;
-  p.a2 = (r.w | 1u);
-  p.b2 = s.x;
-  p.sh = bits > 1 ? (uint32_t)(bits / 2) : 1u;
-  p.on = (on && n_chunks > 1) ? 1 : 0;
-  return p;
-}
-
-// ---------------------------------------------------------------------------
-// Forward pass of one path (fp32).  W is wave-uniform.
-// ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD>
-RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], float alpha,
-                            float (&z1)[H], float (&a1)[H], float (&z2)[H], float (&a2)[H],
-                            float (&hold)[NetShape<NIN, H, NO, HEAD>::NHOLD]) {
-  using S = NetShape<NIN, H, NO, HEAD>;
-#pragma unroll
-  for (int j = 0; j < H; ++j) {
-    float acc = W[S::OB1 + j];
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], W[S::OW1 + f * H + j], acc);
-    z1[j] = acc;
-    a1[j] = lrelu(acc, alpha);
-  }
-#pragma unroll
-  for (int j = 0; j < H; ++j) {
-    float acc = W[S::OB2 + j];
-#pragma unroll
-    for (int i = 0; i < H; ++i) acc = fmaf(a1[i], W[S::OW2 + i * H + j], acc);
-    z2[j] = acc;
-    a2[j] = lrelu(acc, alpha);
-  }
-  float o[NO];
-#pragma unroll
-  for (int k = 0; k < NO; ++k) {
-    float acc = W[S::OB3 + k];
-#pragma unroll
-    for (int j = 0; j < H; ++j) acc = fmaf(a2[j], W[S::OW3 + j * NO + k], acc);
-    o[k] = acc;
-  }
-  if (HEAD == HEAD_COMPLEMENT) {  // EO: psi = 1 - phi  ("European Options.ipynb" cell 12)
-    hold[0] = o[0];
-    hold[1] = 1.0f - o[0];
-  } else {
-#pragma unroll
-    for (int k = 0; k < S::NHOLD; ++k) hold[k] = o[k];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Adam + EarlyStopping + LR schedule (K10).  Runs in ONE workgroup of 256
-// threads, weights updated IN PLACE (every other workgroup of the launch has
-// already passed the arrival ticket, i.e. finished reading them).  gsum (LDS)
-// holds the summed gradient [P] followed by the 4 loss statistics.
-// Keras 2.x semantics:
-//   lr_t = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
-//   w -= lr_t*m/(sqrt(v)+eps)
-// EarlyStopping.on_epoch_end: wait+=1; if loss<best: best=loss, save, wait=0;
-//   if wait>=patience and epoch>0: stop (+restore best).
-// ---------------------------------------------------------------------------
-// Optimizer/early-stop state prefetched by EVERY workgroup at kernel start, so
-// the last arriver can apply the update without another memory round trip.
-struct UpdPre {
-  float m, v, w, wbest;                 // this thread's parameter (tid < P)
-  float t, lr, b1, b2, eps, nan_steps;
-  float loss_sum, abs_sum, ape_sum, loss_cnt;
-  float wait, has_best, best_loss, patience, max_epochs, restore_best, restore_at_end;
-  float lr_sched_e;                     // lr_sched[epoch] (NaN if none)
-};
-
-template <int P>
-RPH_INLINE void prefetch_update(UpdPre& u, const NetWeights* wts, const OptState* opt, const FitState* fs,
-                                const float* lr_sched, int epoch, int step) {
-  const int tid = threadIdx.x;
-  if (tid < P) {
-    u.m = opt->m[tid];
-    u.v = opt->v[tid];
-    u.w = wts->w[0][tid];
-    u.wbest = fs->w_best[tid];
-  } else {
-    u.m = u.v = u.w = u.wbest = 0.f;
-  }
-  u.t = opt->t; u.lr = opt->lr; u.b1 = opt->beta1; u.b2 = opt->beta2; u.eps = opt->eps;
-  u.nan_steps = opt->nan_steps;
-  u.loss_sum = fs->loss_sum; u.abs_sum = fs->abs_sum; u.ape_sum = fs->ape_sum; u.loss_cnt = fs->loss_cnt;
-  u.wait = fs->wait; u.has_best = fs->has_best; u.best_loss = fs->best_loss; u.patience = fs->patience;
-  u.max_epochs = fs->max_epochs; u.restore_best = fs->restore_best; u.restore_at_end = fs->restore_at_end;
-  u.lr_sched_e = (step == 0 && lr_sched != nullptr) ? lr_sched[epoch] : __builtin_nanf("");
-}
-
-// ---------------------------------------------------------------------------
-// Adam + EarlyStopping + LR schedule (K10).  Runs in ONE workgroup of 256
-// threads, weights updated IN PLACE (every other workgroup of the launch has
-// already passed the arrival ticket, i.e. finished reading them).  gsum (LDS)
-// holds the summed gradient [P] followed by the 4 loss statistics.
-// Keras 2.x semantics:
-//   lr_t = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
-//   w -= lr_t*m/(sqrt(v)+eps)
-// EarlyStopping.on_epoch_end: wait+=1; if loss<best: best=loss, save, wait=0;
-//   if wait>=patience and epoch>0: stop (+restore best).
-// ---------------------------------------------------------------------------
-template <int P>
-RPH_INLINE void apply_update(const float* gsum, const UpdPre& u, NetWeights* wts, OptState* opt, FitState* fs,
-                             int epoch, int step, int steps_per_epoch) {
-  const int tid = threadIdx.x;
-  const bool mine = tid < P;
-  const float g = mine ? gsum[tid] : 0.f;
-  const float lr = (u.lr_sched_e == u.lr_sched_e) ? u.lr_sched_e : u.lr;  // on_epoch_begin (NaN => keep)
-  const int finite = __syncthreads_and(mine ? (int)__builtin_isfinite(g) : 1);  // NaN/Inf guard
-  const float t = u.t + (finite ? 1.f : 0.f);
-  // b^t = exp2(t log2 b) on the transcendental unit (v_log/v_exp, ~1 ulp)
-  const float bc1 = 1.f - __builtin_amdgcn_exp2f(t * __builtin_amdgcn_logf(u.b1));
-  const float bc2 = 1.f - __builtin_amdgcn_exp2f(t * __builtin_amdgcn_logf(u.b2));
-  const float lr_t = lr * sqrtf(bc2) * __frcp_rn(bc1);
-  float wnew = u.w;
-  if (mine && finite) {
-    const float m = u.m + (g - u.m) * (1.f - u.b1);
-    const float v = u.v + (g * g - u.v) * (1.f - u.b2);
-    opt->m[tid] = m;
-    opt->v[tid] = v;
-    wnew = u.w - lr_t * m * __frcp_rn(sqrtf(v) + u.eps);
-  }
-  // epoch bookkeeping: computed redundantly by every thread from the prefetched
-  // (uniform) state — no extra barrier; thread 0 persists it.
-  const float loss_sum = u.loss_sum + gsum[P + 0];
-  const float abs_sum = u.abs_sum + gsum[P + 1];
-  const float ape_sum = u.ape_sum + gsum[P + 2];
-  const float loss_cnt = u.loss_cnt + gsum[P + 3];
-  int act = 0;
-  if (step == steps_per_epoch - 1) {
-    const float cnt = fmaxf(loss_cnt, 1.f);
-    const float L = loss_sum * __frcp_rn(cnt);
-    float wait = u.wait + 1.f, best = u.best_loss, stopped = 0.f;
-    if (L < best || u.has_best == 0.f) {
-      if (L < best) { best = L; wait = 0.f; }
-      act = 1;
-    }
-    if (wait >= u.patience && epoch > 0) {
-      stopped = 1.f;
-      if (u.restore_best != 0.f) act = 2;
-    }
-    if ((float)(epoch + 1) >= u.max_epochs && stopped == 0.f) {
-      stopped = 1.f;
-      if (u.restore_best != 0.f && u.restore_at_end != 0.f) act = 2;
-    }
-    if (tid == 0) {
-      if (epoch < MAXHIST) fs->hist[epoch] = L;
-      fs->last_loss = L;
-      fs->last_mae = abs_sum * __frcp_rn(cnt);
-      fs->last_mape = 100.f * ape_sum * __frcp_rn(cnt);
-      fs->loss_sum = fs->abs_sum = fs->ape_sum = fs->loss_cnt = 0.f;
-      fs->wait = wait;
-      fs->best_loss = best;
-      fs->has_best = 1.f;
-      fs->epoch = (float)(epoch + 1);
-      fs->stopped = stopped;
-    }
-  } else if (tid == 0) {
-    fs->loss_sum = loss_sum;
-    fs->abs_sum = abs_sum;
-    fs->ape_sum = ape_sum;
-    fs->loss_cnt = loss_cnt;
-  }
-  if (tid == 0) {
-    opt->lr = lr;
-    opt->t = t;
-    if (!finite) opt->nan_steps = u.nan_steps + 1.f;
-  }
-  if (mine) {
-    if (act == 1) fs->w_best[tid] = wnew;
-    wts->w[0][tid] = (act == 2) ? u.wbest : wnew;
-  }
-}
-
-// agent-scope (sc1) 4-byte accesses for the cross-workgroup hand-off
-RPH_INLINE void st_agent(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-RPH_INLINE float ld_agent(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contention / 8)
-
-// ---------------------------------------------------------------------------
-// Fused one-shot all-reduce of the gradient packet over xGMI (data parallel).
-// Runs in the last-arriving workgroup of every rank: push the local packet to
-// every rank's mailbox (IPC-mapped peer HBM, system-scope write-through
-// stores), raise one flag per peer after every storing wave has drained,
-// wait for all peers' flags, then sum the W packets from local HBM in fixed
-// rank order — every rank computes the bitwise-identical sum, so the Adam
-// update and the early-stopping decision are identical everywhere.  The tag is
-// a per-rank device step counter (not a launch argument), so graph replays
-// never see stale flags; DP_SLOTS-deep mailboxes let a fast rank run ahead.
-// Spins are bounded; a timeout sets dp_error (checked by the host).
-// ---------------------------------------------------------------------------
-template <int R>
-RPH_INLINE void dp_allreduce(const TrainDesc& d, float* red) {
-  __shared__ uint32_t s_seq;
-  const int tid = threadIdx.x;
-  const int W = d.dp_world, me = d.dp_rank;
-  if (tid == 0) s_seq = __hip_atomic_load(d.dp_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  __syncthreads();
-  const uint32_t seq = s_seq;
-  const int slot = (int)(seq % DP_SLOTS);
-  if (tid < R) {
-    const float v = red[tid];
-    for (int p = 0; p < W; ++p)
-      __hip_atomic_store(d.dp_mbox[p] + ((size_t)slot * W + me) * R + tid, v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-  __syncthreads();
-  if (tid < W) {
-    __hip_atomic_store(d.dp_flags[tid] + slot * W + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    // wait for rank `tid`'s packet in MY mailbox
-    uint32_t* f = d.dp_flags[me] + slot * W + tid;
-    unsigned it = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 23)) {  // ~seconds: a peer never arrived
-        __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < R) {
-    float s = 0.f;
-    for (int p = 0; p < W; ++p)
-      s += __hip_atomic_load(d.dp_mbox[me] + ((size_t)slot * W + p) * R + tid, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-    red[tid] = s;
-  }
-  if (tid == 0) __hip_atomic_store(d.dp_counter, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-}
-
 
 // ---------------------------------------------------------------------------
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
@@ -341,7 +45,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   RPH_STAMP(0);
   const float stopped = d.fit->stopped;
   const float wv = threadIdx.x < P ? d.wts->w[0][threadIdx.x] : 0.f;
-  UpdPre up;
+  UpdPre<P> up;
   if (d.fused_update) prefetch_update<P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
 
   const int lane = threadIdx.x & 63;
@@ -380,7 +84,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   // broadcast ds_read_b128 (keeps the 100+ weights out of the SGPR file).
   if (threadIdx.x < P) wl[threadIdx.x] = wv;
   if (d.fused_update) {  // keep the prefetch here (the compiler would sink it into the last-arriver branch)
-    asm volatile("" ::"v"(up.m), "v"(up.v), "v"(up.w), "v"(up.wbest), "s"(up.t), "s"(up.lr), "s"(up.loss_sum),
+    asm volatile("" ::"v"(up.m[0]), "v"(up.v[0]), "v"(up.w[0]), "v"(up.wbest[0]), "s"(up.t), "s"(up.lr), "s"(up.loss_sum),
                  "s"(up.wait), "s"(up.best_loss), "s"(up.lr_sched_e));
   }
   __syncthreads();
@@ -578,19 +282,6 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   if (d.dp_world <= 1) RPH_STAMP(7);
 }
 
-// K10 standalone (world_size > 1): one workgroup applies the all-reduced update.
-template <int NIN, int H, int NO, int HEAD>
-__global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const int step, const int epoch) {
-  using S = NetShape<NIN, H, NO, HEAD>;
-  __shared__ float gs[S::R + 8];
-  if (d.fit->stopped != 0.f) return;
-  UpdPre up;
-  prefetch_update<S::P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
-  for (int i = threadIdx.x; i < S::R; i += blockDim.x) gs[i] = d.grad_out[i];
-  __syncthreads();
-  apply_update<S::P>(gs, up, d.wts, d.opt, d.fit, epoch, step, d.steps_per_epoch);
-}
-
 // ---------------------------------------------------------------------------
 // K12: value / holdings / residual epilogue of a backward-induction date.
 //   V_t       = h(state_t) . p_t           (Keras predict(X0), RP:212)
@@ -721,9 +412,6 @@ using namespace rph;
   X(5, 8, 6, HEAD_FREE)          \
   X(6, 8, 7, HEAD_FREE)
 
-static inline bool shape_is(int nin, int h, int nout, int head, int a, int b, int c, int e) {
-  return nin == a && h == b && nout == c && head == e;
-}
 
 extern "C" int rph_net_nparams(int nin, int h, int nout, int head, int* p_out, int* r_out) {
 #define X(A, B, C, E)                                  \
@@ -733,6 +421,7 @@ extern "C" int rph_net_nparams(int nin, int h, int nout, int head, int* p_out, i
     return 0;                                          \
   }
   RPH_SHAPES(X)
+  RPH_WIDE_SHAPES(X)
 #undef X
   return -1;
 }
@@ -748,17 +437,19 @@ extern "C" int rph_train_step(const TrainDesc* d, int step, int epoch, void* str
   }
   RPH_SHAPES(X)
 #undef X
-  return -1;
+  return launch_wide_step(d, step, epoch, perm, s);
 }
 
 extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* stream) {
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
-    hipLaunchKernelGGL((k_hedge_update<A, B, C, E>), dim3(1), dim3(256), 0, s, *d, step, epoch); \
+    using S = NetShape<A, B, C, E>;                                                          \
+    hipLaunchKernelGGL((k_hedge_update<S::P, S::R>), dim3(1), dim3(256), 0, s, *d, step, epoch); \
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)
+  RPH_WIDE_SHAPES(X)
 #undef X
   return -1;
 }
@@ -771,6 +462,7 @@ extern "C" int rph_eval(const EvalDesc* d, void* stream) {
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)
+  RPH_WIDE_SHAPES(X)
 #undef X
   return -1;
 }

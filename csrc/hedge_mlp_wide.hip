@@ -1,0 +1,436 @@
+// rphedge — fused training step for 32-unit hedge MLPs on the matrix cores
+// (K9-wide, gfx950).
+//
+// Same contract as k_hedge_train_step (hedge_mlp.hip): one launch = one Keras
+// optimizer step (forward + loss + backward + gradient reduction + Adam +
+// EarlyStopping bookkeeping in the last-arriving workgroup), reference
+// semantics Replicating_Portfolio.py:149-221.  With 32 hidden units the
+// 32x32 middle layer is GEMM-shaped — three products per minibatch tile:
+//
+//   Z2ᵀ  = W2ᵀ · A1ᵀ     forward           (32 units x 32 paths, K = 32 units)
+//   dA1ᵀ = W2  · dZ2ᵀ    backward          (32 units x 32 paths, K = 32 units)
+//   dW2  = A1ᵀ · dZ2     weight gradient   (32 x 32, K = 32 paths per tile)
+//
+// all on v_mfma_f32_32x32x16_bf16 (2 MFMAs each, fp32 accumulate) or, with
+// d.mfma_fp32, on v_mfma_f32_32x32x2_f32 (exact fp32, 16 MFMAs each).
+//
+// Layout (one wave = one 32-path tile at a time; lane l: path r = l&31 of the
+// tile, lane half h = l>>5):
+//   * every activation lives in the 32x32 MFMA accumulator layout: lane (r,h)
+//     register q holds unit  unit_of(q,h) = (q&3) + 8(q>>2) + 4h  of path r.
+//     Layer 1 (K = nin) is computed by VALU directly in that layout, so the
+//     forward and backward layer-2 products take their B operand straight
+//     from registers (bf16 k-order = the permuted unit order; the W2 operand
+//     fragments are built once per launch in the matching order) — no LDS;
+//   * dW2 sums over PATHS (the lane index), so a1 and dz2 go through a per-wave
+//     LDS transpose image ([unit][path], 80-byte rows) read back as ds_read_b128
+//     MFMA fragments, accumulating in 16 registers across all tiles;
+//   * the small gradients (W1, b1, b2, W3, b3) and the loss statistics are
+//     accumulated per lane in registers and reduced once per launch with a
+//     32-lane reduce-scatter (the two lane halves hold different units);
+//   * the per-workgroup packet [P grads | 4 stats | pad] (R = multiple of 256
+//     floats) goes through the same ticketed hand-off as the narrow kernel
+//     (float-atomic replicas or deterministic slab), optional fused xGMI
+//     all-reduce, and Adam applied in place by the last arriver.
+#include "hedge_core.h"
+
+namespace rph {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int WH = 32;         // hidden width handled by this kernel
+constexpr int IMG_PITCH = 40;  // bf16 per row of the transpose images (80 B rows)
+constexpr int IMG_PITCH32 = 33;
+
+// unit held in accumulator register q by lane half h (32x32 C/D layout)
+RPH_INLINE constexpr int unit_of(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
+
+template <bool F32>
+struct WFrag;
+template <>
+struct WFrag<false> { bf16x8 f[2]; };
+template <>
+struct WFrag<true> { float f[16]; };
+
+// A-operand fragments of a 32x32 layer product whose k index runs over units
+// in accumulator order.  TR=false: element(row r, unit u) = W2[u][r] (W2ᵀ);
+// TR=true: W2[r][u].
+template <bool F32, bool TR>
+RPH_INLINE void load_wfrag(WFrag<F32>& w, const float* __restrict__ W2, int r, int h) {
+  if constexpr (F32) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = unit_of(q, h);
+      w.f[q] = TR ? W2[r * WH + u] : W2[u * WH + r];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = unit_of(8 * s + j, h);
+        w.f[s][j] = (__bf16)(TR ? W2[r * WH + u] : W2[u * WH + r]);
+      }
+  }
+}
+
+// Y[row][path] = Σ_u A[row][u] X[u][path] with X in accumulator layout
+// (x[q] = X[unit_of(q,h)][r]); the result is again in accumulator layout.
+template <bool F32>
+RPH_INLINE f32x16 layer_mfma(const WFrag<F32>& w, const float (&x)[16]) {
+  f32x16 acc = {};
+  if constexpr (F32) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.f[q], x[q], acc, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = (__bf16)x[8 * s + j];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.f[s], b, acc, 0, 0, 0);
+    }
+  }
+  return acc;
+}
+
+// dW2 += A1ᵀ · dZ2 over the 32 paths of the tile (transpose through LDS).
+template <bool F32>
+RPH_INLINE void outer_mfma(void* img, const float (&a1)[16], const float (&dz2)[16], int r, int h, f32x16& acc) {
+  if constexpr (F32) {
+    float* IA = (float*)img;
+    float* IB = IA + WH * IMG_PITCH32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      IA[unit_of(q, h) * IMG_PITCH32 + r] = a1[q];
+      IB[unit_of(q, h) * IMG_PITCH32 + r] = dz2[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(IA[r * IMG_PITCH32 + 2 * s + h], IB[r * IMG_PITCH32 + 2 * s + h],
+                                                 acc, 0, 0, 0);
+  } else {
+    __bf16* IA = (__bf16*)img;
+    __bf16* IB = IA + WH * IMG_PITCH;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      IA[unit_of(q, h) * IMG_PITCH + r] = (__bf16)a1[q];
+      IB[unit_of(q, h) * IMG_PITCH + r] = (__bf16)dz2[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 a = *(const bf16x8*)(IA + r * IMG_PITCH + 16 * s + 8 * h);
+      const bf16x8 b = *(const bf16x8*)(IB + r * IMG_PITCH + 16 * s + 8 * h);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+  }
+  // the next tile rewrites the images: its writes must follow these reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-lane register vector of the small gradients (units of this lane half)
+template <int NIN, int NO>
+struct SmallGrad {
+  static constexpr int DW1 = 0;
+  static constexpr int DB1 = DW1 + 16 * NIN;
+  static constexpr int DB2 = DB1 + 16;
+  static constexpr int DW3 = DB2 + 16;
+  static constexpr int DB3 = DW3 + 16 * NO;
+  static constexpr int ST = DB3 + NO;
+  static constexpr int NV = ST + 4;
+  static constexpr int RV = NV <= 64 ? 64 : NV <= 128 ? 128 : 256;
+  static_assert(NV <= 256, "small-gradient vector too long");
+};
+
+// packet index of small-gradient entry idx held by lane half h (-1: none)
+template <int NIN, int NO, int P>
+RPH_INLINE int small_param(int idx, int h) {
+  using G = SmallGrad<NIN, NO>;
+  using S = NetShape<NIN, WH, NO, HEAD_FREE>;  // offsets do not depend on the head
+  if (idx < G::DB1) return S::OW1 + (idx / 16) * WH + unit_of(idx % 16, h);
+  if (idx < G::DB2) return S::OB1 + unit_of(idx - G::DB1, h);
+  if (idx < G::DW3) return S::OB2 + unit_of(idx - G::DB2, h);
+  if (idx < G::DB3) {
+    const int t = idx - G::DW3;
+    return S::OW3 + unit_of(t / NO, h) * NO + (t % NO);
+  }
+  if (h != 0) return -1;  // path-level entries are accumulated by lane half 0 only
+  if (idx < G::ST) return S::OB3 + (idx - G::DB3);
+  if (idx < G::NV) return P + (idx - G::ST);
+  return -1;
+}
+
+// 32-lane reduce-scatter (bits 4..0): lane (r, h) ends with the half-wave sum
+// of entries [r*RV/32, (r+1)*RV/32) in v[0 .. RV/32).
+template <int RV>
+RPH_INLINE void half_reduce_scatter(float* v, int lane) {
+  halve_step<RV, 4>(v, lane);
+  halve_step<RV / 2, 3>(v, lane);
+  halve_step<RV / 4, 2>(v, lane);
+  halve_step<RV / 8, 1>(v, lane);
+  halve_step<RV / 16, 0>(v, lane);
+}
+
+template <int NIN, int NO, int HEAD, bool F32>
+__global__ __launch_bounds__(256) void k_hedge_train_step_wide(const TrainDesc d, const int step, const int epoch,
+                                                               const Perm perm) {
+  using S = NetShape<NIN, WH, NO, HEAD>;
+  using G = SmallGrad<NIN, NO>;
+  constexpr int P = S::P;
+  constexpr int R = S::R;  // packet width, multiple of 256
+  constexpr int NR = R / 256;
+  constexpr int NHOLD = S::NHOLD;
+  constexpr int RV = G::RV;
+  constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * IMG_PITCH * 2;
+  constexpr int SCR_BYTES = (4 * IMG_BYTES > 4 * R * 4) ? 4 * IMG_BYTES : 4 * R * 4;
+  static_assert(R % 256 == 0, "wide packet must be a multiple of 256");
+  __shared__ __attribute__((aligned(16))) unsigned char scratch[SCR_BYTES];
+  __shared__ __attribute__((aligned(16))) float wl[P + 4];
+  __shared__ int s_last;
+
+  RPH_STAMP(0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const float stopped = d.fit->stopped;
+  const float* __restrict__ Wg = d.wts->w[0];
+  UpdPre<P> up;
+  if (d.fused_update) prefetch_update<P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
+  WFrag<F32> w2t, w2;
+  load_wfrag<F32, false>(w2t, Wg + S::OW2, r, h);
+  load_wfrag<F32, true>(w2, Wg + S::OW2, r, h);
+  for (int i = tid; i < P; i += 256) wl[i] = Wg[i];
+
+  const int nwaves = gridDim.x * 4;
+  const int gw = blockIdx.x * 4 + wid;
+  const long long base = (long long)step * d.batch;
+  const int ntiles = (d.batch + 31) >> 5;
+
+  auto load_path = [&](int T, float (&x)[NIN], float (&pr)[NHOLD], float& y, bool& valid) {
+    const long long jl = (long long)T * 32 + r;
+    const long long j = base + jl;
+    valid = (jl < d.batch) && (j < d.n_local);
+    const uint32_t p = valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) x[f] = valid ? d.feat[f][p] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = valid ? d.price[k][p] : 0.f;
+    pr[NHOLD - 1] = d.bond;
+    y = valid ? d.target[p] : 0.f;
+  };
+  int T = gw;
+  float xn[NIN], prn[NHOLD], yn = 0.f;
+  bool validn = false;
+  if (T < ntiles) load_path(T, xn, prn, yn, validn);
+
+  if (stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
+  if (d.fused_update) {
+    asm volatile("" ::"v"(up.m[0]), "v"(up.v[0]), "v"(up.w[0]), "v"(up.wbest[0]), "s"(up.t), "s"(up.lr),
+                 "s"(up.loss_sum), "s"(up.wait), "s"(up.best_loss), "s"(up.lr_sched_e));
+  }
+  __syncthreads();
+  RPH_STAMP(1);
+
+  void* img = scratch + wid * IMG_BYTES;
+  float g[RV];
+#pragma unroll
+  for (int i = 0; i < RV; ++i) g[i] = 0.f;
+  f32x16 gw2 = {};
+  const float alpha = d.alpha;
+  const float hv0 = (h == 0) ? 1.f : 0.f;
+
+  for (; T < ntiles; T += nwaves) {
+    float x[NIN], pr[NHOLD];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) x[f] = xn[f];
+#pragma unroll
+    for (int k = 0; k < NHOLD; ++k) pr[k] = prn[k];
+    const float y = yn;
+    const bool valid = validn;
+    if (T + nwaves < ntiles) load_path(T + nwaves, xn, prn, yn, validn);
+
+    // ---- forward ----------------------------------------------------------
+    float z1[16], a1[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = unit_of(q, h);
+      float acc = wl[S::OB1 + u];
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], wl[S::OW1 + f * WH + u], acc);
+      z1[q] = acc;
+      a1[q] = lrelu(acc, alpha);
+    }
+    const f32x16 z2acc = layer_mfma<F32>(w2t, a1);
+    float z2[16], a2[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      z2[q] = z2acc[q] + wl[S::OB2 + unit_of(q, h)];
+      a2[q] = lrelu(z2[q], alpha);
+    }
+    float o[NO];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc = fmaf(a2[q], wl[S::OW3 + unit_of(q, h) * NO + k], acc);
+      o[k] = acc + __shfl_xor(acc, 32, 64) + wl[S::OB3 + k];  // both halves: full sum over 32 units
+    }
+    float hold[NHOLD];
+    if (HEAD == HEAD_COMPLEMENT) {
+      hold[0] = o[0];
+      hold[1] = 1.f - o[0];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) hold[k] = o[k];
+    }
+    float V = 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
+    float l, dV;
+    path_loss(d.loss, d.quantile, V, y, l, dV);
+    dV = valid ? dV * d.inv_batch : 0.f;
+    const float hv = valid ? hv0 : 0.f;  // path-level statistics: lane half 0 only
+    const float ae = fabsf(V - y);
+    g[G::ST + 0] = fmaf(hv, l, g[G::ST + 0]);
+    g[G::ST + 1] = fmaf(hv, ae, g[G::ST + 1]);
+    g[G::ST + 2] = fmaf(hv, ae / fmaxf(fabsf(y), 1e-7f), g[G::ST + 2]);
+    g[G::ST + 3] += hv;
+
+    // ---- backward ---------------------------------------------------------
+    float dout[NO];
+    if (HEAD == HEAD_COMPLEMENT) {
+      dout[0] = dV * (pr[0] - pr[1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NO; ++k) g[G::DB3 + k] = fmaf(hv0, dout[k], g[G::DB3 + k]);
+    float dz2[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = unit_of(q, h);
+      float da = 0.f;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        g[G::DW3 + q * NO + k] = fmaf(a2[q], dout[k], g[G::DW3 + q * NO + k]);
+        da = fmaf(wl[S::OW3 + u * NO + k], dout[k], da);
+      }
+      dz2[q] = da * lrelu_d(z2[q], alpha);
+      g[G::DB2 + q] += dz2[q];
+    }
+    const f32x16 da1 = layer_mfma<F32>(w2, dz2);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float dz1 = da1[q] * lrelu_d(z1[q], alpha);
+      g[G::DB1 + q] += dz1;
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) g[G::DW1 + f * 16 + q] = fmaf(x[f], dz1, g[G::DW1 + f * 16 + q]);
+    }
+    outer_mfma<F32>(img, a1, dz2, r, h, gw2);
+  }
+  RPH_STAMP(2);
+
+  // ---- per-wave packet -> LDS, cross-wave sum ---------------------------------
+  half_reduce_scatter<RV>(g, lane);
+  __syncthreads();  // every wave is done with its transpose image (aliases the packet)
+  float* pk = (float*)scratch;
+  float* pkw = pk + wid * R;
+  for (int i = P + 4 + lane; i < R; i += 64) pkw[i] = 0.f;
+  constexpr int PER = RV / 32;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int prm = small_param<NIN, NO, P>(r * PER + i, h);
+    if (prm >= 0) pkw[prm] = g[i];
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) pkw[S::OW2 + unit_of(q, h) * WH + r] = gw2[q];
+  __syncthreads();
+  float val[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const int i = tid + 256 * k;
+    val[k] = (pk[i] + pk[R + i]) + (pk[2 * R + i] + pk[3 * R + i]);
+  }
+  __syncthreads();
+  RPH_STAMP(3);
+
+  if (gridDim.x > 1) {
+    const int Gn = gridDim.x;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int i = tid + 256 * k;
+      if (d.deterministic) st_agent(d.slab + (size_t)blockIdx.x * R + i, val[k]);
+      else __hip_atomic_fetch_add(d.acc + (blockIdx.x % ACC_REPLICAS) * R + i, val[k], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+    __syncthreads();
+    RPH_STAMP(4);
+    if (tid == 0) {
+      const uint32_t ticket = __hip_atomic_fetch_add(d.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = (ticket == (uint32_t)Gn - 1u) ? 1 : 0;
+    }
+    __syncthreads();
+    RPH_STAMP(5);
+    if (!s_last) return;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int i = tid + 256 * k;
+      float a = 0.f;
+      if (d.deterministic) {
+        // fixed combine order => bitwise reproducible
+        for (int row = 0; row < Gn; ++row) a += ld_agent(d.slab + (size_t)row * R + i);
+      } else {
+        float rr[ACC_REPLICAS];
+#pragma unroll
+        for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(d.acc + rp * R + i);
+        a = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+#pragma unroll
+        for (int rp = 0; rp < ACC_REPLICAS; ++rp) st_agent(d.acc + rp * R + i, 0.f);  // re-arm
+      }
+      val[k] = a;
+    }
+    if (tid == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  float* red = pk;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) red[tid + 256 * k] = val[k];
+  __syncthreads();
+  RPH_STAMP(6);
+  if (d.dp_world > 1) dp_allreduce<R>(d, red);
+  if (d.fused_update) {
+    apply_update<P>(red, up, d.wts, d.opt, d.fit, epoch, step, d.steps_per_epoch);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) d.grad_out[tid + 256 * k] = red[tid + 256 * k];
+  }
+  RPH_STAMP(7);
+}
+
+int launch_wide_step(const TrainDesc* d, int step, int epoch, const Perm& perm, hipStream_t s) {
+#define X(A, B, C, E)                                                                                   \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                          \
+    if (d->mfma_fp32)                                                                                   \
+      hipLaunchKernelGGL((k_hedge_train_step_wide<A, C, E, true>), dim3(d->num_wgs), dim3(256), 0, s, *d, \
+                         step, epoch, perm);                                                            \
+    else                                                                                                \
+      hipLaunchKernelGGL((k_hedge_train_step_wide<A, C, E, false>), dim3(d->num_wgs), dim3(256), 0, s, *d, \
+                         step, epoch, perm);                                                            \
+    return (int)hipGetLastError();                                                                      \
+  }
+  RPH_WIDE_SHAPES(X)
+#undef X
+  return -1;
+}
+
+}  // namespace rph

@@ -9,7 +9,7 @@
 
 namespace rph {
 
-constexpr int PMAX = 256;      // max flat parameters per hedge network
+constexpr int PMAX = 2048;     // max flat parameters per hedge network
 constexpr int MAXIN = 8;       // max input features
 constexpr int MAXHOLD = 8;     // max hedging instruments (assets + bond)
 constexpr int MAXHIST = 1024;  // per-fit epoch-loss history
@@ -100,6 +100,7 @@ struct TrainDesc {
   uint32_t* dp_flags[8];
   uint32_t* dp_counter;          // this rank's step sequence counter (device)
   uint32_t* dp_error;            // set on a peer timeout (host checks after the run)
+  int mfma_fp32;                 // 32-unit nets: exact fp32 MFMA (32x32x2) instead of bf16 (32x32x16)
 };
 
 constexpr int DP_SLOTS = 4;

@@ -90,18 +90,19 @@ class HedgeRun:
     def _spec(self) -> hm.NetSpec:
         c = self.cfg
         alpha = c.train.leaky_alpha
+        hid = int(c.train.hidden)
         if self.kind == "european":
             if c.model == "heston":
-                return hm.NetSpec(nin=2, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+                return hm.NetSpec(nin=2, hidden=hid, nout=2, head=L.HEAD_FREE, alpha=alpha)
             if c.parity.complement_head:
-                return hm.NetSpec(nin=1, hidden=8, nout=1, head=L.HEAD_COMPLEMENT, alpha=alpha,
+                return hm.NetSpec(nin=1, hidden=hid, nout=1, head=L.HEAD_COMPLEMENT, alpha=alpha,
                                   layer_names=("LeakyReLU_1", "LeakyReLU_2", "Phi"))
-            return hm.NetSpec(nin=1, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+            return hm.NetSpec(nin=1, hidden=hid, nout=2, head=L.HEAD_FREE, alpha=alpha)
         if self.kind == "basket":
-            return hm.NetSpec(nin=c.n_assets, hidden=8, nout=c.n_assets + 1, head=L.HEAD_FREE, alpha=alpha)
+            return hm.NetSpec(nin=c.n_assets, hidden=hid, nout=c.n_assets + 1, head=L.HEAD_FREE, alpha=alpha)
         if c.model in ("sv_ref", "heston") and not c.mortality:
-            return hm.NetSpec(nin=2, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
-        return hm.NetSpec(nin=3, hidden=8, nout=2, head=L.HEAD_FREE, alpha=alpha)
+            return hm.NetSpec(nin=2, hidden=hid, nout=2, head=L.HEAD_FREE, alpha=alpha)
+        return hm.NetSpec(nin=3, hidden=hid, nout=2, head=L.HEAD_FREE, alpha=alpha)
 
     @property
     def scale(self) -> float:
@@ -206,7 +207,8 @@ class HedgeRun:
         self.w0 = self.init_weights(self.stats0) if w0 is None else w0
         tr = c.train
         tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
-                           lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs)
+                           lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs,
+                           mfma_fp32=str(tr.mfma_precision).lower() == "fp32")
         kw = {}
         if self.backend_kind == "hip" and self.di.world > 1:
             self.mailbox = D.make_mailbox(self.di, self.spec.red_width)

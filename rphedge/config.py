@@ -67,6 +67,8 @@ class TrainingParams:
     poll_every: int = 0              # host early-stop polling (0 = fully async / graph)
     deterministic: bool = False      # fixed-order gradient reduction (bitwise reproducible)
     max_wgs: int = 256               # workgroups per training step
+    hidden: int = 8                  # hidden width: 8 = reference nets (VALU kernel), 32 = MFMA kernel
+    mfma_precision: str = "bf16"     # 32-unit nets: "bf16" (32x32x16 MFMA) or "fp32" (exact 32x32x2 MFMA)
 
 
 @dataclass

@@ -75,6 +75,7 @@ class TrainConfig:
     paths_per_thread: int = 1      # target work per thread per step
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
+    mfma_fp32: bool = False        # 32-unit nets: exact fp32 MFMA instead of bf16 operands
 
 
 @dataclass
@@ -253,6 +254,7 @@ class HipBackend:
             d.dp_world, d.dp_rank = 1, 0
         d.acc = self.acc.data_ptr()
         d.deterministic = 1 if self.tcfg.deterministic else 0
+        d.mfma_fp32 = 1 if self.tcfg.mfma_fp32 else 0
         d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
         d.num_wgs = self.num_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head

@@ -59,7 +59,8 @@ class NetSpec:
 
     @property
     def red_width(self) -> int:
-        return 128 if self.nparams + 4 <= 128 else 256
+        n = self.nparams + 4  # mirrors NetShape::R (csrc/hedge_core.h)
+        return 128 if n <= 128 else 256 if n <= 256 else ((n + 255) // 256) * 256
 
     def shapes(self) -> list[tuple[str, tuple]]:
         h, nin, no = self.hidden, self.nin, self.nout

@@ -1,7 +1,7 @@
 """Float-index layout of the device state blocks (mirror of csrc/rph_types.h).
 
 Checked against the native library at load time (``rph_layout``)."""
-PMAX = 256
+PMAX = 2048
 MAXHIST = 1024
 EVAL_NSTAT = 32
 

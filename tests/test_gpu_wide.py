@@ -1,0 +1,92 @@
+"""32-unit hedge MLPs on the MFMA training-step kernel (csrc/hedge_mlp_wide.hip)
+vs the fp32 torch reference backend (autograd + Keras-Adam, same minibatch
+permutation).
+
+* ``mfma_fp32``: v_mfma_f32_32x32x2_f32 (exact fp32 products, different
+  summation order) -> weights match to fp32 reassociation noise;
+* bf16 (default): v_mfma_f32_32x32x16_bf16 operands -> loss history and fitted
+  values match to bf16 rounding of activations/gradients.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_kernels import _fit_pair, dev  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+
+WIDE = [(1, 32, 2, 0), (3, 32, 2, 0), (1, 32, 1, 1), (2, 32, 2, 0), (5, 32, 6, 0)]
+
+
+@pytest.mark.parametrize("shape", WIDE)
+def test_wide_fp32_mfma_matches_torch(dev, shape):  # noqa: F811
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    nin, h, nout, head = shape
+    spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE,
+                                                                   mfma_fp32=True)
+    assert og[L.O_T] == oc[L.O_T] == 16
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
+    np.testing.assert_allclose(wg, wc, rtol=3e-3, atol=3e-4)
+    np.testing.assert_allclose(vg, vc, rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.parametrize("shape", WIDE)
+def test_wide_bf16_mfma_matches_torch(dev, shape):  # noqa: F811
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    nin, h, nout, head = shape
+    spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE)
+    assert og[L.O_T] == oc[L.O_T] == 16
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=3e-2)
+    # fitted values: bf16 operand rounding only
+    scale = np.abs(vc).mean()
+    assert np.abs(vg - vc).mean() < 2e-2 * scale
+    assert np.corrcoef(vg, vc)[0, 1] > 0.999
+
+
+@pytest.mark.parametrize("det,split", [(False, False), (True, False), (False, True)])
+def test_wide_multi_wg_pinball(dev, det, split):  # noqa: F811
+    """Many workgroups (ticketed hand-off of the 1280-float packet), pinball
+    loss, 64-path chunk shuffle, deterministic slab / standalone update."""
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=3, hidden=32, nout=2, head=0)
+    (wc, oc, fc, *_), (wg, og, fg, *_) = _fit_pair(dev, spec, 1 << 17, 1 << 16, 3, L.LOSS_PINBALL, chunk_log2=6,
+                                                   deterministic=det, split_update=split, mfma_fp32=True)
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 3], fc[L.F_HIST:L.F_HIST + 3], rtol=1e-3)
+    np.testing.assert_allclose(wg, wc, rtol=3e-3, atol=3e-4)
+
+
+def test_wide_deterministic_bitwise(dev):  # noqa: F811
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=1, hidden=32, nout=2, head=0)
+    a = _fit_pair(dev, spec, 1 << 16, 1 << 15, 2, L.LOSS_MSE, chunk_log2=6, deterministic=True)[1]
+    b = _fit_pair(dev, spec, 1 << 16, 1 << 15, 2, L.LOSS_MSE, chunk_log2=6, deterministic=True)[1]
+    assert np.array_equal(a[0], b[0])
+    assert np.array_equal(a[3], b[3])
+
+
+def test_wide_european_end_to_end(dev):  # noqa: F811
+    """Full backward induction with a 1-32-32-2 net on the bf16 MFMA kernel:
+    V0 and phi0 near Black-Scholes (same budget as the 8-unit test)."""
+    from rphedge.api import HedgeRun
+    from rphedge.config import ParityFlags, RunConfig, TrainingParams
+
+    tr = TrainingParams(batch_size=1 << 14, epochs_first=60, epochs_rest=15, early_stopping=False, q99=False,
+                        lr_schedule_first=False, chunk_log2=6, lr=5e-3, hidden=32)
+    cfg = RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1 / 12, dt=1 / 12,
+                    n_paths=18, payoff="call", option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0,
+                    keep_paths=True, verbose=False, train=tr, parity=ParityFlags())
+    run = HedgeRun(cfg)
+    assert run.spec.hidden == 32
+    res = run.run()
+    assert abs(res.v0 - 10.3896) < 0.35, res.v0
+    assert abs(res.phi - 0.7285) < 0.06, res.phi
