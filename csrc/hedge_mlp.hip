@@ -21,8 +21,131 @@
 //     the same stream and k_hedge_update applies the identical update on every
 //     rank (bitwise-identical decisions => identical early stopping).
 #include "hedge_core.h"
+#include "hedge_fit.h"
 
 namespace rph {
+
+// ---------------------------------------------------------------------------
+// Per-workgroup gradient packet of one minibatch step, thread-per-path VALU
+// (the reference's 8-unit nets).  Used by the per-step kernel below and by the
+// persistent per-fit kernel (hedge_fit.h).
+// ---------------------------------------------------------------------------
+template <int NIN, int H, int NO, int HEAD>
+struct NarrowBody {
+  using S = NetShape<NIN, H, NO, HEAD>;
+  static constexpr int P = S::P;
+  static constexpr int R = S::R;
+  static constexpr int NR = (R + 255) / 256;  // packet entries per thread (1)
+  static constexpr int NHOLD = S::NHOLD;
+  static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
+  struct Frags {};  // (weights are read from LDS)
+  struct Pre {      // first path of the step, loaded ahead by the caller
+    float x[NIN], pr[NHOLD], y;
+    bool valid;
+  };
+
+  RPH_INLINE static void make_frags(const float*, Frags&) {}
+
+  RPH_INLINE static long long first(int wid) { return (long long)(blockIdx.x * 4 + wid) * 64; }
+
+  RPH_INLINE static void load(const TrainDesc& d, int step, const Perm& perm, long long j0, int lane, Pre& p) {
+    const long long jl = j0 + lane;
+    const long long j = (long long)step * d.batch + jl;
+    p.valid = (jl < d.batch) && (j < d.n_local);
+    const uint32_t q = p.valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) p.x[f] = p.valid ? d.feat[f][q] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = p.valid ? d.price[k][q] : 0.f;
+    p.pr[NHOLD - 1] = d.bond;
+    p.y = p.valid ? d.target[q] : 0.f;
+  }
+
+  // W: weights in LDS; lds: SCRATCH_FLOATS of LDS; pre: the first path (loaded).
+  // Returns in val[0] (threads < R) the workgroup sum of packet entry tid.
+  RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
+                                 const Frags&, float* lds, Pre& pre, float (&val)[NR]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const long long stride = (long long)gridDim.x * 4 * 64;
+    float g[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) g[i] = 0.f;
+    const float alpha = d.alpha;
+    for (long long j0 = first(wid); j0 < d.batch; j0 += stride) {
+      // (loop-invariant LDS weights are hoisted into registers by the compiler;
+      // re-reading them per iteration to reach 2 waves/SIMD measured slower)
+      const float* __restrict__ Wi = W;
+      float x[NIN], pr[NHOLD];
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) x[f] = pre.x[f];
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) pr[k] = pre.pr[k];
+      const float y = pre.y;
+      const bool valid = pre.valid;
+      if (j0 + stride < d.batch) load(d, step, perm, j0 + stride, lane, pre);  // software pipelining
+
+      float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
+      net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold);
+      float V = 0.f;
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
+      float l, dV;
+      path_loss(d.loss, d.quantile, V, y, l, dV);  // dL/dV (mean over the global batch below)
+      dV = valid ? dV * d.inv_batch : 0.f;
+      const float ae = fabsf(V - y);
+      g[P + 0] += valid ? l : 0.f;
+      g[P + 1] += valid ? ae : 0.f;
+      g[P + 2] += valid ? ae / fmaxf(fabsf(y), 1e-7f) : 0.f;
+      g[P + 3] += valid ? 1.f : 0.f;
+
+      // backward
+      float dout[NO];
+      if (HEAD == HEAD_COMPLEMENT) {
+        dout[0] = dV * (pr[0] - pr[1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k];
+      float dz2[H];
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        float da = 0.f;
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          g[S::OW3 + j * NO + k] = fmaf(a2[j], dout[k], g[S::OW3 + j * NO + k]);
+          da = fmaf(Wi[S::OW3 + j * NO + k], dout[k], da);
+        }
+        dz2[j] = da * lrelu_d(z2[j], alpha);
+        g[S::OB2 + j] += dz2[j];
+      }
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        float da = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
+          da = fmaf(Wi[S::OW2 + i * H + j], dz2[j], da);
+        }
+        const float dz1 = da * lrelu_d(z1[i], alpha);
+        g[S::OB1 + i] += dz1;
+#pragma unroll
+        for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
+      }
+    }
+    RPH_STAMP(2);
+    // ---- in-wave reduce-scatter, cross-wave LDS sum ------------------------
+    wave_reduce_scatter<R>(g, lane);
+    constexpr int PER = R / 64;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
+    __syncthreads();
+    const int t = threadIdx.x;
+    val[0] = (t < R) ? (lds[t] + lds[R + t]) + (lds[2 * R + t] + lds[3 * R + t]) : 0.f;
+    __syncthreads();
+  }
+};
 
 // ---------------------------------------------------------------------------
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.
@@ -30,11 +153,10 @@ namespace rph {
 template <int NIN, int H, int NO, int HEAD>
 __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, const int step, const int epoch,
                                                           const Perm perm) {
-  using S = NetShape<NIN, H, NO, HEAD>;
-  constexpr int R = S::R;
-  constexpr int P = S::P;
-  constexpr int NHOLD = S::NHOLD;
-  __shared__ __attribute__((aligned(16))) float lds[(4 * R > 1024 ? 4 * R : 1024) + 8];
+  using B = NarrowBody<NIN, H, NO, HEAD>;
+  constexpr int R = B::R;
+  constexpr int P = B::P;
+  __shared__ __attribute__((aligned(16))) float lds[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ int s_last;
 
@@ -47,37 +169,10 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   const float wv = threadIdx.x < P ? d.wts->w[0][threadIdx.x] : 0.f;
   UpdPre<P> up;
   if (d.fused_update) prefetch_update<P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
-
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int nwaves = gridDim.x * 4;
-  const int gw = blockIdx.x * 4 + wid;
-
-  const uint32_t cmask = (1u << d.chunk_log2) - 1u;  // perm keys come from the host (launch argument)
-  const long long base = (long long)step * d.batch;
-
-  // path data of iteration `it` (software-pipelined one iteration ahead)
-  auto load_path = [&](long long j0, float (&x)[NIN], float (&pr)[NHOLD], float& y, bool& valid) {
-    const long long jl = j0 + lane;
-    const long long j = base + jl;
-    valid = (jl < d.batch) && (j < d.n_local);
-    uint32_t p = 0;
-    if (valid) {
-      const uint32_t ju = (uint32_t)j;
-      p = (perm(ju >> d.chunk_log2) << d.chunk_log2) | (ju & cmask);
-      if (p >= (uint32_t)d.n_local) p = ju;  // (only when n_local is not chunk-aligned)
-    }
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = valid ? d.feat[f][p] : 0.f;
-#pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = valid ? d.price[k][p] : 0.f;
-    pr[NHOLD - 1] = d.bond;
-    y = valid ? d.target[p] : 0.f;
-  };
-  long long j0 = (long long)gw * 64;
-  float xn[NIN], prn[NHOLD], yn = 0.f;
-  bool validn = false;
-  if (j0 < d.batch) load_path(j0, xn, prn, yn, validn);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  typename B::Pre pre;
+  pre.valid = false;
+  if (B::first(wid) < d.batch) B::load(d, step, perm, B::first(wid), lane, pre);
 
   if (stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
   // Weights are wave-uniform: stage them once in LDS and read them as
@@ -89,101 +184,10 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   }
   __syncthreads();
   RPH_STAMP(1);
-  const float* __restrict__ W = wl;
-
-  float g[R];
-#pragma unroll
-  for (int i = 0; i < R; ++i) g[i] = 0.f;
-
-  const float alpha = d.alpha;
-  for (; j0 < d.batch; j0 += (long long)nwaves * 64) {
-    // (loop-invariant LDS weights are hoisted into registers by the compiler;
-    // re-reading them per iteration to reach 2 waves/SIMD measured slower)
-    const float* __restrict__ Wi = W;
-    float x[NIN], pr[NHOLD];
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = xn[f];
-#pragma unroll
-    for (int k = 0; k < NHOLD; ++k) pr[k] = prn[k];
-    const float y = yn;
-    const bool valid = validn;
-    const long long jnext = j0 + (long long)nwaves * 64;
-    if (jnext < d.batch) load_path(jnext, xn, prn, yn, validn);
-
-    float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
-    net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold);
-    float V = 0.f;
-#pragma unroll
-    for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
-
-    // loss + dL/dV (mean over the global batch)
-    const float e = V - y;
-    float l, dV;
-    if (d.loss == LOSS_PINBALL) {
-      const float ep = -e;  // y - V
-      const float q = d.quantile;
-      const bool pos = q * ep >= (q - 1.f) * ep;
-      l = pos ? q * ep : (q - 1.f) * ep;
-      dV = pos ? -q : (1.f - q);
-    } else {
-      l = e * e;
-      dV = 2.f * e;
-    }
-    dV = valid ? dV * d.inv_batch : 0.f;
-    const float ae = fabsf(e);
-    g[P + 0] += valid ? l : 0.f;
-    g[P + 1] += valid ? ae : 0.f;
-    g[P + 2] += valid ? ae / fmaxf(fabsf(y), 1e-7f) : 0.f;
-    g[P + 3] += valid ? 1.f : 0.f;
-
-    // backward
-    float dout[NO];
-    if (HEAD == HEAD_COMPLEMENT) {
-      dout[0] = dV * (pr[0] - pr[1]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k];
-    float dz2[H];
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-      float da = 0.f;
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        g[S::OW3 + j * NO + k] = fmaf(a2[j], dout[k], g[S::OW3 + j * NO + k]);
-        da = fmaf(Wi[S::OW3 + j * NO + k], dout[k], da);
-      }
-      dz2[j] = da * lrelu_d(z2[j], alpha);
-      g[S::OB2 + j] += dz2[j];
-    }
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      float da = 0.f;
-#pragma unroll
-      for (int j = 0; j < H; ++j) {
-        g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
-        da = fmaf(Wi[S::OW2 + i * H + j], dz2[j], da);
-      }
-      const float dz1 = da * lrelu_d(z1[i], alpha);
-      g[S::OB1 + i] += dz1;
-#pragma unroll
-      for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
-    }
-  }
-
-  RPH_STAMP(2);
-  // ---- in-wave reduce-scatter, cross-wave LDS sum --------------------------
-  wave_reduce_scatter<R>(g, lane);
-  constexpr int PER = R / 64;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
-  __syncthreads();
-  float* red = lds;  // reuse: red[t] for t < R after the sum below
-  float val = 0.f;
-  if (threadIdx.x < R) val = lds[threadIdx.x] + lds[R + threadIdx.x] + lds[2 * R + threadIdx.x] + lds[3 * R + threadIdx.x];
-  __syncthreads();
+  float vv[1];
+  B::partial(d, step, perm, wl, typename B::Frags{}, lds, pre, vv);
+  float val = vv[0];
+  float* red = lds;  // reuse: red[t] for t < R after the hand-off below
   RPH_STAMP(3);
 
   if (gridDim.x > 1) {
@@ -438,6 +442,17 @@ extern "C" int rph_train_step(const TrainDesc* d, int step, int epoch, void* str
   RPH_SHAPES(X)
 #undef X
   return launch_wide_step(d, step, epoch, perm, s);
+}
+
+// One launch per Keras fit() (persistent kernel, hedge_fit.h); world_size 1.
+extern "C" int rph_train_fit(const TrainDesc* d, int epochs, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E))         \
+    return launch_fit<NarrowBody<A, B, C, E>>(d, epochs, s);
+  RPH_SHAPES(X)
+#undef X
+  return launch_wide_fit(d, epochs, s);
 }
 
 extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* stream) {

@@ -33,6 +33,7 @@
 //     (float-atomic replicas or deterministic slab), optional fused xGMI
 //     all-reduce, and Adam applied in place by the last arriver.
 #include "hedge_core.h"
+#include "hedge_fit.h"
 
 namespace rph {
 
@@ -180,57 +181,207 @@ RPH_INLINE void half_reduce_scatter(float* v, int lane) {
   halve_step<RV / 16, 0>(v, lane);
 }
 
+// Per-workgroup gradient packet of one minibatch step on the matrix cores.
+// Used by the per-step kernel below and by the persistent per-fit kernel.
+template <int NIN, int NO, int HEAD, bool F32>
+struct WideBody {
+  using S = NetShape<NIN, WH, NO, HEAD>;
+  using G = SmallGrad<NIN, NO>;
+  static constexpr int P = S::P;
+  static constexpr int R = S::R;  // packet width, multiple of 256
+  static constexpr int NR = R / 256;
+  static constexpr int NHOLD = S::NHOLD;
+  static constexpr int RV = G::RV;
+  static constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * IMG_PITCH * 2;
+  static constexpr int SCRATCH_FLOATS = ((4 * IMG_BYTES > 4 * R * 4) ? 4 * IMG_BYTES : 4 * R * 4) / 4 + 8;
+  static_assert(R % 256 == 0, "wide packet must be a multiple of 256");
+  struct Frags {
+    WFrag<F32> w2t, w2;
+  };
+  struct Pre {  // this lane's path of the first tile, loaded ahead by the caller
+    float x[NIN], pr[NHOLD], y;
+    bool valid;
+  };
+
+  // W2src: the 32x32 W2 block (global memory or LDS)
+  RPH_INLINE static void make_frags(const float* __restrict__ W2src, Frags& f) {
+    const int lane = threadIdx.x & 63;
+    load_wfrag<F32, false>(f.w2t, W2src, lane & 31, lane >> 5);
+    load_wfrag<F32, true>(f.w2, W2src, lane & 31, lane >> 5);
+  }
+
+  RPH_INLINE static int first(int wid) { return blockIdx.x * 4 + wid; }  // first tile of this wave
+
+  RPH_INLINE static void load(const TrainDesc& d, int step, const Perm& perm, int T, int lane, Pre& p) {
+    const long long jl = (long long)T * 32 + (lane & 31);
+    const long long j = (long long)step * d.batch + jl;
+    p.valid = (jl < d.batch) && (j < d.n_local);
+    const uint32_t q = p.valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) p.x[f] = p.valid ? d.feat[f][q] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = p.valid ? d.price[k][q] : 0.f;
+    p.pr[NHOLD - 1] = d.bond;
+    p.y = p.valid ? d.target[q] : 0.f;
+  }
+
+  // wl: weights in LDS; scratch: SCRATCH_FLOATS of LDS; pre: first tile (loaded).
+  // Returns in val[k] the workgroup sum of packet entry tid + 256 k.
+  RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ wl,
+                                 const Frags& fr, float* scratch, Pre& pre, float (&val)[NR]) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int nwaves = gridDim.x * 4;
+    const int ntiles = (d.batch + 31) >> 5;
+    void* img = (unsigned char*)scratch + wid * IMG_BYTES;
+    float g[RV];
+#pragma unroll
+    for (int i = 0; i < RV; ++i) g[i] = 0.f;
+    f32x16 gw2 = {};
+    const float alpha = d.alpha;
+    const float hv0 = (h == 0) ? 1.f : 0.f;
+
+    for (int T = first(wid); T < ntiles; T += nwaves) {
+      float x[NIN], pr[NHOLD];
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) x[f] = pre.x[f];
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) pr[k] = pre.pr[k];
+      const float y = pre.y;
+      const bool valid = pre.valid;
+      if (T + nwaves < ntiles) load(d, step, perm, T + nwaves, lane, pre);  // software pipelining
+
+      // ---- forward --------------------------------------------------------
+      float z1[16], a1[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int u = unit_of(q, h);
+        float acc = wl[S::OB1 + u];
+#pragma unroll
+        for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], wl[S::OW1 + f * WH + u], acc);
+        z1[q] = acc;
+        a1[q] = lrelu(acc, alpha);
+      }
+      const f32x16 z2acc = layer_mfma<F32>(fr.w2t, a1);
+      float z2[16], a2[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        z2[q] = z2acc[q] + wl[S::OB2 + unit_of(q, h)];
+        a2[q] = lrelu(z2[q], alpha);
+      }
+      float o[NO];
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc = fmaf(a2[q], wl[S::OW3 + unit_of(q, h) * NO + k], acc);
+        o[k] = acc + __shfl_xor(acc, 32, 64) + wl[S::OB3 + k];  // both halves: full sum over 32 units
+      }
+      float hold[NHOLD];
+      if (HEAD == HEAD_COMPLEMENT) {
+        hold[0] = o[0];
+        hold[1] = 1.f - o[0];
+      } else {
+#pragma unroll
+        for (int k = 0; k < NHOLD; ++k) hold[k] = o[k];
+      }
+      float V = 0.f;
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
+      float l, dV;
+      path_loss(d.loss, d.quantile, V, y, l, dV);
+      dV = valid ? dV * d.inv_batch : 0.f;
+      const float hv = valid ? hv0 : 0.f;  // path-level statistics: lane half 0 only
+      const float ae = fabsf(V - y);
+      g[G::ST + 0] = fmaf(hv, l, g[G::ST + 0]);
+      g[G::ST + 1] = fmaf(hv, ae, g[G::ST + 1]);
+      g[G::ST + 2] = fmaf(hv, ae / fmaxf(fabsf(y), 1e-7f), g[G::ST + 2]);
+      g[G::ST + 3] += hv;
+
+      // ---- backward -------------------------------------------------------
+      float dout[NO];
+      if (HEAD == HEAD_COMPLEMENT) {
+        dout[0] = dV * (pr[0] - pr[1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) g[G::DB3 + k] = fmaf(hv0, dout[k], g[G::DB3 + k]);
+      float dz2[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int u = unit_of(q, h);
+        float da = 0.f;
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          g[G::DW3 + q * NO + k] = fmaf(a2[q], dout[k], g[G::DW3 + q * NO + k]);
+          da = fmaf(wl[S::OW3 + u * NO + k], dout[k], da);
+        }
+        dz2[q] = da * lrelu_d(z2[q], alpha);
+        g[G::DB2 + q] += dz2[q];
+      }
+      const f32x16 da1 = layer_mfma<F32>(fr.w2, dz2);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float dz1 = da1[q] * lrelu_d(z1[q], alpha);
+        g[G::DB1 + q] += dz1;
+#pragma unroll
+        for (int f = 0; f < NIN; ++f) g[G::DW1 + f * 16 + q] = fmaf(x[f], dz1, g[G::DW1 + f * 16 + q]);
+      }
+      outer_mfma<F32>(img, a1, dz2, r, h, gw2);
+    }
+    RPH_STAMP(2);
+
+    // ---- per-wave packet -> LDS, cross-wave sum -----------------------------
+    half_reduce_scatter<RV>(g, lane);
+    __syncthreads();  // every wave is done with its transpose image (aliases the packet)
+    float* pk = scratch;
+    float* pkw = pk + wid * R;
+    for (int i = P + 4 + lane; i < R; i += 64) pkw[i] = 0.f;
+    constexpr int PER = RV / 32;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int prm = small_param<NIN, NO, P>(r * PER + i, h);
+      if (prm >= 0) pkw[prm] = g[i];
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pkw[S::OW2 + unit_of(q, h) * WH + r] = gw2[q];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int i = tid + 256 * k;
+      val[k] = (pk[i] + pk[R + i]) + (pk[2 * R + i] + pk[3 * R + i]);
+    }
+    __syncthreads();
+  }
+};
+
 template <int NIN, int NO, int HEAD, bool F32>
 __global__ __launch_bounds__(256) void k_hedge_train_step_wide(const TrainDesc d, const int step, const int epoch,
                                                                const Perm perm) {
-  using S = NetShape<NIN, WH, NO, HEAD>;
-  using G = SmallGrad<NIN, NO>;
-  constexpr int P = S::P;
-  constexpr int R = S::R;  // packet width, multiple of 256
-  constexpr int NR = R / 256;
-  constexpr int NHOLD = S::NHOLD;
-  constexpr int RV = G::RV;
-  constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * IMG_PITCH * 2;
-  constexpr int SCR_BYTES = (4 * IMG_BYTES > 4 * R * 4) ? 4 * IMG_BYTES : 4 * R * 4;
-  static_assert(R % 256 == 0, "wide packet must be a multiple of 256");
-  __shared__ __attribute__((aligned(16))) unsigned char scratch[SCR_BYTES];
+  using B = WideBody<NIN, NO, HEAD, F32>;
+  constexpr int P = B::P;
+  constexpr int R = B::R;
+  constexpr int NR = B::NR;
+  __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ int s_last;
 
   RPH_STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
   const float stopped = d.fit->stopped;
   const float* __restrict__ Wg = d.wts->w[0];
   UpdPre<P> up;
   if (d.fused_update) prefetch_update<P>(up, d.wts, d.opt, d.fit, d.lr_sched, epoch, step);
-  WFrag<F32> w2t, w2;
-  load_wfrag<F32, false>(w2t, Wg + S::OW2, r, h);
-  load_wfrag<F32, true>(w2, Wg + S::OW2, r, h);
+  typename B::Frags fr;
+  B::make_frags(Wg + B::S::OW2, fr);
   for (int i = tid; i < P; i += 256) wl[i] = Wg[i];
-
-  const int nwaves = gridDim.x * 4;
-  const int gw = blockIdx.x * 4 + wid;
-  const long long base = (long long)step * d.batch;
-  const int ntiles = (d.batch + 31) >> 5;
-
-  auto load_path = [&](int T, float (&x)[NIN], float (&pr)[NHOLD], float& y, bool& valid) {
-    const long long jl = (long long)T * 32 + r;
-    const long long j = base + jl;
-    valid = (jl < d.batch) && (j < d.n_local);
-    const uint32_t p = valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = valid ? d.feat[f][p] : 0.f;
-#pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = valid ? d.price[k][p] : 0.f;
-    pr[NHOLD - 1] = d.bond;
-    y = valid ? d.target[p] : 0.f;
-  };
-  int T = gw;
-  float xn[NIN], prn[NHOLD], yn = 0.f;
-  bool validn = false;
-  if (T < ntiles) load_path(T, xn, prn, yn, validn);
+  typename B::Pre pre;
+  pre.valid = false;
+  if (B::first(wid) < ((d.batch + 31) >> 5)) B::load(d, step, perm, B::first(wid), lane, pre);
 
   if (stopped != 0.f) return;  // early-stopped fit: remaining steps are no-ops
   if (d.fused_update) {
@@ -239,129 +390,9 @@ __global__ __launch_bounds__(256) void k_hedge_train_step_wide(const TrainDesc d
   }
   __syncthreads();
   RPH_STAMP(1);
-
-  void* img = scratch + wid * IMG_BYTES;
-  float g[RV];
-#pragma unroll
-  for (int i = 0; i < RV; ++i) g[i] = 0.f;
-  f32x16 gw2 = {};
-  const float alpha = d.alpha;
-  const float hv0 = (h == 0) ? 1.f : 0.f;
-
-  for (; T < ntiles; T += nwaves) {
-    float x[NIN], pr[NHOLD];
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = xn[f];
-#pragma unroll
-    for (int k = 0; k < NHOLD; ++k) pr[k] = prn[k];
-    const float y = yn;
-    const bool valid = validn;
-    if (T + nwaves < ntiles) load_path(T + nwaves, xn, prn, yn, validn);
-
-    // ---- forward ----------------------------------------------------------
-    float z1[16], a1[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int u = unit_of(q, h);
-      float acc = wl[S::OB1 + u];
-#pragma unroll
-      for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], wl[S::OW1 + f * WH + u], acc);
-      z1[q] = acc;
-      a1[q] = lrelu(acc, alpha);
-    }
-    const f32x16 z2acc = layer_mfma<F32>(w2t, a1);
-    float z2[16], a2[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      z2[q] = z2acc[q] + wl[S::OB2 + unit_of(q, h)];
-      a2[q] = lrelu(z2[q], alpha);
-    }
-    float o[NO];
-#pragma unroll
-    for (int k = 0; k < NO; ++k) {
-      float acc = 0.f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc = fmaf(a2[q], wl[S::OW3 + unit_of(q, h) * NO + k], acc);
-      o[k] = acc + __shfl_xor(acc, 32, 64) + wl[S::OB3 + k];  // both halves: full sum over 32 units
-    }
-    float hold[NHOLD];
-    if (HEAD == HEAD_COMPLEMENT) {
-      hold[0] = o[0];
-      hold[1] = 1.f - o[0];
-    } else {
-#pragma unroll
-      for (int k = 0; k < NHOLD; ++k) hold[k] = o[k];
-    }
-    float V = 0.f;
-#pragma unroll
-    for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
-    float l, dV;
-    path_loss(d.loss, d.quantile, V, y, l, dV);
-    dV = valid ? dV * d.inv_batch : 0.f;
-    const float hv = valid ? hv0 : 0.f;  // path-level statistics: lane half 0 only
-    const float ae = fabsf(V - y);
-    g[G::ST + 0] = fmaf(hv, l, g[G::ST + 0]);
-    g[G::ST + 1] = fmaf(hv, ae, g[G::ST + 1]);
-    g[G::ST + 2] = fmaf(hv, ae / fmaxf(fabsf(y), 1e-7f), g[G::ST + 2]);
-    g[G::ST + 3] += hv;
-
-    // ---- backward ---------------------------------------------------------
-    float dout[NO];
-    if (HEAD == HEAD_COMPLEMENT) {
-      dout[0] = dV * (pr[0] - pr[1]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NO; ++k) g[G::DB3 + k] = fmaf(hv0, dout[k], g[G::DB3 + k]);
-    float dz2[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int u = unit_of(q, h);
-      float da = 0.f;
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        g[G::DW3 + q * NO + k] = fmaf(a2[q], dout[k], g[G::DW3 + q * NO + k]);
-        da = fmaf(wl[S::OW3 + u * NO + k], dout[k], da);
-      }
-      dz2[q] = da * lrelu_d(z2[q], alpha);
-      g[G::DB2 + q] += dz2[q];
-    }
-    const f32x16 da1 = layer_mfma<F32>(w2, dz2);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float dz1 = da1[q] * lrelu_d(z1[q], alpha);
-      g[G::DB1 + q] += dz1;
-#pragma unroll
-      for (int f = 0; f < NIN; ++f) g[G::DW1 + f * 16 + q] = fmaf(x[f], dz1, g[G::DW1 + f * 16 + q]);
-    }
-    outer_mfma<F32>(img, a1, dz2, r, h, gw2);
-  }
-  RPH_STAMP(2);
-
-  // ---- per-wave packet -> LDS, cross-wave sum ---------------------------------
-  half_reduce_scatter<RV>(g, lane);
-  __syncthreads();  // every wave is done with its transpose image (aliases the packet)
-  float* pk = (float*)scratch;
-  float* pkw = pk + wid * R;
-  for (int i = P + 4 + lane; i < R; i += 64) pkw[i] = 0.f;
-  constexpr int PER = RV / 32;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int prm = small_param<NIN, NO, P>(r * PER + i, h);
-    if (prm >= 0) pkw[prm] = g[i];
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) pkw[S::OW2 + unit_of(q, h) * WH + r] = gw2[q];
-  __syncthreads();
   float val[NR];
-#pragma unroll
-  for (int k = 0; k < NR; ++k) {
-    const int i = tid + 256 * k;
-    val[k] = (pk[i] + pk[R + i]) + (pk[2 * R + i] + pk[3 * R + i]);
-  }
-  __syncthreads();
+  B::partial(d, step, perm, wl, fr, scratch, pre, val);
+  float* pk = scratch;
   RPH_STAMP(3);
 
   if (gridDim.x > 1) {
@@ -427,6 +458,17 @@ int launch_wide_step(const TrainDesc* d, int step, int epoch, const Perm& perm, 
       hipLaunchKernelGGL((k_hedge_train_step_wide<A, C, E, false>), dim3(d->num_wgs), dim3(256), 0, s, *d, \
                          step, epoch, perm);                                                            \
     return (int)hipGetLastError();                                                                      \
+  }
+  RPH_WIDE_SHAPES(X)
+#undef X
+  return -1;
+}
+
+int launch_wide_fit(const TrainDesc* d, int epochs, hipStream_t s) {
+#define X(A, B, C, E)                                                          \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                 \
+    if (d->mfma_fp32) return launch_fit<WideBody<A, C, E, true>>(d, epochs, s); \
+    return launch_fit<WideBody<A, C, E, false>>(d, epochs, s);                 \
   }
   RPH_WIDE_SHAPES(X)
 #undef X

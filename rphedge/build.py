@@ -73,12 +73,34 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False, asan:
     if not force and lib.exists() and stamp.exists() and stamp.read_text().strip() == digest:
         return lib
     tmp = lib.with_suffix(".so.tmp")
-    cmd = [_hipcc(), *flags, *[str(s) for s in sources()], "-o", str(tmp)]
+    # one hipcc per translation unit in parallel (the kernels are template-heavy),
+    # then one link into the shared object
+    objdir = LIBDIR / ("obj_asan" if asan else "obj")
+    objdir.mkdir(exist_ok=True)
+    cflags = [f for f in flags if f not in ("-shared", "-lrccl") and not f.startswith("-L")]
+    jobs = []
+    for src in sources():
+        obj = objdir / (src.name + ".o")
+        jobs.append(([_hipcc(), *cflags, "-c", str(src), "-o", str(obj)], obj))
+    from concurrent.futures import ThreadPoolExecutor
+
+    def _run(job):
+        cmd, _ = job
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        return subprocess.run(cmd, capture_output=True, text=True)
+
+    with ThreadPoolExecutor(max_workers=min(len(jobs), max(1, (os.cpu_count() or 2)))) as ex:
+        results = list(ex.map(_run, jobs))
+    for (cmd, _), res in zip(jobs, results):
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc failed ({res.returncode}): {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    cmd = [_hipcc(), *flags, *[str(o) for _, o in jobs], "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+        raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
     os.replace(tmp, lib)
     stamp.write_text(digest)
     return lib

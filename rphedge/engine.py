@@ -76,6 +76,7 @@ class TrainConfig:
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
     mfma_fp32: bool = False        # 32-unit nets: exact fp32 MFMA instead of bf16 operands
+    persistent: bool = True        # one resident launch per fit (world 1, float-atomic reduction)
 
 
 @dataclass
@@ -195,6 +196,9 @@ class HipBackend:
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
         self.grad = torch.zeros(self.R, dtype=torch.float32, device=dev)
         self.acc = torch.zeros(8, self.R, dtype=torch.float32, device=dev)
+        # persistent per-fit kernel: 3 rotating accumulator buffers + [arrivals, error] counters
+        self.acc_fit = torch.zeros(3, 8, self.R, dtype=torch.float32, device=dev)
+        self.fit_ctl = torch.zeros(4, dtype=torch.int32, device=dev)
         self.stamps = None  # set to an int64 [num_wgs, 8] tensor for phase diagnostics
         self.eval_wgs = int(max(1, min(1024, (self.n_local + 255) // 256)))
         self._cache = _Cache()
@@ -270,6 +274,12 @@ class HipBackend:
         lr_t = self._lr(fcfg)
         d = self._train_desc(wts, opt, fit, data, fcfg, seed, lr_t)
         n, S = self.native, self.steps_per_epoch
+        if self.use_persistent(poll_every):
+            n.memset_async(self.acc_fit, 0, self.stream)
+            n.memset_async(self.fit_ctl, 0, self.stream)
+            d.acc, d.counter = self.acc_fit.data_ptr(), self.fit_ctl.data_ptr()
+            n.train_fit(d, fcfg.epochs, self.stream)
+            return
         for e in range(fcfg.epochs):
             for s in range(S):
                 n.train_step(d, s, e, self.stream)
@@ -280,6 +290,17 @@ class HipBackend:
             if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:
                 if float(fit[L.F_STOPPED].item()) != 0.0:
                     break
+
+    def use_persistent(self, poll_every: int = 0) -> bool:
+        t = self.tcfg
+        return (t.persistent and self.world == 1 and not t.deterministic and not t.split_update
+                and not poll_every)
+
+    def check(self):
+        """Raise if a persistent fit timed out waiting for co-resident workgroups."""
+        if int(self.fit_ctl[1].item()) != 0:
+            raise RuntimeError("persistent fit kernel: workgroups not co-resident (wait timed out); "
+                               "set TrainConfig.persistent=False")
 
     def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
              v_out=None, hold_out=None, resid_out=None, pred1_out=None):
@@ -448,6 +469,7 @@ class TorchBackend:
         opt[L.O_NAN] += nan_steps
         fit[L.F_BEST] = best
         fit[L.F_WAIT] = wait
+        fit[L.F_HASBEST] = 1.0 if has_best else 0.0
         fit[L.F_STOPPED] = 1.0
         fit[L.F_EPOCH] = n_ep
         fit[L.F_LAST_LOSS] = hist[-1] if hist else float("nan")

@@ -111,6 +111,7 @@ def _bind(lib):
         "rph_net_nparams": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "rph_train_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
         "rph_train_update": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
+        "rph_train_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
@@ -208,6 +209,12 @@ def simulate(desc: SimDesc, stream=None):
 
 def train_step(desc: TrainDesc, step: int, epoch: int, stream=None):
     _check(_lib.rph_train_step(C.byref(desc), int(step), int(epoch), stream_handle(stream)), "rph_train_step")
+
+
+def train_fit(desc: TrainDesc, epochs: int, stream=None):
+    """One persistent launch for a whole fit (csrc/hedge_fit.h); desc.counter
+    (>= 2 u32) and desc.acc (3 x 8 x R floats) must be zeroed before it."""
+    _check(_lib.rph_train_fit(C.byref(desc), int(epochs), stream_handle(stream)), "rph_train_fit")
 
 
 def train_update(desc: TrainDesc, step: int, epoch: int, stream=None):

@@ -170,15 +170,18 @@ def _fit_pair(dev, spec, n, batch, epochs, loss, chunk_log2=0, lr=1e-2, **tkw):
     return out
 
 
+@pytest.mark.parametrize("persistent", [True, False])
 @pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (5, 8, 6, 0)])
-def test_train_step_matches_torch(dev, shape):
-    """Fused HIP training (fwd+bwd+reduce+Adam, several steps) vs torch autograd + Keras-Adam."""
+def test_train_step_matches_torch(dev, shape, persistent):
+    """Fused HIP training (fwd+bwd+reduce+Adam, several steps) vs torch autograd
+    + Keras-Adam — per-step kernels and the persistent one-launch-per-fit kernel."""
     from rphedge.models.hedge_mlp import NetSpec
     from rphedge.ops import layout as L
 
     nin, h, nout, head = shape
     spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
-    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE,
+                                                                   persistent=persistent)
     np.testing.assert_allclose(wg, wc, rtol=2e-3, atol=2e-4)
     assert og[L.O_T] == oc[L.O_T] == 16
     np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
@@ -201,7 +204,8 @@ def test_train_pinball_multi_wg(dev, det, split):
     np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 3], fc[L.F_HIST:L.F_HIST + 3], rtol=1e-3)
 
 
-def test_early_stopping_device_matches_torch(dev):
+@pytest.mark.parametrize("persistent", [True, False])
+def test_early_stopping_device_matches_torch(dev, persistent):
     from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
     from rphedge.models.hedge_mlp import NetSpec, init_weights
     from rphedge.ops import layout as L
@@ -215,11 +219,17 @@ def test_early_stopping_device_matches_torch(dev):
     fc = FitConfig(epochs=40, patience=3, loss=L.LOSS_MSE, lr_schedule=tuple([0.05] * 40))
     res = []
     for be, dd in ((TorchBackend(spec, n, TrainConfig(batch_size=512), device="cpu"), data_c),
-                   (HipBackend(spec, n, TrainConfig(batch_size=512), device=dev), data_g)):
+                   (HipBackend(spec, n, TrainConfig(batch_size=512, persistent=persistent), device=dev), data_g)):
         w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
         be.fit(w, o, f, dd, fc, seed=3)
-        res.append((int(f[L.F_EPOCH].item()), current_weights(spec, w)))
+        res.append((int(f[L.F_EPOCH].item()), current_weights(spec, w), f.cpu().numpy(), o.cpu().numpy()))
     assert res[0][0] == res[1][0]
+    fc_, fg_ = res[0][2], res[1][2]
+    for k in (L.F_STOPPED, L.F_WAIT, L.F_HASBEST):
+        assert fc_[k] == fg_[k], k
+    np.testing.assert_allclose(fg_[L.F_BEST], fc_[L.F_BEST], rtol=1e-3)
+    np.testing.assert_allclose(fg_[L.F_HIST:L.F_HIST + res[0][0]], fc_[L.F_HIST:L.F_HIST + res[0][0]], rtol=2e-3)
+    assert res[0][3][L.O_T] == res[1][3][L.O_T]
     np.testing.assert_allclose(res[1][1], res[0][1], rtol=5e-2, atol=1e-2)
 
 
@@ -361,3 +371,33 @@ def test_nan_gradient_guard_gpu(dev):
     assert np.all(np.isfinite(current_weights(spec, w)))
     assert float(o[L.O_NAN].item()) == 3.0
     assert float(o[L.O_T].item()) == 9.0   # 12 steps, 3 skipped
+
+
+def test_persistent_fit_matches_step_kernels(dev):
+    """One-launch-per-fit kernel == per-step kernels (same math; float-atomic
+    summation order only), many workgroups, pinball loss, lr schedule."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(nin=3, hidden=8, nout=2, head=0)
+    n = 1 << 18
+    g = torch.Generator().manual_seed(5)
+    feats = [(torch.rand(n, generator=g) * 0.5 + 0.75).to(dev) for _ in range(3)]
+    prices = [feats[0] * 1.02]
+    data = DateData(feats=feats, prices_next=prices, bond_next=1.01, target=torch.relu(prices[0] - 1.0),
+                    prices_now=feats[:1])
+    fc = FitConfig(epochs=12, patience=4, loss=L.LOSS_PINBALL, lr_schedule=tuple([1e-2] * 6 + [1e-3] * 6))
+    out = []
+    for persistent in (True, False):
+        be = HipBackend(spec, n, TrainConfig(batch_size=1 << 15, chunk_log2=6, persistent=persistent), device=dev)
+        w, o, f = be.new_weights(init_weights(spec, [0.5, 0.1])), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, fc, seed=11)
+        torch.cuda.synchronize()
+        be.check()
+        out.append((current_weights(spec, w), o.cpu().numpy(), f.cpu().numpy()))
+    (wp, op, fp), (ws, os_, fs) = out
+    assert fp[L.F_EPOCH] == fs[L.F_EPOCH] and op[L.O_T] == os_[L.O_T]
+    np.testing.assert_allclose(fp[L.F_HIST:L.F_HIST + 12], fs[L.F_HIST:L.F_HIST + 12], rtol=1e-4)
+    np.testing.assert_allclose(wp, ws, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(op[L.O_M:L.O_M + spec.nparams], os_[L.O_M:L.O_M + spec.nparams], rtol=1e-2, atol=1e-7)
