@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 
 
@@ -33,6 +34,15 @@ def _summary(res) -> dict:
             "timings": res.timings}
 
 
+def _plots(res, out_dir):
+    if not out_dir:
+        return
+    from .utils.reports import plot_run
+
+    os.makedirs(out_dir, exist_ok=True)
+    res.summary["figures"] = plot_run(res, out_prefix=os.path.join(out_dir, "rphedge"))
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="rphedge", description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -41,11 +51,13 @@ def main(argv=None) -> int:
     r.add_argument("--set", nargs="*", default=[])
     r.add_argument("--sv", action="store_true")
     r.add_argument("--out", default=None)
+    r.add_argument("--plots", default=None, help="directory for the report figures (C26-C32)")
     e = sub.add_parser("european")
     e.add_argument("--paths", type=int, default=3000)
     e.add_argument("--rebalancing", type=float, default=1 / 52)
     e.add_argument("--parity", action="store_true")
     e.add_argument("--set", nargs="*", default=[])
+    e.add_argument("--plots", default=None, help="directory for the report figures (C26-C32)")
     sub.add_parser("sts").add_argument("--no-parity", action="store_true")
     s = sub.add_parser("sweep")
     s.add_argument("--sigmas", default="0.05,0.10,0.15,0.20,0.30")
@@ -68,12 +80,14 @@ def main(argv=None) -> int:
         if a.out:
             params["save_dir"] = a.out
         res = run_params(params, sv=a.sv)
+        _plots(res, a.plots)
         print(json.dumps(_summary(res), default=float, indent=1))
     elif a.cmd == "european":
         from .api import european_option
 
         extra = {k: _coerce(v) for k, v in (kv.split("=", 1) for kv in a.set)}
         res = european_option(N_paths=a.paths, rebalancing_frequency=a.rebalancing, parity=a.parity, **extra)
+        _plots(res, a.plots)
         print(json.dumps(_summary(res), default=float, indent=1))
     elif a.cmd == "sts":
         from .experiments import single_time_step

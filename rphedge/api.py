@@ -46,6 +46,7 @@ class RunResult:
     summary: dict = field(default_factory=dict)
     timings: dict = field(default_factory=dict)
     config: dict = field(default_factory=dict)
+    paths: object = None                   # ops.paths.Paths of this rank (plots, C32)
 
     def as_tuple(self):
         return self.phi, self.psi
@@ -384,7 +385,7 @@ class HedgeRun:
             summary["bs_price"], summary["bs_delta"] = bs
         return RunResult(phi=phi, psi=psi, v0=ind.v0 * scale, scale=scale, holdings0=h0, induction=ind,
                          errors=error_history(ind), p_e_values=pe, terminal_pnl=tp, var=var, summary=summary,
-                         timings=self.timer.summary(), config=c.to_dict())
+                         timings=self.timer.summary(), config=c.to_dict(), paths=self.paths)
 
 
 # ---------------------------------------------------------------------------

@@ -191,6 +191,23 @@ def test_reports():
     assert 8.5e5 < cf[0] < 1.0e6  # SURVEY: ~917,112 EUR
 
 
+def test_report_figures(tmp_path):
+    """C26-C32 figures (Agg backend): holdings violins, residual scatter/hist,
+    value fan, trajectory/errors, sampled paths incl. lambda/N for the pension."""
+    from rphedge import Replicating_Portfolio  # noqa: F401
+    from rphedge.api import run_params
+    from rphedge.utils import reports
+
+    res = run_params(_small(), sv=False)
+    files = reports.plot_run(res, out_prefix=str(tmp_path / "mts"))
+    names = {os.path.basename(f) for f in files}
+    for want in ("mts_holdings.png", "mts_residuals.png", "mts_value_fan.png", "mts_trajectory.png",
+                 "mts_paths.png", "mts_lambda.png", "mts_survivors.png", "mts_terminal_hist.png"):
+        assert want in names, (want, names)
+    for f in files:
+        assert os.path.getsize(f) > 1000
+
+
 def test_resume_from_saved_date(tmp_path):
     """Checkpoint/resume: a run restarted at date i from the saved weights and
     values reproduces the dates < i of the uninterrupted run (CPU backend is
