@@ -40,6 +40,14 @@ RPH_INLINE uint32_t ld_agent_u32(const uint32_t* p) {
   return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// sum of the ACC_REPLICAS float-atomic replicas of packet entry i (fixed order)
+RPH_INLINE float sum_replicas(const float* buf, int R, int i) {
+  float rr[ACC_REPLICAS];
+#pragma unroll
+  for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
+  return ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+}
+
 template <class B>
 __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int epochs) {
   constexpr int P = B::P;
@@ -79,6 +87,10 @@ __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int 
   float loss_sum = f->loss_sum, abs_sum = f->abs_sum, ape_sum = f->ape_sum, loss_cnt = f->loss_cnt;
   float last_L = f->last_loss, last_mae = f->last_mae, last_mape = f->last_mape;
   int ep_done = (int)f->epoch;
+  const bool dp = d.dp_world > 1;
+  // per-rank DP step sequence (read by every workgroup before the first
+  // barrier; workgroup 0 advances it after the last one)
+  const uint32_t seq0 = dp ? ld_agent_u32(d.dp_counter) : 0u;
   if (stopped != 0.f) return;
 #pragma unroll
   for (int k = 0; k < NPT; ++k)
@@ -91,7 +103,8 @@ __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int 
   // drained, 3 all arrived (thread 0), 4 sums read, 5 update done
 #define FIT_STAMP(k) \
   if (d.stamps != nullptr && tid == 0) d.stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
-  uint32_t gstep = 0;
+  uint32_t gstep = 0;  // steps started (rotating buffers, barrier targets)
+  uint32_t done = 0;   // steps completed (DP sequence)
   bool bad = false;
   // first path(s) of the next step are loaded BEFORE the barrier of the
   // current one (they do not depend on the weights), hiding their latency
@@ -160,14 +173,67 @@ __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int 
       }
 
       // ---- summed packet (bitwise identical in every workgroup) ----------------
+      if (!dp) {
 #pragma unroll
-      for (int k = 0; k < NR; ++k) {
-        const int i = tid + 256 * k;
-        if (i < R) {
-          float rr[ACC_REPLICAS];
+        for (int k = 0; k < NR; ++k) {
+          const int i = tid + 256 * k;
+          if (i < R) red[i] = sum_replicas(buf, R, i);
+        }
+      } else {
+        // data parallel: this rank's last arriver pushes the local sum into every
+        // rank's IPC mailbox (system-scope stores over xGMI) and raises one flag
+        // per peer; EVERY workgroup of every rank then waits for the W flags of
+        // this step and sums the W packets in fixed rank order (identical
+        // everywhere).  A peer can be at most one step ahead, so the DP_SLOTS-deep
+        // slot of `seq` is never overwritten while it is read.
+        const uint32_t seq = seq0 + gstep + 1u;
+        const int slot = (int)(seq % DP_SLOTS);
+        const int W = d.dp_world, me = d.dp_rank;
+        if (s_last) {
 #pragma unroll
-          for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
-          red[i] = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+          for (int k = 0; k < NR; ++k) {
+            const int i = tid + 256 * k;
+            if (i < R) {
+              const float vloc = sum_replicas(buf, R, i);
+              for (int p = 0; p < W; ++p)
+                __hip_atomic_store(d.dp_mbox[p] + ((size_t)slot * W + me) * R + i, vloc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid < W)
+            __hip_atomic_store(d.dp_flags[tid] + slot * W + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        int b = 0;
+        if (tid < W) {
+          const uint32_t* fl = d.dp_flags[me] + slot * W + tid;
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          unsigned it = 0;
+          while (__hip_atomic_load(const_cast<uint32_t*>(fl), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((++it & 255u) == 0u && __builtin_amdgcn_s_memrealtime() - t0 > FIT_SPIN_TICKS) {
+              __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              b = 1;
+              break;
+            }
+          }
+        }
+        if (__syncthreads_or(b)) {
+          bad = true;
+          break;
+        }
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          const int i = tid + 256 * k;
+          if (i < R) {
+            float a = 0.f;
+            for (int p = 0; p < W; ++p)
+              a += __hip_atomic_load(d.dp_mbox[me] + ((size_t)slot * W + p) * R + i, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+            red[i] = a;
+          }
         }
       }
       if (s_last) {  // re-zero the buffer of step gstep+2 (last read at gstep-1)
@@ -244,6 +310,7 @@ __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int 
       for (int k = 0; k < NPT; ++k)
         if (tid + 256 * k < P) wl[tid + 256 * k] = w[k];
       __syncthreads();
+      ++done;
       FIT_STAMP(5);
       if (stopped != 0.f) break;
     }
@@ -264,6 +331,7 @@ __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int 
     }
   }
   if (tid == 0) {
+    if (dp) __hip_atomic_store(d.dp_counter, seq0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     d.opt->t = t;
     d.opt->lr = lr;
     d.opt->nan_steps = nan_steps;
@@ -300,5 +368,6 @@ int launch_fit(const TrainDesc* d, int epochs, hipStream_t s) {
 }
 
 int launch_wide_fit(const TrainDesc* d, int epochs, hipStream_t s);
+int launch_wide_lag_step(const TrainDesc* d, int k, int epoch, const Perm& perm, hipStream_t s);
 
 }  // namespace rph

@@ -22,6 +22,7 @@
 //     rank (bitwise-identical decisions => identical early stopping).
 #include "hedge_core.h"
 #include "hedge_fit.h"
+#include "hedge_lag.h"
 
 namespace rph {
 
@@ -453,6 +454,36 @@ extern "C" int rph_train_fit(const TrainDesc* d, int epochs, void* stream) {
   RPH_SHAPES(X)
 #undef X
   return launch_wide_fit(d, epochs, s);
+}
+
+// Lagged-update step kernel k of a fit (hedge_lag.h) and its finalize.
+extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t n_chunks = (uint32_t)((d->n_local + (1 << d->chunk_log2) - 1) >> d->chunk_log2);
+  const Perm perm = make_perm(n_chunks, d->seed, (uint32_t)epoch, d->shuffle != 0);
+#define X(A, B, C, E)                                                                                 \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                        \
+    hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, *d, k, \
+                       epoch, perm);                                                                  \
+    return (int)hipGetLastError();                                                                    \
+  }
+  RPH_SHAPES(X)
+#undef X
+  return launch_wide_lag_step(d, k, epoch, perm, s);
+}
+
+extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                        \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
+    using S = NetShape<A, B, C, E>;                                                          \
+    hipLaunchKernelGGL((k_hedge_lag_finalize<S::P, S::R>), dim3(1), dim3(256), 0, s, *d, K); \
+    return (int)hipGetLastError();                                                           \
+  }
+  RPH_SHAPES(X)
+  RPH_WIDE_SHAPES(X)
+#undef X
+  return -1;
 }
 
 extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* stream) {

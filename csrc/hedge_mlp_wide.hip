@@ -34,6 +34,7 @@
 //     all-reduce, and Adam applied in place by the last arriver.
 #include "hedge_core.h"
 #include "hedge_fit.h"
+#include "hedge_lag.h"
 
 namespace rph {
 
@@ -469,6 +470,22 @@ int launch_wide_fit(const TrainDesc* d, int epochs, hipStream_t s) {
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                 \
     if (d->mfma_fp32) return launch_fit<WideBody<A, C, E, true>>(d, epochs, s); \
     return launch_fit<WideBody<A, C, E, false>>(d, epochs, s);                 \
+  }
+  RPH_WIDE_SHAPES(X)
+#undef X
+  return -1;
+}
+
+int launch_wide_lag_step(const TrainDesc* d, int k, int epoch, const Perm& perm, hipStream_t s) {
+#define X(A, B, C, E)                                                                                         \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                                \
+    if (d->mfma_fp32)                                                                                         \
+      hipLaunchKernelGGL((k_hedge_step_lag<WideBody<A, C, E, true>>), dim3(d->num_wgs), dim3(256), 0, s, *d, k, \
+                         epoch, perm);                                                                        \
+    else                                                                                                      \
+      hipLaunchKernelGGL((k_hedge_step_lag<WideBody<A, C, E, false>>), dim3(d->num_wgs), dim3(256), 0, s, *d,  \
+                         k, epoch, perm);                                                                     \
+    return (int)hipGetLastError();                                                                            \
   }
   RPH_WIDE_SHAPES(X)
 #undef X

@@ -69,7 +69,7 @@ class TrainingParams:
     max_wgs: int = 256               # workgroups per training step
     hidden: int = 8                  # hidden width: 8 = reference nets (VALU kernel), 32 = MFMA kernel
     mfma_precision: str = "bf16"     # 32-unit nets: "bf16" (32x32x16 MFMA) or "fp32" (exact 32x32x2 MFMA)
-    persistent: bool = True          # one resident kernel launch per fit (single GPU); False = per-step kernels
+    step_mode: str = "auto"          # GPU step schedule: auto | lag | ticket | persistent (engine.TrainConfig)
 
 
 @dataclass

@@ -76,7 +76,14 @@ class TrainConfig:
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
     mfma_fp32: bool = False        # 32-unit nets: exact fp32 MFMA instead of bf16 operands
-    persistent: bool = True        # one resident launch per fit (world 1, float-atomic reduction)
+    # optimizer-step schedule on the GPU:
+    #   "lag"        one kernel per step, the Adam update of step k applied by every
+    #                workgroup in the prologue of kernel k+1 (no in-kernel sync)
+    #   "ticket"     one kernel per step, last-arriving workgroup reduces + updates
+    #                (deterministic slab / split update / fused xGMI DP)
+    #   "persistent" one resident kernel per fit with an in-kernel grid barrier
+    #   "auto"       lag where valid (1 rank, float-atomic reduction), else ticket
+    step_mode: str = "auto"
 
 
 @dataclass
@@ -199,6 +206,7 @@ class HipBackend:
         # persistent per-fit kernel: 3 rotating accumulator buffers + [arrivals, error] counters
         self.acc_fit = torch.zeros(3, 8, self.R, dtype=torch.float32, device=dev)
         self.fit_ctl = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.lag = torch.zeros(2, L.LAG_FLOATS, dtype=torch.float32, device=dev)
         self.stamps = None  # set to an int64 [num_wgs, 8] tensor for phase diagnostics
         self.eval_wgs = int(max(1, min(1024, (self.n_local + 255) // 256)))
         self._cache = _Cache()
@@ -274,11 +282,25 @@ class HipBackend:
         lr_t = self._lr(fcfg)
         d = self._train_desc(wts, opt, fit, data, fcfg, seed, lr_t)
         n, S = self.native, self.steps_per_epoch
-        if self.use_persistent(poll_every):
+        mode = self.step_mode(poll_every)
+        if mode == "persistent":
             n.memset_async(self.acc_fit, 0, self.stream)
             n.memset_async(self.fit_ctl, 0, self.stream)
             d.acc, d.counter = self.acc_fit.data_ptr(), self.fit_ctl.data_ptr()
             n.train_fit(d, fcfg.epochs, self.stream)
+            return
+        if mode == "lag":
+            n.memset_async(self.acc_fit, 0, self.stream)
+            d.acc, d.lag = self.acc_fit.data_ptr(), self.lag.data_ptr()
+            k = 0
+            for e in range(fcfg.epochs):
+                for s in range(S):
+                    n.train_lag_step(d, k, e, self.stream)
+                    k += 1
+                if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:
+                    if float(fit[L.F_STOPPED].item()) != 0.0:
+                        break
+            n.train_lag_finalize(d, k, self.stream)
             return
         for e in range(fcfg.epochs):
             for s in range(S):
@@ -291,16 +313,22 @@ class HipBackend:
                 if float(fit[L.F_STOPPED].item()) != 0.0:
                     break
 
-    def use_persistent(self, poll_every: int = 0) -> bool:
+    def step_mode(self, poll_every: int = 0) -> str:
+        """Resolve TrainConfig.step_mode for this backend (see TrainConfig)."""
         t = self.tcfg
-        return (t.persistent and self.world == 1 and not t.deterministic and not t.split_update
-                and not poll_every)
+        atomic = not t.deterministic and not t.split_update
+        dp_fused = self.mailbox is not None and self.comm is None
+        if t.step_mode == "persistent" and atomic and not poll_every and (self.world == 1 or dp_fused):
+            return "persistent"
+        if t.step_mode in ("auto", "lag") and atomic and self.world == 1:
+            return "lag"
+        return "ticket"
 
     def check(self):
         """Raise if a persistent fit timed out waiting for co-resident workgroups."""
         if int(self.fit_ctl[1].item()) != 0:
             raise RuntimeError("persistent fit kernel: workgroups not co-resident (wait timed out); "
-                               "set TrainConfig.persistent=False")
+                               "use TrainConfig.step_mode='lag' or 'ticket'")
 
     def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
              v_out=None, hold_out=None, resid_out=None, pred1_out=None):

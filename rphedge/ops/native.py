@@ -38,7 +38,7 @@ class TrainDesc(C.Structure):
         ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
         ("acc", VP), ("deterministic", C.c_int), ("stamps", VP),
         ("dp_world", C.c_int), ("dp_rank", C.c_int), ("dp_mbox", VP * 8), ("dp_flags", VP * 8),
-        ("dp_counter", VP), ("dp_error", VP), ("mfma_fp32", C.c_int),
+        ("dp_counter", VP), ("dp_error", VP), ("mfma_fp32", C.c_int), ("lag", VP),
     ]
 
 
@@ -112,6 +112,8 @@ def _bind(lib):
         "rph_train_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
         "rph_train_update": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
         "rph_train_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
+        "rph_train_lag_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
+        "rph_train_lag_finalize": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
@@ -215,6 +217,15 @@ def train_fit(desc: TrainDesc, epochs: int, stream=None):
     """One persistent launch for a whole fit (csrc/hedge_fit.h); desc.counter
     (>= 2 u32) and desc.acc (3 x 8 x R floats) must be zeroed before it."""
     _check(_lib.rph_train_fit(C.byref(desc), int(epochs), stream_handle(stream)), "rph_train_fit")
+
+
+def train_lag_step(desc: TrainDesc, k: int, epoch: int, stream=None):
+    """Lagged-update step kernel k of a fit (csrc/hedge_lag.h)."""
+    _check(_lib.rph_train_lag_step(C.byref(desc), int(k), int(epoch), stream_handle(stream)), "rph_train_lag_step")
+
+
+def train_lag_finalize(desc: TrainDesc, K: int, stream=None):
+    _check(_lib.rph_train_lag_finalize(C.byref(desc), int(K), stream_handle(stream)), "rph_train_lag_finalize")
 
 
 def train_update(desc: TrainDesc, step: int, epoch: int, stream=None):

@@ -36,7 +36,8 @@ def _fit(rank, world, n, epochs, dev, mailbox=None, deterministic=True):
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
     per = n // world
     f, p1, y = _data(n, dev, rank * per, per)
-    tc = TrainConfig(batch_size=n, chunk_log2=6, lr=1e-2, shuffle=False, deterministic=deterministic)
+    tc = TrainConfig(batch_size=n, chunk_log2=6, lr=1e-2, shuffle=False, deterministic=deterministic,
+                     step_mode="ticket" if deterministic else "persistent")
     be = HipBackend(spec, per, tc, device=dev, world=world, rank=rank, mailbox=mailbox)
     data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f])
     w, o, fs = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
@@ -45,7 +46,7 @@ def _fit(rank, world, n, epochs, dev, mailbox=None, deterministic=True):
     return current_weights(spec, w), fs.cpu().numpy()
 
 
-def _worker(rank, world, port, n, epochs, out):
+def _worker(rank, world, port, n, epochs, out, deterministic=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     from torch.distributed import distributed_c10d as c10d
@@ -57,7 +58,7 @@ def _worker(rank, world, port, n, epochs, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mb = IpcMailbox(rank, world, 128, c10d._get_default_store(), dev, tag="t_dp")
     dist.barrier()
-    w, fs = _fit(rank, world, n, epochs, dev, mailbox=mb)
+    w, fs = _fit(rank, world, n, epochs, dev, mailbox=mb, deterministic=deterministic)
     mb.check()
     np.save(out + f".{rank}.npy", w)
     dist.barrier()
@@ -65,13 +66,17 @@ def _worker(rank, world, port, n, epochs, out):
     dist.destroy_process_group()
 
 
-def test_fused_xgmi_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("deterministic", [True, False])
+def test_fused_xgmi_allreduce_two_ranks_one_gpu(deterministic):
+    """deterministic=True: per-step kernels + slab reduction; False: the
+    persistent one-launch-per-fit kernel with the in-kernel DP exchange."""
     n, epochs, world = 1 << 15, 6, 2
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "w")
         ctx = mp.get_context("spawn")
         port = _port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, n, epochs, out)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, n, epochs, out, deterministic))
+                 for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
@@ -79,5 +84,5 @@ def test_fused_xgmi_allreduce_two_ranks_one_gpu():
             assert p.exitcode == 0
         w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
     assert np.array_equal(w0, w1)                      # bitwise-identical replicas
-    ref, _ = _fit(0, 1, n, epochs, torch.device("cuda", 0))
+    ref, _ = _fit(0, 1, n, epochs, torch.device("cuda", 0), deterministic=deterministic)
     np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-5)
