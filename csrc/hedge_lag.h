@@ -89,7 +89,10 @@ RPH_INLINE void lag_store(const LagState<P>& st, float* slot) {
       slot[2 * PMAX + i] = st.v[k];
     }
   }
-  if (tid < LG_NSCALAR) slot[3 * PMAX + tid] = st.sc[tid];
+  if (tid == 0) {
+#pragma unroll
+    for (int j = 0; j < LG_NSCALAR; ++j) slot[3 * PMAX + j] = st.sc[j];  // (constant indices: no scratch)
+  }
 }
 
 // canonical write-back (one workgroup); `stopped`, `ep_done` as decided
@@ -215,7 +218,7 @@ RPH_INLINE void lag_sums(const float* buf, float* red) {
 }
 
 template <class B>
-__global__ __launch_bounds__(256) void k_hedge_step_lag(const TrainDesc d, const int k, const int epoch,
+__global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const TrainDesc d, const int k, const int epoch,
                                                         const Perm perm) {
   constexpr int P = B::P;
   constexpr int R = B::R;

@@ -31,8 +31,9 @@ namespace rph {
 // (the reference's 8-unit nets).  Used by the per-step kernel below and by the
 // persistent per-fit kernel (hedge_fit.h).
 // ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD>
+template <int NIN, int H, int NO, int HEAD, int WPE = 1>
 struct NarrowBody {
+  static constexpr int WAVES_PER_SIMD = WPE;
   using S = NetShape<NIN, H, NO, HEAD>;
   static constexpr int P = S::P;
   static constexpr int R = S::R;
@@ -73,9 +74,15 @@ struct NarrowBody {
     for (int i = 0; i < R; ++i) g[i] = 0.f;
     const float alpha = d.alpha;
     for (long long j0 = first(wid); j0 < d.batch; j0 += stride) {
-      // (loop-invariant LDS weights are hoisted into registers by the compiler;
-      // re-reading them per iteration to reach 2 waves/SIMD measured slower)
+      // WPE 1: the loop-invariant LDS weights are hoisted into registers (AGPR
+      // overflow); WPE 2: an opaque zero offset makes every iteration re-read
+      // them as LDS broadcasts, so the kernel fits 256 registers = 2 waves/SIMD
       const float* __restrict__ Wi = W;
+      if constexpr (WPE > 1) {
+        int z = 0;
+        asm volatile("" : "+v"(z));
+        Wi = W + z;
+      }
       float x[NIN], pr[NHOLD];
 #pragma unroll
       for (int f = 0; f < NIN; ++f) x[f] = pre.x[f];
@@ -96,7 +103,7 @@ struct NarrowBody {
       const float ae = fabsf(V - y);
       g[P + 0] += valid ? l : 0.f;
       g[P + 1] += valid ? ae : 0.f;
-      g[P + 2] += valid ? ae / fmaxf(fabsf(y), 1e-7f) : 0.f;
+      g[P + 2] += valid ? ae * __frcp_rn(fmaxf(fabsf(y), 1e-7f)) : 0.f;
       g[P + 3] += valid ? 1.f : 0.f;
 
       // backward
@@ -463,8 +470,12 @@ extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* st
   const Perm perm = make_perm(n_chunks, d->seed, (uint32_t)epoch, d->shuffle != 0);
 #define X(A, B, C, E)                                                                                 \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                        \
-    hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, *d, k, \
-                       epoch, perm);                                                                  \
+    if (d->variant == 1)                                                                              \
+      hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 2>>), dim3(d->num_wgs), dim3(256), 0, s, *d, \
+                         k, epoch, perm);                                                             \
+    else                                                                                              \
+      hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, *d, k, \
+                         epoch, perm);                                                                \
     return (int)hipGetLastError();                                                                    \
   }
   RPH_SHAPES(X)

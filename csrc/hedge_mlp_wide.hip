@@ -186,6 +186,7 @@ RPH_INLINE void half_reduce_scatter(float* v, int lane) {
 // Used by the per-step kernel below and by the persistent per-fit kernel.
 template <int NIN, int NO, int HEAD, bool F32>
 struct WideBody {
+  static constexpr int WAVES_PER_SIMD = 1;
   using S = NetShape<NIN, WH, NO, HEAD>;
   using G = SmallGrad<NIN, NO>;
   static constexpr int P = S::P;
@@ -297,7 +298,7 @@ struct WideBody {
       const float ae = fabsf(V - y);
       g[G::ST + 0] = fmaf(hv, l, g[G::ST + 0]);
       g[G::ST + 1] = fmaf(hv, ae, g[G::ST + 1]);
-      g[G::ST + 2] = fmaf(hv, ae / fmaxf(fabsf(y), 1e-7f), g[G::ST + 2]);
+      g[G::ST + 2] = fmaf(hv, ae * __frcp_rn(fmaxf(fabsf(y), 1e-7f)), g[G::ST + 2]);
       g[G::ST + 3] += hv;
 
       // ---- backward -------------------------------------------------------

@@ -102,6 +102,7 @@ struct TrainDesc {
   uint32_t* dp_error;            // set on a peer timeout (host checks after the run)
   int mfma_fp32;                 // 32-unit nets: exact fp32 MFMA (32x32x2) instead of bf16 (32x32x16)
   float* lag;                    // lagged-update state slots [2][LAG_FLOATS] (hedge_lag.h)
+  int variant;                   // kernel variant (narrow: 1 = 2 waves/SIMD, weights re-read from LDS)
 };
 
 constexpr int DP_SLOTS = 4;

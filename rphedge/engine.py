@@ -84,6 +84,7 @@ class TrainConfig:
     #   "persistent" one resident kernel per fit with an in-kernel grid barrier
     #   "auto"       lag where valid (1 rank, float-atomic reduction), else ticket
     step_mode: str = "auto"
+    variant: int = 0               # narrow lag kernel: 1 = 2 waves/SIMD with LDS weight re-reads
 
 
 @dataclass
@@ -267,6 +268,7 @@ class HipBackend:
         d.acc = self.acc.data_ptr()
         d.deterministic = 1 if self.tcfg.deterministic else 0
         d.mfma_fp32 = 1 if self.tcfg.mfma_fp32 else 0
+        d.variant = int(self.tcfg.variant)
         d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
         d.num_wgs = self.num_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head

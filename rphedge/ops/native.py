@@ -38,7 +38,7 @@ class TrainDesc(C.Structure):
         ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
         ("acc", VP), ("deterministic", C.c_int), ("stamps", VP),
         ("dp_world", C.c_int), ("dp_rank", C.c_int), ("dp_mbox", VP * 8), ("dp_flags", VP * 8),
-        ("dp_counter", VP), ("dp_error", VP), ("mfma_fp32", C.c_int), ("lag", VP),
+        ("dp_counter", VP), ("dp_error", VP), ("mfma_fp32", C.c_int), ("lag", VP), ("variant", C.c_int),
     ]
 
 

@@ -16,7 +16,7 @@ from rphedge.models.hedge_mlp import NetSpec, init_weights  # noqa: E402
 
 
 def run(batch_log2=18, n_log2=20, nin=1, nout=2, hidden=8, epochs=64, max_wgs=256, mode="persistent",
-        mfma_fp32=False):
+        mfma_fp32=False, variant=0):
     dev = torch.device("cuda", 0)
     spec = NetSpec(nin=nin, hidden=hidden, nout=nout, head=0)
     n = 1 << n_log2
@@ -25,7 +25,7 @@ def run(batch_log2=18, n_log2=20, nin=1, nout=2, hidden=8, epochs=64, max_wgs=25
     prices = [f * 1.01 for f in feats[: spec.nhold - 1]]
     target = torch.relu(prices[0] - 1.0)
     tc = TrainConfig(batch_size=1 << batch_log2, chunk_log2=6, max_wgs=max_wgs, step_mode=mode,
-                     mfma_fp32=mfma_fp32)
+                     mfma_fp32=mfma_fp32, variant=variant)
     be = HipBackend(spec, n, tc, device=dev)
     data = DateData(feats=feats, prices_next=prices, bond_next=1.0, target=target, prices_now=feats[:1])
     w0 = init_weights(spec, [0.5] + [0.0] * (nout - 1))
@@ -42,7 +42,8 @@ def run(batch_log2=18, n_log2=20, nin=1, nout=2, hidden=8, epochs=64, max_wgs=25
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1) * 1e3 / (epochs * be.steps_per_epoch))
-    out = {"batch_log2": batch_log2, "hidden": hidden, "mode": be.step_mode(), "num_wgs": be.num_wgs,
+    out = {"batch_log2": batch_log2, "hidden": hidden, "mode": be.step_mode(), "variant": variant,
+           "num_wgs": be.num_wgs,
            "steps_per_fit": epochs * be.steps_per_epoch, "us_per_step": float(np.median(times))}
     if be.step_mode() == "persistent":
         be.stamps = torch.zeros(be.num_wgs, 8, dtype=torch.int64, device=dev)
