@@ -329,7 +329,11 @@ RPH_INLINE void dp_allreduce(const TrainDesc& d, float* red) {
     unsigned it = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
       __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 23)) {  // ~seconds: a peer never arrived
+      ++it;
+      // a peer never arrived (~seconds), or an earlier step already timed out:
+      // fail fast instead of spinning again in every later step
+      if (it > (1u << 23) ||
+          ((it & 255u) == 0u && __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
@@ -380,6 +384,39 @@ __global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const i
 
 static inline bool shape_is(int nin, int h, int nout, int head, int a, int b, int c, int e) {
   return nin == a && h == b && nout == c && head == e;
+}
+
+int rph_report(const char* what, const char* msg);  // runtime.cpp: sets rph_last_error, returns -22
+
+// Host-side check of a training descriptor against what the kernels and their
+// grids assume (run before every launch: a bad shape must not reach the GPU).
+// mode: 0 ticket step, 1 lagged step / finalize, 2 persistent fit.
+inline int validate_train(const TrainDesc* d, int mode, const char* who) {
+  const int nhold = d->head == HEAD_COMPLEMENT ? 2 : d->nout;
+  if (d->nin < 1 || d->nin > MAXIN || nhold < 1 || nhold > MAXHOLD) return rph_report(who, "network shape out of range");
+  if (d->num_wgs < 1 || d->num_wgs > 65535) return rph_report(who, "num_wgs out of range");
+  if (d->batch < 1 || d->n_local < d->batch || d->steps_per_epoch < 1 ||
+      (long long)d->batch * d->steps_per_epoch < d->n_local)
+    return rph_report(who, "batch / steps_per_epoch do not cover n_local");
+  if (d->chunk_log2 < 0 || d->chunk_log2 > 20) return rph_report(who, "chunk_log2 out of range");
+  if (!d->wts || !d->opt || !d->fit || !d->target) return rph_report(who, "null state or target pointer");
+  for (int f = 0; f < d->nin; ++f)
+    if (!d->feat[f]) return rph_report(who, "null feature pointer");
+  for (int k = 0; k < nhold - 1; ++k)
+    if (!d->price[k]) return rph_report(who, "null price pointer");
+  if (mode == 1 && (!d->lag || !d->acc)) return rph_report(who, "lagged step needs lag and acc buffers");
+  if (mode == 2 && (!d->acc || !d->counter)) return rph_report(who, "persistent fit needs acc and counter");
+  if (mode == 0) {
+    if (!d->counter || (d->deterministic ? !d->slab : !d->acc)) return rph_report(who, "null reduction buffer");
+    if (!d->fused_update && !d->grad_out) return rph_report(who, "split update needs grad_out");
+  }
+  if (d->dp_world > 1) {
+    if (d->dp_world > 8 || d->dp_rank < 0 || d->dp_rank >= d->dp_world || !d->dp_counter || !d->dp_error)
+      return rph_report(who, "bad data-parallel mailbox description");
+    for (int p = 0; p < d->dp_world; ++p)
+      if (!d->dp_mbox[p] || !d->dp_flags[p]) return rph_report(who, "null peer mailbox");
+  }
+  return 0;
 }
 
 // Wide (MFMA) training-step launcher (hedge_mlp_wide.hip); returns -1 when the

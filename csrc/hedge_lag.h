@@ -231,6 +231,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   const int S = d.steps_per_epoch;
   const int s = k - epoch * S;
 
+  RPH_DASSERT(d.batch > 0 && k >= 0 && epoch * d.steps_per_epoch <= k && d.lag != nullptr);
   // ---- prologue: every load independent, issued together -----------------------
   RPH_STAMP(0);
   const float stopped0 = d.fit->stopped;

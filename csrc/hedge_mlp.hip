@@ -172,6 +172,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   // weights, the optimizer state for a possible last-arriver update, and the
   // first path's data (epoch is a launch argument, so the permutation needs no
   // device read).
+  RPH_DASSERT(d.batch > 0 && d.n_local >= d.batch && d.num_wgs == (int)gridDim.x);
   RPH_STAMP(0);
   const float stopped = d.fit->stopped;
   const float wv = threadIdx.x < P ? d.wts->w[0][threadIdx.x] : 0.f;
@@ -305,6 +306,7 @@ template <int NIN, int H, int NO, int HEAD>
 __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   using S = NetShape<NIN, H, NO, HEAD>;
   constexpr int NHOLD = S::NHOLD;
+  RPH_DASSERT(d.n_local > 0 && d.num_wgs == (int)gridDim.x && d.wa != nullptr && d.stats != nullptr);
   __shared__ double sst[4][EVAL_NSTAT];
   __shared__ __attribute__((aligned(16))) float wl[2 * S::P + 8];
   const bool has_b = d.wb != nullptr;
@@ -439,6 +441,7 @@ extern "C" int rph_net_nparams(int nin, int h, int nout, int head, int* p_out, i
 }
 
 extern "C" int rph_train_step(const TrainDesc* d, int step, int epoch, void* stream) {
+  if (int rc = validate_train(d, 0, "rph_train_step")) return rc;
   hipStream_t s = (hipStream_t)stream;
   const uint32_t n_chunks = (uint32_t)((d->n_local + (1 << d->chunk_log2) - 1) >> d->chunk_log2);
   const Perm perm = make_perm(n_chunks, d->seed, (uint32_t)epoch, d->shuffle != 0);
@@ -454,6 +457,7 @@ extern "C" int rph_train_step(const TrainDesc* d, int step, int epoch, void* str
 
 // One launch per Keras fit() (persistent kernel, hedge_fit.h); world_size 1.
 extern "C" int rph_train_fit(const TrainDesc* d, int epochs, void* stream) {
+  if (int rc = validate_train(d, 2, "rph_train_fit")) return rc;
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E))         \
@@ -465,6 +469,7 @@ extern "C" int rph_train_fit(const TrainDesc* d, int epochs, void* stream) {
 
 // Lagged-update step kernel k of a fit (hedge_lag.h) and its finalize.
 extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* stream) {
+  if (int rc = validate_train(d, 1, "rph_train_lag_step")) return rc;
   hipStream_t s = (hipStream_t)stream;
   const uint32_t n_chunks = (uint32_t)((d->n_local + (1 << d->chunk_log2) - 1) >> d->chunk_log2);
   const Perm perm = make_perm(n_chunks, d->seed, (uint32_t)epoch, d->shuffle != 0);
@@ -484,6 +489,7 @@ extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* st
 }
 
 extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
+  if (int rc = validate_train(d, 1, "rph_train_lag_finalize")) return rc;
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
@@ -498,6 +504,7 @@ extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
 }
 
 extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* stream) {
+  if (!d->grad_out || !d->wts || !d->opt || !d->fit) return rph_report("rph_train_update", "null pointer");
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
@@ -512,6 +519,10 @@ extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* s
 }
 
 extern "C" int rph_eval(const EvalDesc* d, void* stream) {
+  if (!d->wa || !d->stats || d->n_local < 1 || d->num_wgs < 1 || d->nin < 1 || d->nin > MAXIN)
+    return rph_report("rph_eval", "bad eval descriptor");
+  for (int f = 0; f < d->nin; ++f)
+    if (!d->feat[f]) return rph_report("rph_eval", "null feature pointer");
   hipStream_t s = (hipStream_t)stream;
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \

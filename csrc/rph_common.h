@@ -9,6 +9,21 @@
 #define RPH_WAVE 64
 #define RPH_INLINE __device__ __forceinline__
 
+// Device-side invariant checks, compiled in only for `python -m rphedge.build
+// --debug` (-DRPH_DEBUG=1).  A failed check prints and ends the kernel (no
+// trap: a GPU fault would reset the device); use at kernel scope only.
+#if defined(RPH_DEBUG) && RPH_DEBUG
+#define RPH_DASSERT(cond)                                                                          \
+  do {                                                                                             \
+    if (!(cond)) {                                                                                 \
+      if (threadIdx.x == 0) printf("RPH_DASSERT %s:%d block %d: %s\n", __FILE__, __LINE__, (int)blockIdx.x, #cond); \
+      return;                                                                                      \
+    }                                                                                              \
+  } while (0)
+#else
+#define RPH_DASSERT(cond) do { } while (0)
+#endif
+
 namespace rph {
 
 // ---------------------------------------------------------------------------

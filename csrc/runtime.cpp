@@ -34,6 +34,11 @@ static int set_err(const char* what, int code, const char* msg) {
 
 extern "C" const char* rph_last_error() { return g_err; }
 
+// descriptor validation failures from the kernel launchers (hedge_mlp.hip)
+namespace rph {
+int rph_report(const char* what, const char* msg) { return set_err(what, -22, msg); }
+}  // namespace rph
+
 // ---------------------------------------------------------------------------
 // Layout self-check: the Python ctypes mirrors compare every offset.
 // ---------------------------------------------------------------------------

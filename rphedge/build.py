@@ -63,9 +63,10 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False, asan:
         "-L/opt/rocm/lib",
         "-lrccl",
     ]
-    if debug:
-        flags += ["-g", "-DRPH_DEBUG=1"]
     lib, stamp = LIB, STAMP
+    if debug:  # device RPH_DASSERT checks + host debug info: librphedge_debug.so (RPH_NATIVE_LIB=debug)
+        flags += ["-g", "-DRPH_DEBUG=1"]
+        lib, stamp = LIBDIR / "librphedge_debug.so", LIBDIR / "librphedge_debug.sha256"
     if asan:
         flags += ["-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
         lib, stamp = LIBDIR / "librphedge_asan.so", LIBDIR / "librphedge_asan.sha256"
@@ -75,7 +76,7 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False, asan:
     tmp = lib.with_suffix(".so.tmp")
     # one hipcc per translation unit in parallel (the kernels are template-heavy),
     # then one link into the shared object
-    objdir = LIBDIR / ("obj_asan" if asan else "obj")
+    objdir = LIBDIR / ("obj_asan" if asan else "obj_debug" if debug else "obj")
     objdir.mkdir(exist_ok=True)
     cflags = [f for f in flags if f not in ("-shared", "-lrccl") and not f.startswith("-L")]
     jobs = []

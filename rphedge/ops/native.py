@@ -19,7 +19,10 @@ import torch  # noqa: F401  (must be loaded before librphedge.so)
 
 from . import layout as L
 
-_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / "librphedge.so"
+# RPH_NATIVE_LIB=debug|asan selects the variant built by `python -m rphedge.build --debug|--asan`
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / (
+    {"debug": "librphedge_debug.so", "asan": "librphedge_asan.so"}.get(os.environ.get("RPH_NATIVE_LIB", ""),
+                                                                       "librphedge.so"))
 _lib = None
 _load_error: str | None = None
 
@@ -143,7 +146,8 @@ def load(required: bool | None = None):
         if not _LIB_PATH.exists() or os.environ.get("RPH_REBUILD"):
             from .. import build as _build
 
-            _build.build()
+            v = os.environ.get("RPH_NATIVE_LIB", "")
+            _build.build(debug=v == "debug", asan=v == "asan")
         lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
         _bind(lib)
         cap = 128
@@ -179,6 +183,10 @@ def ptr(t) -> int | None:
 
 
 def stream_handle(stream=None) -> int:
+    """HIP stream handle of a torch stream (None: the current stream; an int is
+    taken as a raw handle, 0 = the null stream)."""
+    if isinstance(stream, int):
+        return stream
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
 

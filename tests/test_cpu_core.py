@@ -145,3 +145,24 @@ def test_european_cpu_end_to_end():
     assert abs(res.v0 - 10.39) < 0.6
     assert abs(res.phi - 0.7285) < 0.08
     assert res.terminal_pnl["std"] < 3.5
+
+
+def test_launcher_rejects_bad_descriptors():
+    """Host-side validation in the native launchers (csrc/hedge_core.h
+    validate_train): a malformed descriptor never reaches the GPU — checked
+    here on CPU, where the library loads but no kernel may run."""
+    from rphedge.ops import native
+
+    native.load(required=True)
+    d = native.TrainDesc()
+    d.nin, d.h, d.nout, d.head = 1, 8, 2, 0
+    d.num_wgs, d.batch, d.n_local, d.steps_per_epoch = 0, 512, 4096, 8
+    with pytest.raises(RuntimeError, match="num_wgs"):
+        native.train_step(d, 0, 0, stream=0)
+    d.num_wgs = 16
+    d.steps_per_epoch = 2  # 2 x 512 < 4096
+    with pytest.raises(RuntimeError, match="batch"):
+        native.train_lag_step(d, 0, 0, stream=0)
+    d.steps_per_epoch = 8
+    with pytest.raises(RuntimeError, match="null state"):
+        native.train_fit(d, 1, stream=0)

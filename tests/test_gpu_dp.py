@@ -86,3 +86,49 @@ def test_fused_xgmi_allreduce_two_ranks_one_gpu(deterministic):
     assert np.array_equal(w0, w1)                      # bitwise-identical replicas
     ref, _ = _fit(0, 1, n, epochs, torch.device("cuda", 0), deterministic=deterministic)
     np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-5)
+
+
+def _worker_missing_peer(rank, world, port, out):
+    """Rank 1 never trains: rank 0's in-kernel exchange must time out (bounded
+    spin), raise dp_error, fail fast in the later steps and surface as an error
+    on the host (SURVEY §5.3 fault injection: a rank lost mid-all-reduce)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from torch.distributed import distributed_c10d as c10d
+
+    from rphedge.ops.native import IpcMailbox
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mb = IpcMailbox(rank, world, 128, c10d._get_default_store(), dev, tag="t_dp_fail")
+    dist.barrier()
+    status = "idle"
+    if rank == 0:
+        _fit(0, world, 1 << 13, 2, dev, mailbox=mb, deterministic=True)
+        try:
+            mb.check()
+            status = "no-error"
+        except RuntimeError as e:
+            status = "error:" + str(e)
+    with open(out + f".{rank}.txt", "w") as f:
+        f.write(status)
+    dist.barrier()
+    mb.close()
+    dist.destroy_process_group()
+
+
+def test_missing_peer_times_out_cleanly():
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "s")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_missing_peer, args=(r, world, port, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        status = open(out + ".0.txt").read()
+    assert status.startswith("error:") and "did not arrive" in status, status
