@@ -293,6 +293,14 @@ RPH_INLINE float ld_agent(const float* p) {
 
 constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contention / 8)
 
+// sum of the ACC_REPLICAS float-atomic replicas of packet entry i (fixed order)
+RPH_INLINE float sum_replicas(const float* buf, int R, int i) {
+  float rr[ACC_REPLICAS];
+#pragma unroll
+  for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
+  return ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+}
+
 // ---------------------------------------------------------------------------
 // Fused one-shot all-reduce of the gradient packet over xGMI (data parallel).
 // Runs in the last-arriving workgroup of every rank: push the local packet to

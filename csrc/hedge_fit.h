@@ -40,13 +40,6 @@ RPH_INLINE uint32_t ld_agent_u32(const uint32_t* p) {
   return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// sum of the ACC_REPLICAS float-atomic replicas of packet entry i (fixed order)
-RPH_INLINE float sum_replicas(const float* buf, int R, int i) {
-  float rr[ACC_REPLICAS];
-#pragma unroll
-  for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
-  return ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
-}
 
 template <class B>
 __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int epochs) {

@@ -34,9 +34,13 @@ namespace rph {
 // lag slot layout (floats): w[PMAX] m[PMAX] v[PMAX] scalars[16]
 enum LagScalar : int {
   LG_T = 0, LG_LR, LG_NAN, LG_BEST, LG_WAIT, LG_HASBEST, LG_LSUM, LG_ASUM, LG_PSUM, LG_CNT,
-  LG_LASTL, LG_LASTMAE, LG_LASTMAPE, LG_NSCALAR
+  LG_LASTL, LG_LASTMAE, LG_LASTMAPE, LG_SEQ /* DP sequence base, u32 bits */, LG_NSCALAR
 };
 constexpr int LAG_FLOATS = 3 * PMAX + 16;
+
+RPH_INLINE uint32_t ld_agent_u32c(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int P>
 struct LagState {
@@ -71,6 +75,10 @@ RPH_INLINE void lag_load(LagState<P>& st, const TrainDesc& d, const float* slot 
     st.sc[LG_LSUM] = f->loss_sum; st.sc[LG_ASUM] = f->abs_sum; st.sc[LG_PSUM] = f->ape_sum;
     st.sc[LG_CNT] = f->loss_cnt; st.sc[LG_LASTL] = f->last_loss; st.sc[LG_LASTMAE] = f->last_mae;
     st.sc[LG_LASTMAPE] = f->last_mape;
+    // data parallel: this fit's exchange sequence starts at the rank's device
+    // counter (written only at the end of a fit — never by a kernel that
+    // also reads it here, i.e. never by kernel 0)
+    st.sc[LG_SEQ] = __uint_as_float(d.dp_world > 1 ? ld_agent_u32c(d.dp_counter) : 0u);
   } else {
 #pragma unroll
     for (int j = 0; j < LG_NSCALAR; ++j) st.sc[j] = slot[3 * PMAX + j];
@@ -119,6 +127,65 @@ RPH_INLINE void lag_store_canonical(const LagState<P>& st, const TrainDesc& d, f
     f->epoch = (float)ep_done;
     f->stopped = stopped;
   }
+}
+
+// data parallel: the exchanges of a fit used sequence numbers seq_base+1 ..
+// seq_base+n; the next fit starts after them
+RPH_INLINE void lag_advance_seq(const TrainDesc& d, float seq_base_bits, uint32_t n) {
+  if (d.dp_world > 1 && threadIdx.x == 0)
+    __hip_atomic_store(d.dp_counter, __float_as_uint(seq_base_bits) + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Cross-rank sum of step k-1's packet (sequence `seq`), fused xGMI one-shot:
+// the pusher workgroup of every rank sums its local accumulator and stores it
+// into every rank's IPC mailbox (system scope), raises one flag per peer; EVERY
+// workgroup then waits for the W flags and sums the W packets in fixed rank
+// order (bitwise identical on all ranks and workgroups).  A rank can be at
+// most one kernel ahead of a peer, so the DP_SLOTS-deep slot of `seq` is
+// never overwritten while it is read.  Bounded spins; fail fast on dp_error.
+template <int R>
+RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* local_acc, float* red, bool pusher) {
+  const int tid = threadIdx.x;
+  const int W = d.dp_world, me = d.dp_rank;
+  const int slot = (int)(seq % DP_SLOTS);
+  if (pusher) {
+    for (int i = tid; i < R; i += 256) {
+      const float v = sum_replicas(local_acc, R, i);
+      for (int p = 0; p < W; ++p)
+        __hip_atomic_store(d.dp_mbox[p] + ((size_t)slot * W + me) * R + i, v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the flags
+    __syncthreads();
+    if (tid < W)
+      __hip_atomic_store(d.dp_flags[tid] + slot * W + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  int bad = 0;
+  if (tid < W) {
+    const uint32_t* fl = d.dp_flags[me] + slot * W + tid;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned it = 0;
+    while (__hip_atomic_load(const_cast<uint32_t*>(fl), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++it & 255u) == 0u &&
+          (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||  // 2 s: a peer never arrived
+           __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+        __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        bad = 1;
+        break;
+      }
+    }
+  }
+  if (__syncthreads_or(bad)) return 1;
+  for (int i = tid; i < R; i += 256) {
+    float a = 0.f;
+    for (int p = 0; p < W; ++p)
+      a += __hip_atomic_load(d.dp_mbox[me] + ((size_t)slot * W + p) * R + i, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    red[i] = a;
+  }
+  __syncthreads();
+  return 0;
 }
 
 // Keras-Adam update of step (e, s) from the summed packet `red` (LDS), then
@@ -239,17 +306,24 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   lag_load<P>(st, d, k == 0 ? nullptr : d.lag + (size_t)(k & 1) * LAG_FLOATS);
   typename B::Pre pre;
   B::load(d, s, perm, B::first(wid), lane, pre);
-  if (k > 0) lag_sums<R>(d.acc + (size_t)((k - 1) % 3) * ACC_REPLICAS * R, red);
+  const bool dp = d.dp_world > 1;
+  const float* prev = d.acc + (size_t)((k + 2) % 3) * ACC_REPLICAS * R;  // accumulator of step k-1
+  if (k > 0 && !dp) lag_sums<R>(prev, red);
   if (stopped0 != 0.f) return;  // early-stopped fit: the remaining steps are no-ops
   __syncthreads();
-  RPH_STAMP(1);
   const bool w0 = blockIdx.x == 0;
+  if (k > 0 && dp && lag_dp_exchange<R>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)k, prev, red, w0))
+    return;  // a peer timed out (dp_error is set; the host raises)
+  RPH_STAMP(1);
   if (k > 0) {
     const int kp = k - 1;
     const int ep = kp / S;
     int ep_done = ep;
     if (lag_apply<P>(st, red, d, ep, kp - ep * S, w0, ep_done)) {
-      if (w0) lag_store_canonical<P>(st, d, 1.f, ep_done);
+      if (w0) {
+        lag_store_canonical<P>(st, d, 1.f, ep_done);
+        lag_advance_seq(d, st.sc[LG_SEQ], (uint32_t)k);
+      }
       return;
     }
   }
@@ -288,14 +362,20 @@ __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, c
   if (d.fit->stopped != 0.f || K <= 0) return;
   LagState<P> st;
   lag_load<P>(st, d, d.lag + (size_t)(K & 1) * LAG_FLOATS);
-  lag_sums<R>(d.acc + (size_t)((K - 1) % 3) * ACC_REPLICAS * R, red);
-  __syncthreads();
+  const float* prev = d.acc + (size_t)((K - 1) % 3) * ACC_REPLICAS * R;
+  if (d.dp_world > 1) {
+    if (lag_dp_exchange<R>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)K, prev, red, true)) return;
+  } else {
+    lag_sums<R>(prev, red);
+    __syncthreads();
+  }
   const int S = d.steps_per_epoch;
   const int kp = K - 1, ep = kp / S;
   int ep_done = ep;
   const int stop = lag_apply<P>(st, red, d, ep, kp - ep * S, true, ep_done);
   // (a fit whose last launched step does not close an epoch keeps stopped = 0)
   lag_store_canonical<P>(st, d, stop ? 1.f : 0.f, ep_done);
+  lag_advance_seq(d, st.sc[LG_SEQ], (uint32_t)K);
 }
 
 }  // namespace rph

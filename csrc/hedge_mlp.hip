@@ -79,9 +79,11 @@ struct NarrowBody {
       // them as LDS broadcasts, so the kernel fits 256 registers = 2 waves/SIMD
       const float* __restrict__ Wi = W;
       if constexpr (WPE > 1) {
-        int z = 0;
+        // opaque 16-byte-aligned base: every use is a ds_read_b128 broadcast
+        // off ONE address register with an immediate offset
+        uint32_t z = 0;
         asm volatile("" : "+v"(z));
-        Wi = W + z;
+        Wi = (const float*)__builtin_assume_aligned(W + (z & ~3u), 16);
       }
       float x[NIN], pr[NHOLD];
 #pragma unroll

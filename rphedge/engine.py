@@ -322,7 +322,7 @@ class HipBackend:
         dp_fused = self.mailbox is not None and self.comm is None
         if t.step_mode == "persistent" and atomic and not poll_every and (self.world == 1 or dp_fused):
             return "persistent"
-        if t.step_mode in ("auto", "lag") and atomic and self.world == 1:
+        if t.step_mode in ("auto", "lag") and atomic and (self.world == 1 or dp_fused):
             return "lag"
         return "ticket"
 
