@@ -330,6 +330,13 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
 #pragma unroll
   for (int j = 0; j < LagState<P>::NPT; ++j)
     if (tid + 256 * j < P) wl[tid + 256 * j] = st.w[j];
+  if (w0) {
+    // persist the updated state and re-arm the accumulator of step k+1 now, so
+    // no optimizer state stays live (in registers) across the partial
+    float* z = d.acc + (size_t)((k + 1) % 3) * ACC_REPLICAS * R;
+    for (int i = tid; i < ACC_REPLICAS * R; i += 256) st_agent(z + i, 0.f);
+    lag_store<P>(st, d.lag + (size_t)((k + 1) & 1) * LAG_FLOATS);
+  }
   __syncthreads();
   RPH_STAMP(2);
   typename B::Frags fr;
@@ -338,7 +345,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   B::partial(d, s, perm, wl, fr, scratch, pre, val);
   RPH_STAMP(3);
 
-  // ---- epilogue: fire-and-forget adds; workgroup 0 persists the state ------------
+  // ---- epilogue: fire-and-forget adds ----------------------------------------------
   float* buf = d.acc + (size_t)(k % 3) * ACC_REPLICAS * R;
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
@@ -346,11 +353,6 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
     if (i < R)
       __hip_atomic_fetch_add(buf + (blockIdx.x % ACC_REPLICAS) * R + i, val[j], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (w0) {
-    float* z = d.acc + (size_t)((k + 1) % 3) * ACC_REPLICAS * R;
-    for (int i = tid; i < ACC_REPLICAS * R; i += 256) st_agent(z + i, 0.f);
-    lag_store<P>(st, d.lag + (size_t)((k + 1) & 1) * LAG_FLOATS);
   }
   RPH_STAMP(4);
 }
