@@ -171,16 +171,41 @@ extern "C" int rph_nccl_destroy(void* comm) {
 // IPC mailboxes for the fused xGMI all-reduce (one allocation per rank,
 // exported with hipIpcGetMemHandle and opened by every peer process).
 // ---------------------------------------------------------------------------
+// Mailboxes are written by PEER GPUs over xGMI and polled locally, so they are
+// allocated fine-grained (coherent across devices by memory type) when the
+// driver can export such an allocation; otherwise coarse-grained hipMalloc
+// (the kernels use system-scope stores/loads either way).
+static int g_ipc_finegrained = -1;  // 1/0 once decided
+
 extern "C" int rph_ipc_alloc(long long bytes, void** ptr_out, char* handle_out /*64 B*/) {
   void* p = nullptr;
-  HIP_TRY(hipMalloc(&p, (size_t)bytes));
-  HIP_TRY(hipMemset(p, 0, (size_t)bytes));
   hipIpcMemHandle_t h;
-  HIP_TRY(hipIpcGetMemHandle(&h, p));
+  bool done = false;
+  if (g_ipc_finegrained != 0 && hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained) == hipSuccess) {
+    if (hipIpcGetMemHandle(&h, p) == hipSuccess) {
+      done = true;
+      g_ipc_finegrained = 1;
+    } else {
+      (void)hipGetLastError();
+      (void)hipFree(p);
+      p = nullptr;
+      g_ipc_finegrained = 0;
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  if (!done) {
+    HIP_TRY(hipMalloc(&p, (size_t)bytes));
+    HIP_TRY(hipIpcGetMemHandle(&h, p));
+  }
+  HIP_TRY(hipMemset(p, 0, (size_t)bytes));
+  HIP_TRY(hipDeviceSynchronize());
   memcpy(handle_out, &h, sizeof(h));
   *ptr_out = p;
   return 0;
 }
+
+extern "C" int rph_ipc_is_finegrained() { return g_ipc_finegrained; }
 
 extern "C" int rph_ipc_open(const char* handle /*64 B*/, void** ptr_out) {
   hipIpcMemHandle_t h;

@@ -127,6 +127,7 @@ def _bind(lib):
         "rph_ipc_close": (C.c_int, [VP]),
         "rph_free": (C.c_int, [VP]),
         "rph_ipc_handle_size": (C.c_int, []),
+        "rph_ipc_is_finegrained": (C.c_int, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -362,6 +363,7 @@ class IpcMailbox:
         p = VP()
         _check(lib.rph_ipc_alloc(nbytes, C.byref(p), buf), "rph_ipc_alloc")
         self.own = p.value
+        self.finegrained = lib.rph_ipc_is_finegrained() == 1  # coherent-by-memory-type mailbox
         store.set(f"{tag}_{rank}", bytes(buf.raw[:hs]))
         self.ptrs, self.opened = [], []
         for q in range(world):
