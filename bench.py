@@ -84,6 +84,8 @@ def main(argv=None):
     from rphedge.api import HedgeRun
 
     di = D.init() if world > 1 else None
+    if di is not None and not a.cpu:
+        D.select_transport(di)  # in-kernel xGMI exchange if a probe fit is clean, else RCCL
     cfg = build_run(a, world)
     if a.cpu and di is None:
         di = D.DistInfo(device=torch.device("cpu"))
@@ -169,7 +171,9 @@ def main(argv=None):
                    "parallelism": f"dp{world}", "paths_global": n_total, "paths_per_gpu": run.n_local,
                    "epochs_first": a.epochs_first, "epochs_rest": a.epochs_rest,
                    "steps_per_epoch": run.backend.steps_per_epoch, "graph": use_graph,
-                   "backend": run.backend_kind},
+                   "backend": run.backend_kind,
+                   "step_schedule": run.backend.step_mode() if hasattr(run.backend, "step_mode") else "torch",
+                   "dp_transport": (run.di.dp_mode if world > 1 else None)},
         "quality": {"terminal_pnl_std": res.terminal_pnl["std"], "terminal_pnl_mean": res.terminal_pnl["mean"],
                     "V0": res.v0, "bs_price": res.summary.get("bs_price"), "phi0": res.phi,
                     "bs_delta": res.summary.get("bs_delta"),

@@ -321,8 +321,12 @@ class HipBackend:
         atomic = not t.deterministic and not t.split_update
         dp_fused = self.mailbox is not None and self.comm is None
         if t.step_mode == "persistent" and atomic and not poll_every and (self.world == 1 or dp_fused):
+            # (explicit only: needs every workgroup of every rank co-resident)
             return "persistent"
-        if t.step_mode in ("auto", "lag") and atomic and (self.world == 1 or dp_fused):
+        shared = dp_fused and getattr(self.mailbox, "shared_device", False)
+        if t.step_mode == "lag" and atomic and (self.world == 1 or dp_fused):
+            return "lag"
+        if t.step_mode == "auto" and atomic and (self.world == 1 or (dp_fused and not shared)):
             return "lag"
         return "ticket"
 

@@ -30,6 +30,7 @@ class DistInfo:
     comm: object = None          # native RCCL communicator (HIP path)
     initialized_here: bool = False
     dp_mode: str = "xgmi"        # xgmi: fused IPC all-reduce in the step kernel; rccl: RCCL + update kernel
+    shared_device: bool = False  # several local ranks on ONE GPU (single-GPU rehearsal of the DP path)
 
     @property
     def is_main(self) -> bool:
@@ -66,6 +67,8 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
         torch.cuda.set_device(dev)
     info = DistInfo(rank=rank, world=world, local_rank=local, device=dev,
                     dp_mode=os.environ.get("RPH_DP", "xgmi" if world <= 8 else "rccl"))
+    if use_gpu:
+        info.shared_device = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) > torch.cuda.device_count()
     if world > 1:
         be = backend or os.environ.get("RPH_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
@@ -100,7 +103,60 @@ def make_mailbox(info: DistInfo, R: int, tag: str = "rph_mbox"):
         return None
     from ..ops.native import IpcMailbox
 
-    return IpcMailbox(info.rank, info.world, R, _store(), info.device, tag=tag)
+    mb = IpcMailbox(info.rank, info.world, R, _store(), info.device, tag=tag)
+    # ranks sharing one GPU cannot use schedules whose EVERY workgroup waits for
+    # the peers (a peer's kernel may find no free CU): engine picks "ticket"
+    mb.shared_device = info.shared_device
+    return mb
+
+
+def _probe_xgmi(info: DistInfo) -> bool:
+    """Tiny data-parallel fit over the fused xGMI exchange (the default lagged
+    schedule): no peer timeout, and bitwise-identical weights on every rank."""
+    from ..engine import DateData, FitConfig, HipBackend, TrainConfig
+    from ..models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    mb = make_mailbox(info, spec.red_width, tag="rph_probe")
+    try:
+        n = 1 << 12
+        g = torch.Generator().manual_seed(100 + info.rank)          # different data per rank
+        x = (torch.rand(n, generator=g) * 0.6 + 0.7).to(info.device)
+        be = HipBackend(spec, n, TrainConfig(batch_size=n * info.world, chunk_log2=6), device=info.device,
+                        world=info.world, rank=info.rank, mailbox=mb)
+        data = DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=torch.relu(x - 1.0),
+                        prices_now=[x])
+        w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, FitConfig(epochs=4, patience=10 ** 6, early_stopping=False), seed=5)
+        torch.cuda.synchronize(info.device)
+        if int(mb.error[0].item()) != 0:
+            return False
+        wv = w[: spec.nparams].double()
+        mx, mn = wv.clone(), wv.clone()
+        all_reduce_(mx, "max")
+        all_reduce_(mn, "min")
+        return bool(torch.equal(mx, mn)) and bool(torch.isfinite(wv).all())
+    except Exception:
+        return False
+    finally:
+        mb.close()
+
+
+def select_transport(info: DistInfo) -> str:
+    """Probe-then-choose, like a collective library's transport selection: keep
+    the in-kernel xGMI exchange when a tiny DP fit over it is clean on every
+    rank, otherwise fall back to an RCCL all-reduce of the packet (+ update
+    kernel).  Runs once, outside any timed region; all ranks agree."""
+    if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
+        return info.dp_mode
+    ok = torch.tensor([1.0 if _probe_xgmi(info) else 0.0], dtype=torch.float64, device=info.device)
+    all_reduce_(ok, "min")
+    if float(ok.item()) < 1.0:
+        from ..ops.native import NcclComm
+
+        info.dp_mode = "rccl"
+        info.comm = NcclComm(info.rank, info.world, _store(), tag="rph_fallback")
+    return info.dp_mode
 
 
 def shard(n_total: int, world: int, rank: int) -> tuple[int, int]:
