@@ -136,13 +136,17 @@ RPH_INLINE void lag_advance_seq(const TrainDesc& d, float seq_base_bits, uint32_
     __hip_atomic_store(d.dp_counter, __float_as_uint(seq_base_bits) + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Cross-rank sum of step k-1's packet (sequence `seq`), fused xGMI one-shot:
-// the pusher workgroup of every rank sums its local accumulator and stores it
-// into every rank's IPC mailbox (system scope), raises one flag per peer; EVERY
-// workgroup then waits for the W flags and sums the W packets in fixed rank
-// order (bitwise identical on all ranks and workgroups).  A rank can be at
-// most one kernel ahead of a peer, so the DP_SLOTS-deep slot of `seq` is
-// never overwritten while it is read.  Bounded spins; fail fast on dp_error.
+// Cross-rank sum of step k-1's packet (sequence `seq`), fused xGMI one-shot
+// with DATA-TAGGED GRANULES: the pusher workgroup of every rank sums its local
+// accumulator and writes every entry as one 8-byte {value, seq} granule (a
+// single system-scope 64-bit store, single-copy atomic) into every rank's IPC
+// mailbox; every workgroup then polls the W granules of each entry until their
+// tags equal `seq` and sums the values in fixed rank order (bitwise identical
+// on all ranks and workgroups).  No separate flag hop: the load that observes
+// the tag also returns the data (MI355X_MICROARCH price list: 'handoff-1to1'
+// vs 'handoff-flag').  A rank can be at most one kernel ahead of a peer, so
+// slot seq % DP_SLOTS is never overwritten while it is read; a stale granule
+// carries an older tag.  Bounded spins; fail fast on dp_error.
 template <int R>
 RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* local_acc, float* red, bool pusher) {
   const int tid = threadIdx.x;
@@ -151,23 +155,36 @@ RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* lo
   if (pusher) {
     for (int i = tid; i < R; i += 256) {
       const float v = sum_replicas(local_acc, R, i);
-      for (int p = 0; p < W; ++p)
-        __hip_atomic_store(d.dp_mbox[p] + ((size_t)slot * W + me) * R + i, v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+      const unsigned long long g = ((unsigned long long)seq << 32) | (unsigned long long)__float_as_uint(v);
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (p < W)
+          __hip_atomic_store((unsigned long long*)d.dp_mbox[p] + ((size_t)slot * W + me) * R + i, g,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the flags
-    __syncthreads();
-    if (tid < W)
-      __hip_atomic_store(d.dp_flags[tid] + slot * W + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   int bad = 0;
-  if (tid < W) {
-    const uint32_t* fl = d.dp_flags[me] + slot * W + tid;
+  const unsigned long long* mb = (const unsigned long long*)d.dp_mbox[me] + (size_t)slot * W * R;
+  for (int i = tid; i < R; i += 256) {
+    float vals[8];
+    unsigned todo = (1u << W) - 1u;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     unsigned it = 0;
-    while (__hip_atomic_load(const_cast<uint32_t*>(fl), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+    while (true) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        if ((todo >> p) & 1u) {
+          const unsigned long long g = __hip_atomic_load(const_cast<unsigned long long*>(mb + (size_t)p * R + i),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((uint32_t)(g >> 32) == seq) {
+            vals[p] = __uint_as_float((uint32_t)g);
+            todo &= ~(1u << p);
+          }
+        }
+      }
+      if (todo == 0u) break;
       __builtin_amdgcn_s_sleep(1);
-      if ((++it & 255u) == 0u &&
+      if ((++it & 63u) == 0u &&
           (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||  // 2 s: a peer never arrived
            __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -175,22 +192,16 @@ RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* lo
         break;
       }
     }
-  }
-  if (__syncthreads_or(bad)) return 1;
-  for (int i = tid; i < R; i += 256) {
     float a = 0.f;
-    for (int p = 0; p < W; ++p)
-      a += __hip_atomic_load(d.dp_mbox[me] + ((size_t)slot * W + p) * R + i, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      if (p < W) a += vals[p];
     red[i] = a;
+    if (bad) break;
   }
-  __syncthreads();
-  return 0;
+  return __syncthreads_or(bad);
 }
 
-// Keras-Adam update of step (e, s) from the summed packet `red` (LDS), then
-// EarlyStopping if s closes the epoch.  Returns 1 when the fit stops here.
-// `writer`: this workgroup persists w_best / the loss history.
 template <int P>
 RPH_INLINE int lag_apply(LagState<P>& st, const float* red, const TrainDesc& d, int e, int s, bool writer,
                          int& ep_done) {

@@ -344,7 +344,9 @@ DP_SLOTS = 4
 class IpcMailbox:
     """Peer-mapped mailboxes for the fused xGMI gradient all-reduce.
 
-    Every rank hipMallocs ``[DP_SLOTS][W][R]`` floats + ``[DP_SLOTS][W]`` flags,
+    Every rank allocates ``[DP_SLOTS][W][R]`` 8-byte entries (a float + flag
+    pair per entry for the ticket path; a data-tagged {value, seq} granule for
+    the lagged path) + ``[DP_SLOTS][W]`` flags,
     exports an IPC handle through the torch.distributed store and opens every
     peer's handle.  The step kernel's last-arriving workgroup then writes its
     packet straight into each peer's HBM over xGMI (no RCCL launch, no extra
@@ -355,7 +357,7 @@ class IpcMailbox:
         if world > 8:
             raise ValueError("fused xGMI all-reduce supports up to 8 ranks (one node)")
         self.rank, self.world, self.R = rank, world, R
-        data_bytes = DP_SLOTS * world * R * 4
+        data_bytes = DP_SLOTS * world * R * 8
         self.flag_off = (data_bytes + 255) // 256 * 256
         nbytes = self.flag_off + DP_SLOTS * world * 4 + 256
         hs = lib.rph_ipc_handle_size()
