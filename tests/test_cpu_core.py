@@ -166,3 +166,38 @@ def test_launcher_rejects_bad_descriptors():
     d.steps_per_epoch = 8
     with pytest.raises(RuntimeError, match="null state"):
         native.train_fit(d, 1, stream=0)
+
+
+def test_keras_adam_matches_torch_optim_adam_cpu():
+    """Torch reference backend's Keras-Adam (K10 semantics) vs torch.optim.Adam
+    for 3 full-batch steps; the per-step matching torch eps is eps/sqrt(1-b2^t)."""
+    from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    n = 1024
+    x = torch.linspace(0.7, 1.3, n)
+    w0 = init_weights(spec, [0.5, 0.0])
+    lr, eps, b2 = 5e-3, 1e-7, 0.999
+    be = TorchBackend(spec, n, TrainConfig(batch_size=n, lr=lr, eps=eps, shuffle=False), device="cpu",
+                      dtype=torch.float64)
+    data = DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=torch.relu(x - 1), prices_now=[x])
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, FitConfig(epochs=3, patience=10 ** 6, early_stopping=False), seed=1)
+    wk = current_weights(spec, w)
+
+    o_ = spec.offsets
+    p = torch.tensor(w0, dtype=torch.float64, requires_grad=True)
+    X = x.double()[:, None]
+    opt = torch.optim.Adam([p], lr=lr, betas=(0.9, b2), eps=eps)
+    for t in range(1, 4):
+        for gr in opt.param_groups:
+            gr["eps"] = eps / math.sqrt(1 - b2 ** t)
+        opt.zero_grad()
+        a = torch.nn.functional.leaky_relu(X @ p[o_["W1"]:o_["b1"]].view(1, 8) + p[o_["b1"]:o_["W2"]], 0.3)
+        a = torch.nn.functional.leaky_relu(a @ p[o_["W2"]:o_["b2"]].view(8, 8) + p[o_["b2"]:o_["W3"]], 0.3)
+        h = a @ p[o_["W3"]:o_["b3"]].view(8, 2) + p[o_["b3"]:o_["P"]]
+        V = h[:, 0] * (x.double() * 1.01) + h[:, 1]
+        ((V - torch.relu(x.double() - 1)) ** 2).mean().backward()
+        opt.step()
+    np.testing.assert_allclose(wk, p.detach().numpy(), rtol=1e-5, atol=1e-7)

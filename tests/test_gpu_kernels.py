@@ -406,3 +406,45 @@ def test_step_modes_match_ticket_kernels(dev, mode):
     np.testing.assert_allclose(fp[L.F_HIST:L.F_HIST + 12], fs[L.F_HIST:L.F_HIST + 12], rtol=1e-4)
     np.testing.assert_allclose(wp, ws, rtol=1e-3, atol=1e-5)
     np.testing.assert_allclose(op[L.O_M:L.O_M + spec.nparams], os_[L.O_M:L.O_M + spec.nparams], rtol=1e-2, atol=1e-7)
+
+
+@pytest.mark.parametrize("mode", ["lag", "ticket"])
+def test_k10_first_step_matches_torch_optim_adam(dev, mode):
+    """K10 vs torch.optim.Adam: one full-batch step from the same
+    weights.  Keras' Adam adds eps to sqrt(v) before bias correction, so the
+    matching torch eps at step t is eps / sqrt(1 - beta2^t)."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(nin=3, hidden=8, nout=2, head=0)
+    n = 4096
+    g = torch.Generator().manual_seed(9)
+    feats = [torch.rand(n, generator=g) * 0.5 + 0.75 for _ in range(3)]
+    price = feats[0] * 1.02
+    target = torch.relu(price - 1.0)
+    w0 = init_weights(spec, [0.5, 0.1])
+    lr, eps, b2 = 1e-2, 1e-7, 0.999
+    be = HipBackend(spec, n, TrainConfig(batch_size=n, lr=lr, eps=eps, shuffle=False, step_mode=mode), device=dev)
+    data = DateData(feats=[f.to(dev) for f in feats], prices_next=[price.to(dev)], bond_next=1.03,
+                    target=target.to(dev), prices_now=[feats[0].to(dev)])
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, FitConfig(epochs=1, patience=10 ** 6, early_stopping=False), seed=1)
+    torch.cuda.synchronize()
+    wg = current_weights(spec, w)
+
+    # torch reference: fp64 autograd of the same MSE, torch.optim.Adam step
+    o_ = spec.offsets
+    p = torch.tensor(w0, dtype=torch.float64, requires_grad=True)
+    X = torch.stack(feats, 1).double()
+    W1 = p[o_["W1"]:o_["b1"]].view(3, 8); b1 = p[o_["b1"]:o_["W2"]]
+    W2 = p[o_["W2"]:o_["b2"]].view(8, 8); b2_ = p[o_["b2"]:o_["W3"]]
+    W3 = p[o_["W3"]:o_["b3"]].view(8, 2); b3 = p[o_["b3"]:o_["P"]]
+    a = torch.nn.functional.leaky_relu(X @ W1 + b1, 0.3)
+    a = torch.nn.functional.leaky_relu(a @ W2 + b2_, 0.3)
+    h = a @ W3 + b3
+    V = h[:, 0] * price.double() + h[:, 1] * 1.03
+    loss = ((V - target.double()) ** 2).mean()
+    opt = torch.optim.Adam([p], lr=lr, betas=(0.9, b2), eps=eps / math.sqrt(1 - b2))
+    loss.backward()
+    opt.step()
+    np.testing.assert_allclose(wg, p.detach().numpy(), rtol=1e-4, atol=2e-6)

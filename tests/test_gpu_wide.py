@@ -89,5 +89,9 @@ def test_wide_european_end_to_end(dev):  # noqa: F811
     run = HedgeRun(cfg)
     assert run.spec.hidden == 32
     res = run.run()
-    assert abs(res.v0 - 10.3896) < 0.35, res.v0
-    assert abs(res.phi - 0.7285) < 0.06, res.phi
+    # phi0 is stable; V0 (the net evaluated at the single point S0) scatters by
+    # +-0.5 between runs at this small budget (float-atomic summation order;
+    # tools/wide_e2e_check.py), so its band is wider than the 8-unit test's
+    assert abs(res.phi - 0.7285) < 0.03, res.phi
+    assert abs(res.v0 - 10.3896) < 0.8, res.v0
+    assert res.terminal_pnl["std"] < 1.3, res.terminal_pnl
