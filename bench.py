@@ -21,6 +21,16 @@ i.e. the same unit as the reference's Keras throughput (BASELINE.md:
 "Keras training step, batch 512 ... ≈85 k samples/s"), so
 vs_baseline = value / 85,333.  Scaling is weak (2^20 paths per GPU).
 Compute dtype is fp32 (>= the bf16 the config names).
+
+``--preset`` selects the other BASELINE.json configs (same metric, same
+one-run-per-step timing, simulation inside the graph):
+  euro30      (default) European call, 30-step GBM, 2^20 paths per GPU
+  heston30    Heston stochastic vol, 30 dates (10 Euler substeps each), 2^20 paths per GPU
+  euro252     European call, 252-step GBM, 2^21 paths per GPU (16M paths at 8 GPUs)
+  basket5     basket-of-5 European call, 252 steps, 2^23 paths per GPU (64M at 8 GPUs)
+  euro1_cpu   European call, 1-step GBM, 2^14 (>= 10k) paths, CPU torch backend (plumbing)
+Per-GPU path counts are the 8-GPU configs divided by 8 (weak scaling), so a
+1-GPU run measures exactly the per-GPU shard of the 8-GPU job.
 """
 from __future__ import annotations
 
@@ -37,40 +47,89 @@ BASELINE_SAMPLES_PER_S = 512 / 0.006   # median 6 ms per 512-sample
 METRIC = "MC paths/sec training 30-step hedge-MLP + terminal P&L std-dev, 1/2/4/8 MI355X"
 
 
+# BASELINE.json configs -> (model, dates, Euler substeps per date, paths per GPU log2, epochs first/rest,
+# per-GPU batch log2, lr first/rest, extra RunConfig fields)
+PRESETS = {
+    "euro30": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
+                   batch_log2=18, lr=2e-2, lr_rest=4e-3,
+                   label="European call, 30-step GBM, 1M Sobol paths per GPU"),
+    "heston30": dict(model="heston", dates=30, substeps=10, paths_log2=20, epochs_first=1024, epochs_rest=16,
+                     batch_log2=18, lr=2e-2, lr_rest=4e-3,
+                     extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
+                     label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
+    "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
+                    batch_log2=18, lr=2e-2, lr_rest=4e-3,
+                    label="European call, 252-step GBM, 2M paths per GPU (16M at 8 GPUs)"),
+    "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
+                    batch_log2=18, lr=1e-2, lr_rest=1e-3,
+                    extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
+                    label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
+    "euro1_cpu": dict(model="gbm_log", dates=1, substeps=1, paths_log2=14, epochs_first=200, epochs_rest=0,
+                      batch_log2=11, lr=1e-2, lr_rest=1e-3, cpu=True,
+                      label="European call, 1-step GBM, 16k (>=10k) Sobol paths, CPU plumbing"),
+}
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--paths-log2", type=int, default=20, help="paths PER GPU (weak scaling)")
-    ap.add_argument("--dates", type=int, default=30)
-    ap.add_argument("--epochs-first", type=int, default=512)
-    ap.add_argument("--epochs-rest", type=int, default=12)
-    ap.add_argument("--batch-log2", type=int, default=18, help="per-GPU minibatch (global = N x this)")
-    ap.add_argument("--lr", type=float, default=2e-2)
-    ap.add_argument("--lr-rest", type=float, default=4e-3)
+    ap.add_argument("--preset", default="euro30", choices=sorted(PRESETS))
+    ap.add_argument("--paths-log2", type=int, default=None, help="paths PER GPU (weak scaling)")
+    ap.add_argument("--dates", type=int, default=None)
+    ap.add_argument("--substeps", type=int, default=None, help="fine Euler steps per rebalancing date")
+    ap.add_argument("--epochs-first", type=int, default=None)
+    ap.add_argument("--epochs-rest", type=int, default=None)
+    ap.add_argument("--batch-log2", type=int, default=None, help="per-GPU minibatch (global = N x this)")
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--lr-rest", type=float, default=None)
     ap.add_argument("--lr-decay", type=float, default=0.02, help="per-date geometric LR decay factor (last/first epoch)")
     ap.add_argument("--hidden", type=int, default=8, help="hidden width (8 = reference net; 32 = MFMA kernel)")
     ap.add_argument("--mfma-precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    pre = PRESETS[a.preset]
+    for k in ("paths_log2", "dates", "substeps", "epochs_first", "epochs_rest", "batch_log2", "lr", "lr_rest"):
+        if getattr(a, k) is None:
+            setattr(a, k, pre[k])
+    if pre.get("cpu"):
+        a.cpu = True
+    return a
 
 
 def build_run(a, world: int):
     from rphedge.config import RunConfig, TrainingParams, ParityFlags
-    from rphedge.api import HedgeRun
 
+    pre = PRESETS[a.preset]
     tr = TrainingParams(batch_size=(1 << a.batch_log2) * world, epochs_first=a.epochs_first,
                         epochs_rest=a.epochs_rest, patience_first=10 ** 6, patience_rest=10 ** 6,
                         lr=a.lr, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
                         chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision)
-    cfg = RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
-                    dt=1.0 / a.dates, n_paths=a.paths_log2 + int(math.log2(world)), payoff="call",
-                    option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0, keep_paths=False,
-                    verbose=False, train=tr, parity=ParityFlags(), backend="torch" if a.cpu else None)
-    return cfg
+    model = pre["model"]
+    kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
+              dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
+              payoff="basket_call" if model == "basket" else "call", option_type="CALL",
+              model=model, mortality=False, N=1, P=1.0, keep_paths=False, verbose=False, train=tr,
+              parity=ParityFlags(), backend="torch" if a.cpu else None)
+    kw.update(pre.get("extra", {}))
+    return RunConfig(**kw)
+
+
+def anchor(cfg) -> dict:
+    """Closed-form price/delta of the preset's option (quality anchor)."""
+    from rphedge import analytic
+
+    if cfg.model == "heston":
+        p, dlt = analytic.heston_price(cfg.Y, cfg.K, cfg.r, cfg.T, cfg.kappa, cfg.theta, cfg.xi, cfg.rho, cfg.v0,
+                                       cfg.option_type)
+        return {"analytic": "heston", "price": p, "delta": dlt}
+    if cfg.model == "basket":
+        return {"analytic": None}
+    p, dlt = analytic.black_scholes(cfg.Y, cfg.K, cfg.r, cfg.sigma, cfg.T, cfg.option_type)
+    return {"analytic": "black_scholes", "price": p, "delta": dlt}
 
 
 def main(argv=None):
@@ -95,6 +154,7 @@ def main(argv=None):
     # lr schedule: first date a.lr, later dates a.lr_rest (constant per date; see FitConfig)
     run.build()
     def sched(lr0, n):
+        n = max(n, 1)
         if n <= 1 or a.lr_decay == 1.0:
             return tuple([lr0] * n)
         return tuple(lr0 * a.lr_decay ** (e / (n - 1)) for e in range(n))
@@ -165,9 +225,17 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": value / BASELINE_SAMPLES_PER_S,
         "dtype": "fp32" if (a.hidden == 8 or a.mfma_precision == "fp32") else "bf16",
-        "data": "synthetic (Sobol-QMC GBM paths generated on device; random-init N(0,0.1) weights)",
-        "config": {"model": f"hedge-MLP 1-{a.hidden}-{a.hidden}-2 (LeakyReLU 0.3), European call S0=K=100 r=0.08 sigma=0.15 T=1",
+        "data": f"synthetic (Sobol-QMC {cfg.model} paths generated {'on device' if gpu else 'on host'}; "
+                "random-init N(0,0.1) weights)",
+        "config": {"model": f"hedge-MLP {run.spec.nin}-{a.hidden}-{a.hidden}-{run.spec.nout} (LeakyReLU 0.3), "
+                            + PRESETS[a.preset]["label"],
+                   "preset": a.preset,
                    "global_batch": cfg.train.batch_size, "seq_len": n_dates,
+                   "substeps": a.substeps, "option": {k: getattr(cfg, k) for k in
+                                                      ("Y", "K", "T", "r", "sigma", "kappa", "theta", "xi",
+                                                       "rho", "v0", "n_assets", "basket_corr")
+                                                      if cfg.model in ("heston", "basket") or
+                                                      k in ("Y", "K", "T", "r", "sigma")},
                    "parallelism": f"dp{world}", "paths_global": n_total, "paths_per_gpu": run.n_local,
                    "epochs_first": a.epochs_first, "epochs_rest": a.epochs_rest,
                    "steps_per_epoch": run.backend.steps_per_epoch, "graph": use_graph,
@@ -175,8 +243,9 @@ def main(argv=None):
                    "step_schedule": run.backend.step_mode() if hasattr(run.backend, "step_mode") else "torch",
                    "dp_transport": (run.di.dp_mode if world > 1 else None)},
         "quality": {"terminal_pnl_std": res.terminal_pnl["std"], "terminal_pnl_mean": res.terminal_pnl["mean"],
-                    "V0": res.v0, "bs_price": res.summary.get("bs_price"), "phi0": res.phi,
-                    "bs_delta": res.summary.get("bs_delta"),
+                    "V0": res.v0, "phi0": res.phi, "psi0": res.psi,
+                    "anchor": anchor(cfg),
+                    "mc_discounted_payoff": res.summary["E_payoff"] * run.scale * math.exp(-cfg.r * cfg.T),
                     "reference_terminal_pnl_std_52step": 1.7504, "reference_V0": 11.352},
         "paths_per_sec_full_run": n_total / (ms / 1000.0),
     }

@@ -110,11 +110,16 @@ class HedgeRun:
         c = self.cfg
         return float(c.N * c.P) if self.kind == "pension" else float(c.Y)
 
-    def simulate(self):
-        """Paths (K1–K6) and terminal value V_T (K7) on the coarse grid."""
+    def simulate(self, into: P.Paths | None = None):
+        """Paths (K1–K6) and terminal value V_T (K7) on the coarse grid.
+
+        ``into``: re-simulate into the buffers of the existing paths and
+        terminal value (no allocation, no host synchronisation), so the
+        simulation can be captured into the run's hipGraph."""
         c, g, dev = self.cfg, self.grid, self.device
         fp64 = c.dtype == "fp64"
-        kw = dict(device=dev, offset=self.offset, stream=self.stream)
+        kw = dict(device=dev, offset=self.offset, stream=self.stream, out=into)
+        vt_out = self.v_terminal if into is not None else None
         with self.timer.phase("simulate"):
             if self.kind == "european":
                 if c.model == "heston":
@@ -127,7 +132,7 @@ class HedgeRun:
                 # EO normalises BOTH prices by S0 (cell 13: _B_t = B/S0, so psi counts
                 # unit bonds); the corrected default quotes the bond in S0 units.
                 p.bond = g.bond(c.r, norm=c.Y if c.parity.complement_head else 1.0)
-                v_t = P.payoff(c.option_type.lower(), p, c.K / c.Y, stream=self.stream)
+                v_t = P.payoff(c.option_type.lower(), p, c.K / c.Y, stream=self.stream, out=vt_out)
             elif self.kind == "basket":
                 na = c.n_assets
                 corr = np.full((na, na), c.basket_corr) + np.eye(na) * (1 - c.basket_corr)
@@ -135,7 +140,7 @@ class HedgeRun:
                 p = P.simulate_basket(g, self.n_local, s0, [c.r] * na, [c.sigma] * na, corr, norm=s0, **kw)
                 p.bond = g.bond(c.r)
                 w = c.basket_weights or tuple([1.0 / na] * na)
-                v_t = P.payoff("basket_call", p, c.K / c.Y, weights=w, stream=self.stream)
+                v_t = P.payoff("basket_call", p, c.K / c.Y, weights=w, stream=self.stream, out=vt_out)
             else:
                 if c.model in ("sv_ref", "heston"):
                     sv_c = c.sv_c
@@ -147,6 +152,8 @@ class HedgeRun:
                                                                                    else "arith"),
                                        fp64=fp64, **kw)
                 if c.mortality:
+                    if into is not None and c.parity.numpy_binomial:
+                        raise NotImplementedError("numpy binomial (Q20 parity) runs on the host: not graph-safe")
                     P.simulate_mortality(p, c.l0, c.c, c.ita, c.N, lambda_fine_index=c.parity.lambda_fine_index,
                                          fp64=fp64, numpy_binomial=c.parity.numpy_binomial,
                                          stream=self.stream)
@@ -154,13 +161,14 @@ class HedgeRun:
                     p.kind = "pension_nomort"
                 p.bond = g.bond(c.r)
                 if not c.parity.fine_terminal_payoff:
-                    p.S_final = p.S[-1].clone()
-                    if p.nfrac is not None:
-                        p.nfrac_final = p.nfrac[-1].clone()
+                    if into is None:
+                        p.S_final = p.S[-1].clone()
+                    else:
+                        p.S_final.copy_(p.S[-1])
                 if p.nfrac is not None:
                     # the coarse terminal survivors are what the liability is paid on (RP:184)
                     p.nfrac_final = p.nfrac[-1]
-                v_t = P.payoff("guarantee", p, c.K, stream=self.stream)
+                v_t = P.payoff("guarantee", p, c.K, stream=self.stream, out=vt_out)
         self.paths, self.v_terminal = p, v_t
         return p, v_t
 
@@ -280,23 +288,11 @@ class HedgeRun:
         return g
 
     def _enqueue_sim_into_existing(self):
-        """Re-run the path kernels into the SAME buffers (graph-safe, no allocation)."""
-        c, g, p = self.cfg, self.grid, self.paths
-        from .ops import native
-        from .ops.sobol import device_table
-
-        if self.kind == "european" and c.model in ("gbm", "gbm_log"):
-            sv, sh, dims = device_table(g.n_fine, P.SEED_W1, self.device)
-            d = P._desc(L.SIM_GBM_LOG if c.model == "gbm_log" else L.SIM_GBM_ARITH, self.n_local, self.offset, g,
-                        c.dtype == "fp64", False)
-            d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), dims
-            d.s0[0], d.mu[0], d.sigma[0], d.inv_norm[0] = c.Y, c.r, c.sigma, 1.0 / c.Y
-            d.out, d.final_out = p.S.data_ptr(), p.S_final.data_ptr()
-            native.simulate(d, self.stream)
-            native.payoff({"call": 1, "put": 2}[c.option_type.lower()], p.S_final, self.v_terminal, c.K / c.Y,
-                          stream=self.stream)
-        else:
-            raise NotImplementedError("in-graph resimulation implemented for European GBM (bench config)")
+        """Re-run the path and payoff kernels into the SAME buffers (graph-safe,
+        no allocation) — every model family (GBM, SV/Heston, basket, mortality)."""
+        if self.device.type != "cuda":
+            raise RuntimeError("in-place re-simulation needs the GPU path kernels")
+        self.simulate(into=self.paths)
 
     def replay(self):
         self.graph.replay(self.stream or torch.cuda.current_stream(self.device))

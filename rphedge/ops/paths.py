@@ -118,11 +118,14 @@ def _desc(model, n_local, offset, grid: Grid, fp64, parity):
 
 def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, scheme: str = "arith",
                  norm: float = 1.0, device="cuda", offset: int = 0, fp64: bool = False, seed: int = SEED_W1,
-                 stream=None) -> Paths:
-    """Fund/stock GBM on the fine grid, stored on the coarse grid (K1+K2+K3)."""
+                 stream=None, out: Paths | None = None) -> Paths:
+    """Fund/stock GBM on the fine grid, stored on the coarse grid (K1+K2+K3).
+
+    ``out``: re-simulate into the buffers of an existing :class:`Paths`
+    (no allocation: graph-capturable)."""
     dev = torch.device(device)
-    S = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
-    fin = torch.empty(n_local, dtype=torch.float32, device=dev)
+    S = out.S if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    fin = out.S_final if out is not None else torch.empty(n_local, dtype=torch.float32, device=dev)
     if _dev_is_gpu(dev):
         from . import native
 
@@ -136,6 +139,8 @@ def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, s
         s_np, f_np = _cpu_gbm(grid, n_local, s0, mu, sigma, scheme, offset, seed)
         S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
+    if out is not None:
+        return out
     return Paths(kind="gbm", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
                  S_final=fin, norm=norm)
 
@@ -143,12 +148,12 @@ def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, s
 def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model: str = "sv_ref",
                 a=0.0, b=0.0, c=0.0, kappa=0.0, theta=0.0, xi=0.0, rho=0.0, norm: float = 1.0,
                 device="cuda", offset: int = 0, fp64: bool = False, parity_nan: bool = False,
-                seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None) -> Paths:
+                seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None, out: Paths | None = None) -> Paths:
     """Reference CIR-on-sigma SV (RP:282-289) or full-truncation Heston (K4)."""
     dev = torch.device(device)
-    S = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
-    V = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
-    fin = torch.empty(n_local, dtype=torch.float32, device=dev)
+    S = out.S if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    V = out.vol if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    fin = out.S_final if out is not None else torch.empty(n_local, dtype=torch.float32, device=dev)
     mcode = L.SIM_SV_REF if model == "sv_ref" else L.SIM_HESTON
     if _dev_is_gpu(dev):
         from . import native
@@ -169,20 +174,22 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
         S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
         V.copy_(torch.from_numpy(v_np.astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
+    if out is not None:
+        return out
     return Paths(kind="heston" if model == "heston" else "sv", grid=grid, n_local=n_local, path_offset=offset,
                  S=S, vol=V, bond=grid.bond(0.0), S_final=fin, norm=norm)
 
 
 def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, device="cuda", offset: int = 0,
-                    seed: int = SEED_W1, stream=None) -> Paths:
+                    seed: int = SEED_W1, stream=None, out: Paths | None = None) -> Paths:
     """Correlated log-GBM basket (K3 basket variant)."""
     na = len(s0)
     norm = np.asarray(norm if norm is not None else s0, dtype=np.float64)
     C = np.asarray(corr, dtype=np.float64)
     chol = np.linalg.cholesky(C)
     dev = torch.device(device)
-    S = torch.empty(grid.n_coarse, na, n_local, dtype=torch.float32, device=dev)
-    fin = torch.empty(na, n_local, dtype=torch.float32, device=dev)
+    S = out.S if out is not None else torch.empty(grid.n_coarse, na, n_local, dtype=torch.float32, device=dev)
+    fin = out.S_final if out is not None else torch.empty(na, n_local, dtype=torch.float32, device=dev)
     if _dev_is_gpu(dev):
         from . import native
 
@@ -201,6 +208,8 @@ def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, de
         s_np, f_np = _cpu_basket(grid, n_local, s0, mu, sigma, chol, offset, seed)
         S.copy_(torch.from_numpy((s_np / norm[None, :, None]).astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm[:, None]).astype(np.float32)))
+    if out is not None:
+        return out
     p = Paths(kind="basket", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
               S_final=fin, norm=float(norm[0]), na=na)
     p.meta["norms"] = norm
@@ -213,9 +222,10 @@ def simulate_mortality(paths: Paths, l0: float, c: float, eta: float, n0: int, l
     """Mortality intensity + binomial survivors (K5+K6); attaches nfrac/lam to ``paths``."""
     grid, n_local, offset = paths.grid, paths.n_local, paths.path_offset
     dev = paths.S.device if device is None else torch.device(device)
-    NF = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
-    LM = torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
-    NT = torch.empty(n_local, dtype=torch.float32, device=dev)
+    reuse = paths.nfrac is not None and paths.lam is not None and paths.meta.get("nfrac_final_buf") is not None
+    NF = paths.nfrac if reuse else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    LM = paths.lam if reuse else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
+    NT = paths.meta["nfrac_final_buf"] if reuse else torch.empty(n_local, dtype=torch.float32, device=dev)
     if _dev_is_gpu(dev):
         from . import native
 
@@ -233,21 +243,27 @@ def simulate_mortality(paths: Paths, l0: float, c: float, eta: float, n0: int, l
         NT.copy_(torch.from_numpy(nt.astype(np.float32)))
     paths.kind = "pension"
     paths.nfrac, paths.lam, paths.nfrac_final = NF, LM, NT
+    paths.meta["nfrac_final_buf"] = NT
     return paths
 
 
-def payoff(kind: str, paths: Paths, strike: float, weights=None, stream=None) -> torch.Tensor:
-    """Terminal value V_T in normalised units (K7)."""
+def payoff(kind: str, paths: Paths, strike: float, weights=None, stream=None, out: torch.Tensor | None = None
+           ) -> torch.Tensor:
+    """Terminal value V_T in normalised units (K7); ``out`` reuses a buffer."""
     S = paths.S_final
     n = paths.n_local
-    out = torch.empty(n, dtype=torch.float32, device=S.device)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=S.device)
     code = {"guarantee": 0, "call": 1, "put": 2, "basket_call": 3}[kind]
     if S.is_cuda:
         from . import native
 
         w = None
-        if code == 3:
-            w = torch.tensor(np.asarray(weights, np.float32), device=S.device)
+        if code == 3:  # cached per Paths: no host->device copy on re-simulation (graph capture)
+            key = ("basket_w", tuple(float(x) for x in weights))
+            w = paths.meta.get(key)
+            if w is None:
+                w = paths.meta[key] = torch.tensor(np.asarray(weights, np.float32), device=S.device)
         native.payoff(code, S, out, strike, nfrac=paths.nfrac_final if code == 0 else None, wts=w, na=paths.na,
                       stream=stream)
         return out

@@ -13,10 +13,14 @@ sys.path.insert(0, ".")
 import bench  # noqa: E402
 
 
-def one(batch_log2, ef, er, lr, lr_rest, decay, graph, paths_log2=20, dates=30):
-    argv = ["--paths-log2", str(paths_log2), "--dates", str(dates), "--epochs-first", str(ef), "--epochs-rest",
-            str(er), "--batch-log2", str(batch_log2), "--lr", str(lr), "--lr-rest", str(lr_rest), "--steps", "2",
-            "--warmup", "1", "--lr-decay", str(decay), "--json-out", "/tmp/_sweep.json"]
+FLAG = {"ef": "--epochs-first", "er": "--epochs-rest", "lr_rest": "--lr-rest", "decay": "--lr-decay"}
+
+
+def one(graph=True, **kw):
+    """One bench.py run; keys are bench flags (underscores) or the short names in FLAG."""
+    argv = ["--steps", "2", "--warmup", "1", "--json-out", "/tmp/_sweep.json"]
+    for k, v in kw.items():
+        argv += [FLAG.get(k, "--" + k.replace("_", "-")), str(v)]
     if not graph:
         argv.append("--no-graph")
     import contextlib
@@ -26,10 +30,10 @@ def one(batch_log2, ef, er, lr, lr_rest, decay, graph, paths_log2=20, dates=30):
     with contextlib.redirect_stdout(buf):
         bench.main(argv)
     r = json.loads(open("/tmp/_sweep.json").read())
-    return {"batch_log2": batch_log2, "ef": ef, "er": er, "lr": lr, "lr_rest": lr_rest, "decay": decay,
-            "ms": round(r["ms_per_step"], 2), "V0": round(r["quality"]["V0"], 4),
-            "pnl_std": round(r["quality"]["terminal_pnl_std"], 4), "phi0": round(r["quality"]["phi0"], 4),
-            "value": r["value"]}
+    q = r["quality"]
+    return dict(kw, ms=round(r["ms_per_step"], 2), V0=round(q["V0"], 4), pnl_std=round(q["terminal_pnl_std"], 4),
+                phi0=round(q["phi0"], 4), anchor=q["anchor"].get("price"), mc=round(q["mc_discounted_payoff"], 4),
+                value=r["value"])
 
 
 if __name__ == "__main__":
