@@ -87,6 +87,8 @@ def parse(argv=None):
     ap.add_argument("--lr-decay", type=float, default=0.02, help="per-date geometric LR decay factor (last/first epoch)")
     ap.add_argument("--hidden", type=int, default=8, help="hidden width (8 = reference net; 32 = MFMA kernel)")
     ap.add_argument("--mfma-precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--variant", type=int, default=-1, help="narrow lag-kernel variant (-1: engine default)")
+    ap.add_argument("--max-wgs", type=int, default=256, help="workgroups per training step")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -107,7 +109,8 @@ def build_run(a, world: int):
     tr = TrainingParams(batch_size=(1 << a.batch_log2) * world, epochs_first=a.epochs_first,
                         epochs_rest=a.epochs_rest, patience_first=10 ** 6, patience_rest=10 ** 6,
                         lr=a.lr, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
-                        chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision)
+                        chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision,
+                        variant=a.variant, max_wgs=a.max_wgs)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),

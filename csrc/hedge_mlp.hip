@@ -31,9 +31,13 @@ namespace rph {
 // (the reference's 8-unit nets).  Used by the per-step kernel below and by the
 // persistent per-fit kernel (hedge_fit.h).
 // ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD, int WPE = 1>
+template <int NIN, int H, int NO, int HEAD, int WPE = 1, int PFD = 1>
 struct NarrowBody {
   static constexpr int WAVES_PER_SIMD = WPE;
+  // path-data prefetch distance in loop iterations (1: the next path is loaded
+  // while the current one computes; >1 keeps PFD loads in flight, so a thread's
+  // later paths never wait on a fresh L2/MALL round trip)
+  static constexpr int PF = PFD;
   using S = NetShape<NIN, H, NO, HEAD>;
   static constexpr int P = S::P;
   static constexpr int R = S::R;
@@ -73,6 +77,15 @@ struct NarrowBody {
 #pragma unroll
     for (int i = 0; i < R; ++i) g[i] = 0.f;
     const float alpha = d.alpha;
+    // ring of prefetched paths: q[0] = current (loaded by the caller), q[i] the
+    // path i iterations ahead
+    Pre q[PF];
+    q[0] = pre;
+#pragma unroll
+    for (int i = 1; i < PF; ++i) {
+      q[i].valid = false;
+      if (first(wid) + i * stride < d.batch) load(d, step, perm, first(wid) + i * stride, lane, q[i]);
+    }
     for (long long j0 = first(wid); j0 < d.batch; j0 += stride) {
       // WPE 1: the loop-invariant LDS weights are hoisted into registers (AGPR
       // overflow); WPE 2: an opaque zero offset makes every iteration re-read
@@ -87,12 +100,14 @@ struct NarrowBody {
       }
       float x[NIN], pr[NHOLD];
 #pragma unroll
-      for (int f = 0; f < NIN; ++f) x[f] = pre.x[f];
+      for (int f = 0; f < NIN; ++f) x[f] = q[0].x[f];
 #pragma unroll
-      for (int k = 0; k < NHOLD; ++k) pr[k] = pre.pr[k];
-      const float y = pre.y;
-      const bool valid = pre.valid;
-      if (j0 + stride < d.batch) load(d, step, perm, j0 + stride, lane, pre);  // software pipelining
+      for (int k = 0; k < NHOLD; ++k) pr[k] = q[0].pr[k];
+      const float y = q[0].y;
+      const bool valid = q[0].valid;
+#pragma unroll
+      for (int i = 0; i + 1 < PF; ++i) q[i] = q[i + 1];
+      if (j0 + PF * stride < d.batch) load(d, step, perm, j0 + PF * stride, lane, q[PF - 1]);  // software pipelining
 
       float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
       net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold);
@@ -477,12 +492,16 @@ extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* st
   const Perm perm = make_perm(n_chunks, d->seed, (uint32_t)epoch, d->shuffle != 0);
 #define X(A, B, C, E)                                                                                 \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                        \
-    if (d->variant == 1)                                                                              \
-      hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 2>>), dim3(d->num_wgs), dim3(256), 0, s, *d, \
-                         k, epoch, perm);                                                             \
-    else                                                                                              \
-      hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, *d, k, \
-                         epoch, perm);                                                                \
+    switch (d->variant) {                                                                             \
+      case 1: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 2>>), dim3(d->num_wgs), dim3(256), 0, s, \
+                                 *d, k, epoch, perm); break;                                           \
+      case 2: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 1, 3>>), dim3(d->num_wgs), dim3(256), 0, \
+                                 s, *d, k, epoch, perm); break;                                        \
+      case 3: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 2, 3>>), dim3(d->num_wgs), dim3(256), 0, \
+                                 s, *d, k, epoch, perm); break;                                        \
+      default: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, \
+                                  *d, k, epoch, perm);                                                 \
+    }                                                                                                 \
     return (int)hipGetLastError();                                                                    \
   }
   RPH_SHAPES(X)

@@ -218,6 +218,8 @@ class HedgeRun:
         tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
                            lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs,
                            mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode)
+        if int(tr.variant) >= 0:
+            tcfg.variant = int(tr.variant)
         kw = {}
         if self.backend_kind == "hip" and self.di.world > 1:
             self.mailbox = D.make_mailbox(self.di, self.spec.red_width)

@@ -70,6 +70,7 @@ class TrainingParams:
     hidden: int = 8                  # hidden width: 8 = reference nets (VALU kernel), 32 = MFMA kernel
     mfma_precision: str = "bf16"     # 32-unit nets: "bf16" (32x32x16 MFMA) or "fp32" (exact 32x32x2 MFMA)
     step_mode: str = "auto"          # GPU step schedule: auto | lag | ticket | persistent (engine.TrainConfig)
+    variant: int = -1                # narrow lag-kernel variant (-1: engine default; see engine.TrainConfig)
 
 
 @dataclass

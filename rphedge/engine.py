@@ -84,7 +84,9 @@ class TrainConfig:
     #   "persistent" one resident kernel per fit with an in-kernel grid barrier
     #   "auto"       lag where valid (1 rank, float-atomic reduction), else ticket
     step_mode: str = "auto"
-    variant: int = 0               # narrow lag kernel: 1 = 2 waves/SIMD with LDS weight re-reads
+    # narrow lag kernel: bit 0 = 2 waves/SIMD with LDS weight re-reads,
+    # bit 1 = path-data prefetch 2 iterations deeper (3 loads in flight)
+    variant: int = 0
 
 
 @dataclass

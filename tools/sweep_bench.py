@@ -18,7 +18,7 @@ FLAG = {"ef": "--epochs-first", "er": "--epochs-rest", "lr_rest": "--lr-rest", "
 
 def one(graph=True, **kw):
     """One bench.py run; keys are bench flags (underscores) or the short names in FLAG."""
-    argv = ["--steps", "2", "--warmup", "1", "--json-out", "/tmp/_sweep.json"]
+    argv = ["--steps", str(kw.pop("steps", 2)), "--warmup", "1", "--json-out", "/tmp/_sweep.json"]
     for k, v in kw.items():
         argv += [FLAG.get(k, "--" + k.replace("_", "-")), str(v)]
     if not graph:
