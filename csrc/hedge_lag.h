@@ -50,7 +50,8 @@ struct LagState {
 };
 
 template <int P>
-RPH_INLINE void lag_load(LagState<P>& st, const TrainDesc& d, const float* slot /* null: canonical */) {
+RPH_INLINE void lag_load(LagState<P>& st, const TrainDesc& d, const float* slot /* null: canonical */,
+                         const FitState* fit0 /* fit state to start from (canonical load only) */) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < LagState<P>::NPT; ++k) {
@@ -65,11 +66,11 @@ RPH_INLINE void lag_load(LagState<P>& st, const TrainDesc& d, const float* slot 
       st.m[k] = ok ? slot[PMAX + i] : 0.f;
       st.v[k] = ok ? slot[2 * PMAX + i] : 0.f;
     }
-    st.wb[k] = ok ? d.fit->w_best[i] : 0.f;
+    st.wb[k] = ok ? (slot == nullptr ? fit0 : d.fit)->w_best[i] : 0.f;
   }
   if (slot == nullptr) {
     const OptState* o = d.opt;
-    const FitState* f = d.fit;
+    const FitState* f = fit0;
     st.sc[LG_T] = o->t; st.sc[LG_LR] = o->lr; st.sc[LG_NAN] = o->nan_steps;
     st.sc[LG_BEST] = f->best_loss; st.sc[LG_WAIT] = f->wait; st.sc[LG_HASBEST] = f->has_best;
     st.sc[LG_LSUM] = f->loss_sum; st.sc[LG_ASUM] = f->abs_sum; st.sc[LG_PSUM] = f->ape_sum;
@@ -312,9 +313,12 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   RPH_DASSERT(d.batch > 0 && k >= 0 && epoch * d.steps_per_epoch <= k && d.lag != nullptr);
   // ---- prologue: every load independent, issued together -----------------------
   RPH_STAMP(0);
-  const float stopped0 = d.fit->stopped;
+  // kernel 0 starts from the fit-state template (and workgroup 0 publishes it
+  // as the canonical FitState below); later kernels see that copy
+  const FitState* fit0 = (k == 0 && d.fit_init != nullptr) ? d.fit_init : d.fit;
+  const float stopped0 = fit0->stopped;
   LagState<P> st;
-  lag_load<P>(st, d, k == 0 ? nullptr : d.lag + (size_t)(k & 1) * LAG_FLOATS);
+  lag_load<P>(st, d, k == 0 ? nullptr : d.lag + (size_t)(k & 1) * LAG_FLOATS, fit0);
   typename B::Pre pre;
   B::load(d, s, perm, B::first(wid), lane, pre);
   const bool dp = d.dp_world > 1;
@@ -342,6 +346,11 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   for (int j = 0; j < LagState<P>::NPT; ++j)
     if (tid + 256 * j < P) wl[tid + 256 * j] = st.w[j];
   if (w0) {
+    if (k == 0 && d.fit_init != nullptr) {  // canonical FitState := template (read by kernels >= 1)
+      const float* src = (const float*)d.fit_init;
+      float* dst = (float*)d.fit;
+      for (int i = tid; i < FIT_FLOATS; i += 256) dst[i] = src[i];
+    }
     // persist the updated state and re-arm the accumulator of step k+1 now, so
     // no optimizer state stays live (in registers) across the partial
     float* z = d.acc + (size_t)((k + 1) % 3) * ACC_REPLICAS * R;
@@ -372,16 +381,23 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
 template <int P, int R>
 __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, const int K) {
   __shared__ __attribute__((aligned(16))) float red[((R + 255) / 256) * 256 + 8];
-  if (d.fit->stopped != 0.f || K <= 0) return;
+  const bool run = d.fit->stopped == 0.f && K > 0;
   LagState<P> st;
-  lag_load<P>(st, d, d.lag + (size_t)(K & 1) * LAG_FLOATS);
-  const float* prev = d.acc + (size_t)((K - 1) % 3) * ACC_REPLICAS * R;
-  if (d.dp_world > 1) {
-    if (lag_dp_exchange<R>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)K, prev, red, true)) return;
-  } else {
-    lag_sums<R>(prev, red);
-    __syncthreads();
+  int bad = 0;
+  if (run) {
+    lag_load<P>(st, d, d.lag + (size_t)(K & 1) * LAG_FLOATS, d.fit);
+    const float* prev = d.acc + (size_t)((K - 1) % 3) * ACC_REPLICAS * R;
+    if (d.dp_world > 1) {
+      bad = lag_dp_exchange<R>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)K, prev, red, true);
+    } else {
+      lag_sums<R>(prev, red);
+    }
   }
+  // leave all three accumulators zeroed for the next fit (its kernel 0 adds
+  // into accumulator 0 without a memset); every lag kernel of this fit is done
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * ACC_REPLICAS * R; i += 256) st_agent(d.acc + i, 0.f);
+  if (!run || bad) return;
   const int S = d.steps_per_epoch;
   const int kp = K - 1, ep = kp / S;
   int ep_done = ep;

@@ -325,15 +325,16 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   constexpr int NHOLD = S::NHOLD;
   RPH_DASSERT(d.n_local > 0 && d.num_wgs == (int)gridDim.x && d.wa != nullptr && d.stats != nullptr);
   __shared__ double sst[4][EVAL_NSTAT];
-  __shared__ __attribute__((aligned(16))) float wl[2 * S::P + 8];
+  constexpr int WBOFF = (S::P + 3) / 4 * 4;  // net B's weights 16-byte aligned (ds_read_b128)
+  __shared__ __attribute__((aligned(16))) float wl[WBOFF + S::P + 4];
   const bool has_b = d.wb != nullptr;
   for (int i = threadIdx.x; i < S::P; i += 256) {
     wl[i] = d.wa->w[0][i];
-    if (has_b) wl[S::P + 4 + i] = d.wb->w[0][i];
+    if (has_b) wl[WBOFF + i] = d.wb->w[0][i];
   }
   __syncthreads();
   const float* __restrict__ WA = wl;
-  const float* __restrict__ WB = has_b ? wl + S::P + 4 : wl;
+  const float* __restrict__ WB = has_b ? wl + WBOFF : wl;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 
   // per-thread fp32 partials (a thread sees only a handful of paths), one
@@ -344,42 +345,73 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   for (int i = 0; i < NS; ++i) st[i] = 0.f;
   float rmin = INFINITY, rmax = -INFINITY;
 
-  for (int p0 = blockIdx.x * 256; p0 < d.n_local; p0 += gridDim.x * 256) {
-    const int p = p0 + threadIdx.x;
-    const bool valid = p < d.n_local;
-    const int pp = valid ? p : 0;
-    float x[NIN];
+  // Inputs of one path; a ring of EPF of them is kept in flight so every
+  // iteration's loads were issued EPF-1 iterations earlier (a thread walks
+  // n_local / (256 * num_wgs) paths, typically 16: one resident wave per SIMD
+  // would otherwise wait a full memory round trip per path).
+  struct In {
+    float x[NIN], pt[NHOLD], pt1[NHOLD], tgt, gb;
+    int p;
+    bool valid;
+  };
+  constexpr int EPF = 4;
+  const int stride = (int)gridDim.x * 256;
+  const bool has1 = d.price_t1[0] != nullptr;
+  auto load_in = [&](int p, In& in) {
+    in.p = p;
+    in.valid = p < d.n_local;
+    const int pp = in.valid ? p : 0;
 #pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = d.feat[f][pp];
+    for (int f = 0; f < NIN; ++f) in.x[f] = d.feat[f][pp];
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) {
+      in.pt[k] = d.price_t[k][pp];
+      in.pt1[k] = has1 ? d.price_t1[k][pp] : 0.f;
+    }
+    in.tgt = (has1 && d.target) ? d.target[pp] : 0.f;
+    in.gb = d.g_base ? d.g_base[pp] : 0.f;
+  };
+  In q[EPF];
+  const int p_first = blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < EPF; ++i) load_in(p_first + i * stride, q[i]);
+
+  for (int p0 = blockIdx.x * 256; p0 < d.n_local; p0 += stride) {
+    const In cur = q[0];
+#pragma unroll
+    for (int i = 0; i + 1 < EPF; ++i) q[i] = q[i + 1];
+    if (p0 + EPF * stride < d.n_local) load_in(cur.p + EPF * stride, q[EPF - 1]);
+    const int p = cur.p;
+    const bool valid = cur.valid;
+    // opaque zero offset: the weights stay in LDS and are read as broadcasts
+    // every iteration instead of being hoisted into (and spilling out of) VGPRs
+    uint32_t zo = 0;
+    asm volatile("" : "+v"(zo));
+    const float* __restrict__ WAi = (const float*)__builtin_assume_aligned(WA + (zo & ~3u), 16);
+    const float* __restrict__ WBi = (const float*)__builtin_assume_aligned(WB + (zo & ~3u), 16);
     float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], holdv[NHOLD];
-    net_forward<NIN, H, NO, HEAD>(WA, x, d.alpha, z1, a1, z2, a2, hold);
+    net_forward<NIN, H, NO, HEAD>(WAi, cur.x, d.alpha, z1, a1, z2, a2, hold);
 #pragma unroll
     for (int k = 0; k < NHOLD; ++k) holdv[k] = hold[k];
     if (has_b) {
       // V_t comes from net B (model2.predict, RP:218); reported holdings are
       // the blend hA + hold_c (hB - hA) (get_phi_psi_VaR, RP:114-115).
-      net_forward<NIN, H, NO, HEAD>(WB, x, d.alpha, z1, a1, z2, a2, holdv);
+      net_forward<NIN, H, NO, HEAD>(WBi, cur.x, d.alpha, z1, a1, z2, a2, holdv);
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) hold[k] = hold[k] + d.hold_c * (holdv[k] - hold[k]);
     }
     float V = 0.f;
 #pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) V = fmaf(holdv[k], d.price_t[k][pp], V);
+    for (int k = 0; k < NHOLD - 1; ++k) V = fmaf(holdv[k], cur.pt[k], V);
     V = fmaf(holdv[NHOLD - 1], d.bond_t, V);
-    if (d.g_base) {
-      const float gb = d.g_base[pp];
-      V = gb + d.blend_c * (V - gb);
-    }
-    float res = 0.f, pred1 = 0.f, tgt = 0.f;
-    const bool has1 = d.price_t1[0] != nullptr;
+    if (d.g_base) V = cur.gb + d.blend_c * (V - cur.gb);
+    float res = 0.f, pred1 = 0.f;
+    const float tgt = cur.tgt;
     if (has1) {
 #pragma unroll
-      for (int k = 0; k < NHOLD - 1; ++k) pred1 = fmaf(hold[k], d.price_t1[k][pp], pred1);
+      for (int k = 0; k < NHOLD - 1; ++k) pred1 = fmaf(hold[k], cur.pt1[k], pred1);
       pred1 = fmaf(hold[NHOLD - 1], d.bond_t1, pred1);
-      if (d.target) {
-        tgt = d.target[pp];
-        res = tgt - pred1;
-      }
+      if (d.target) res = tgt - pred1;
     }
     if (valid) {
       if (d.v_out) d.v_out[p] = V;

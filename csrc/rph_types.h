@@ -103,6 +103,8 @@ struct TrainDesc {
   int mfma_fp32;                 // 32-unit nets: exact fp32 MFMA (32x32x2) instead of bf16 (32x32x16)
   float* lag;                    // lagged-update state slots [2][LAG_FLOATS] (hedge_lag.h)
   int variant;                   // kernel variant (narrow: 1 = 2 waves/SIMD, weights re-read from LDS)
+  const FitState* fit_init;      // lagged schedule: fit-state template read by kernel 0, which also
+                                 // writes it to `fit` (no separate template copy per fit); may be null
 };
 
 constexpr int DP_SLOTS = 4;

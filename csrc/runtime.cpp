@@ -55,6 +55,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(TrainDesc, bond), OFF(TrainDesc, inv_batch), OFF(TrainDesc, loss), OFF(TrainDesc, seed),
       OFF(TrainDesc, num_wgs), OFF(TrainDesc, head), OFF(TrainDesc, acc), OFF(TrainDesc, deterministic), OFF(TrainDesc, stamps),
       OFF(TrainDesc, dp_world), OFF(TrainDesc, dp_mbox), OFF(TrainDesc, dp_flags), OFF(TrainDesc, dp_counter), OFF(TrainDesc, dp_error),
+      OFF(TrainDesc, fit_init),
       // EvalDesc
       (long long)sizeof(EvalDesc), OFF(EvalDesc, price_t), OFF(EvalDesc, price_t1), OFF(EvalDesc, target),
       OFF(EvalDesc, wa), OFF(EvalDesc, g_base), OFF(EvalDesc, v_out), OFF(EvalDesc, hold_out),

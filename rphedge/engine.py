@@ -18,6 +18,7 @@ Reference semantics: ``Replicating_Portfolio.py:128-221`` (C17-C24).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -210,8 +211,12 @@ class HipBackend:
         self.acc_fit = torch.zeros(3, 8, self.R, dtype=torch.float32, device=dev)
         self.fit_ctl = torch.zeros(4, dtype=torch.int32, device=dev)
         self.lag = torch.zeros(2, L.LAG_FLOATS, dtype=torch.float32, device=dev)
+        self._acc_clean = False  # acc_fit known zero (set by a lagged fit's finalize)
         self.stamps = None  # set to an int64 [num_wgs, 8] tensor for phase diagnostics
-        self.eval_wgs = int(max(1, min(1024, (self.n_local + 255) // 256)))
+        # eval epilogue (k_hedge_eval): weights read from LDS, 2-4 resident waves
+        # per SIMD, each thread walks its paths with a 4-deep load ring
+        ewg = int(os.environ.get("RPH_EVAL_WGS", "512"))
+        self.eval_wgs = int(max(1, min(ewg, (self.n_local + 255) // 256)))
         self._cache = _Cache()
 
     # -- state ---------------------------------------------------------------
@@ -282,11 +287,19 @@ class HipBackend:
         enqueueing; otherwise everything is asynchronous (graph-capturable) and
         surplus steps after an early stop are device-side no-ops."""
         assert len(data.feats) == self.spec.nin and len(data.prices_next) == self.spec.nhold - 1
-        fit.copy_(self._template(fcfg), non_blocking=True)
         lr_t = self._lr(fcfg)
         d = self._train_desc(wts, opt, fit, data, fcfg, seed, lr_t)
         n, S = self.native, self.steps_per_epoch
         mode = self.step_mode(poll_every)
+        if mode == "lag" and fcfg.epochs > 0:
+            # kernel 0 reads the fit-state template and publishes it as `fit`;
+            # the previous lag fit's finalize left the accumulators zeroed
+            d.fit_init = self._template(fcfg).data_ptr()
+            if not self._acc_clean:
+                n.memset_async(self.acc_fit, 0, self.stream)
+        else:
+            fit.copy_(self._template(fcfg), non_blocking=True)
+        self._acc_clean = False
         if mode == "persistent":
             n.memset_async(self.acc_fit, 0, self.stream)
             n.memset_async(self.fit_ctl, 0, self.stream)
@@ -294,7 +307,6 @@ class HipBackend:
             n.train_fit(d, fcfg.epochs, self.stream)
             return
         if mode == "lag":
-            n.memset_async(self.acc_fit, 0, self.stream)
             d.acc, d.lag = self.acc_fit.data_ptr(), self.lag.data_ptr()
             k = 0
             for e in range(fcfg.epochs):
@@ -305,6 +317,7 @@ class HipBackend:
                     if float(fit[L.F_STOPPED].item()) != 0.0:
                         break
             n.train_lag_finalize(d, k, self.stream)
+            self._acc_clean = True  # (finalize zeroes the three accumulators)
             return
         for e in range(fcfg.epochs):
             for s in range(S):

@@ -42,6 +42,7 @@ class TrainDesc(C.Structure):
         ("acc", VP), ("deterministic", C.c_int), ("stamps", VP),
         ("dp_world", C.c_int), ("dp_rank", C.c_int), ("dp_mbox", VP * 8), ("dp_flags", VP * 8),
         ("dp_counter", VP), ("dp_error", VP), ("mfma_fp32", C.c_int), ("lag", VP), ("variant", C.c_int),
+        ("fit_init", VP),
     ]
 
 
@@ -84,6 +85,7 @@ def _expected_layout() -> list[int]:
         T.counter.offset, T.grad_out.offset, T.bond.offset, T.inv_batch.offset, T.loss.offset, T.seed.offset,
         T.num_wgs.offset, T.head.offset, T.acc.offset, T.deterministic.offset, T.stamps.offset,
         T.dp_world.offset, T.dp_mbox.offset, T.dp_flags.offset, T.dp_counter.offset, T.dp_error.offset,
+        T.fit_init.offset,
         C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
         E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
         E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset,

@@ -264,6 +264,41 @@ def test_graph_replay_equals_eager(dev):
     assert r_graph.terminal_pnl["std"] == pytest.approx(r_eager.terminal_pnl["std"], rel=1e-6)
 
 
+@pytest.mark.parametrize("family", ["heston", "basket", "pension"])
+def test_graph_resimulation_all_models(dev, family):
+    """The captured graph re-simulates every path family into the SAME buffers:
+    bitwise-identical paths/terminal values and the same run as eager."""
+    from rphedge.config import ParityFlags, RunConfig, TrainingParams
+    from rphedge.api import HedgeRun
+
+    tr = TrainingParams(batch_size=4096, epochs_first=3, epochs_rest=2, early_stopping=False,
+                        q99=family == "pension", lr_schedule_first=False, chunk_log2=6, deterministic=False)
+    kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.05, r=0.05, sigma=0.2, rebalancing=0.25, dt=0.05, n_paths=13,
+              N=1, P=1.0, keep_paths=False, verbose=False, train=tr, parity=ParityFlags())
+    if family == "heston":
+        kw.update(payoff="call", option_type="CALL", model="heston", mortality=False)
+    elif family == "basket":
+        kw.update(payoff="basket_call", model="basket", n_assets=5, mortality=False)
+    else:
+        kw.update(Y=1.0, K=1.0, T=2.0, payoff="guarantee", model="gbm", mortality=True, N=10000, P=100.0)
+    run = HedgeRun(RunConfig(**kw))
+    run.build()
+    r_eager = run.run()
+    s0 = run.paths.S.clone()
+    v0 = run.v_terminal.clone()
+    nf0 = run.paths.nfrac.clone() if run.paths.nfrac is not None else None
+    run.paths.S.zero_()
+    run.v_terminal.zero_()
+    run.capture(include_simulation=True)
+    run.replay()
+    r_graph = run.collect()
+    assert torch.equal(run.paths.S, s0)
+    assert torch.equal(run.v_terminal, v0)
+    if nf0 is not None:
+        assert torch.equal(run.paths.nfrac, nf0)
+    assert r_graph.v0 == pytest.approx(r_eager.v0, rel=2e-3)
+
+
 def test_european_converges_to_black_scholes(dev):
     """Integration: corrected replication at 2^18 paths lands near BS 10.3896."""
     from rphedge.config import ParityFlags, RunConfig, TrainingParams
