@@ -541,6 +541,8 @@ extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* st
   return launch_wide_lag_step(d, k, epoch, perm, s);
 }
 
+extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream);
+
 extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
   if (int rc = validate_train(d, 1, "rph_train_lag_finalize")) return rc;
   hipStream_t s = (hipStream_t)stream;
@@ -555,6 +557,29 @@ extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
 #undef X
   return -1;
 }
+
+// Whole fit on the host side of the native runtime: the epochs x steps launch
+// loop (lagged schedule, or ticketed steps with fused update) runs in C++ so an
+// eager (non-graph) fit pays one hipLaunchKernel per step instead of a Python
+// + ctypes round trip per step.  Graph capture records the same launches.
+extern "C" int rph_train_lag_fit(const TrainDesc* d, int epochs, void* stream) {
+  if (int rc = validate_train(d, 1, "rph_train_lag_fit")) return rc;
+  int k = 0;
+  for (int e = 0; e < epochs; ++e)
+    for (int s = 0; s < d->steps_per_epoch; ++s, ++k)
+      if (int rc = rph_train_lag_step(d, k, e, stream)) return rc;
+  return rph_train_lag_finalize(d, k, stream);
+}
+
+extern "C" int rph_train_ticket_fit(const TrainDesc* d, int epochs, void* stream) {
+  if (int rc = validate_train(d, 0, "rph_train_ticket_fit")) return rc;
+  if (!d->fused_update) return rph_report("rph_train_ticket_fit", "needs the fused (in-kernel) update");
+  for (int e = 0; e < epochs; ++e)
+    for (int s = 0; s < d->steps_per_epoch; ++s)
+      if (int rc = rph_train_step(d, s, e, stream)) return rc;
+  return 0;
+}
+
 
 extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* stream) {
   if (!d->grad_out || !d->wts || !d->opt || !d->fit) return rph_report("rph_train_update", "null pointer");

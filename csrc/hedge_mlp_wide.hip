@@ -466,15 +466,25 @@ int launch_wide_step(const TrainDesc* d, int step, int epoch, const Perm& perm, 
   return -1;
 }
 
+// Persistent per-fit kernel for the wide nets.  The 5-32-6 basket net is not
+// offered: its optimizer state (6 parameters per thread x w/m/v/best) on top of
+// the MFMA tile state spills ~1.4 KB/lane and the spilled variant gave wrong
+// results on gfx950 — that shape runs the lagged/ticketed step kernels.
+#define RPH_WIDE_FIT_SHAPES(X)   \
+  X(1, 32, 1, HEAD_COMPLEMENT)   \
+  X(1, 32, 2, HEAD_FREE)         \
+  X(2, 32, 2, HEAD_FREE)         \
+  X(3, 32, 2, HEAD_FREE)
+
 int launch_wide_fit(const TrainDesc* d, int epochs, hipStream_t s) {
 #define X(A, B, C, E)                                                          \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                 \
     if (d->mfma_fp32) return launch_fit<WideBody<A, C, E, true>>(d, epochs, s); \
     return launch_fit<WideBody<A, C, E, false>>(d, epochs, s);                 \
   }
-  RPH_WIDE_SHAPES(X)
+  RPH_WIDE_FIT_SHAPES(X)
 #undef X
-  return -1;
+  return rph_report("rph_train_fit", "no persistent fit kernel for this network shape (use lag/ticket)");
 }
 
 int launch_wide_lag_step(const TrainDesc* d, int k, int epoch, const Perm& perm, hipStream_t s) {

@@ -83,7 +83,8 @@ class TrainConfig:
     #   "ticket"     one kernel per step, last-arriving workgroup reduces + updates
     #                (deterministic slab / split update / fused xGMI DP)
     #   "persistent" one resident kernel per fit with an in-kernel grid barrier
-    #   "auto"       lag where valid (1 rank, float-atomic reduction), else ticket
+    #   "auto"       1 rank: persistent up to PERSISTENT_MAX_WGS workgroups, lag above;
+    #                data parallel: lag (fused xGMI) where valid, else ticket
     step_mode: str = "auto"
     # narrow lag kernel: bit 0 = 2 waves/SIMD with LDS weight re-reads,
     # bit 1 = path-data prefetch 2 iterations deeper (3 loads in flight)
@@ -183,6 +184,9 @@ def _steps(n_local: int, tcfg: TrainConfig, world: int) -> tuple[int, int]:
 # ---------------------------------------------------------------------------
 # HIP backend
 # ---------------------------------------------------------------------------
+PERSISTENT_MAX_WGS = 64  # "auto" picks the persistent per-fit kernel up to this grid (1 rank)
+
+
 class HipBackend:
     name = "hip"
 
@@ -308,6 +312,10 @@ class HipBackend:
             return
         if mode == "lag":
             d.acc, d.lag = self.acc_fit.data_ptr(), self.lag.data_ptr()
+            if not poll_every:  # whole fit launched from the native runtime
+                n.train_lag_fit(d, fcfg.epochs, self.stream)
+                self._acc_clean = fcfg.epochs > 0
+                return
             k = 0
             for e in range(fcfg.epochs):
                 for s in range(S):
@@ -318,6 +326,10 @@ class HipBackend:
                         break
             n.train_lag_finalize(d, k, self.stream)
             self._acc_clean = True  # (finalize zeroes the three accumulators)
+            return
+        per_step_host = (self.world > 1 and d.fused_update == 0) or self.tcfg.split_update
+        if not poll_every and not per_step_host:
+            n.train_ticket_fit(d, fcfg.epochs, self.stream)
             return
         for e in range(fcfg.epochs):
             for s in range(S):
@@ -335,15 +347,30 @@ class HipBackend:
         t = self.tcfg
         atomic = not t.deterministic and not t.split_update
         dp_fused = self.mailbox is not None and self.comm is None
-        if t.step_mode == "persistent" and atomic and not poll_every and (self.world == 1 or dp_fused):
+        if (t.step_mode == "persistent" and atomic and not poll_every and (self.world == 1 or dp_fused)
+                and self.persistent_supported()):
             # (explicit only: needs every workgroup of every rank co-resident)
             return "persistent"
         shared = dp_fused and getattr(self.mailbox, "shared_device", False)
         if t.step_mode == "lag" and atomic and (self.world == 1 or dp_fused):
             return "lag"
+        # small grids (the reference's batch 512 = 2 workgroups): the persistent
+        # kernel's in-kernel barrier is cheaper than a kernel boundary below ~96
+        # workgroups (profiles/crossover_r1g.jsonl) and one launch per fit
+        # removes the per-step host launch from eager runs
+        if (t.step_mode == "auto" and atomic and self.world == 1 and not poll_every
+                and self.spec.hidden == 8 and self.num_wgs <= PERSISTENT_MAX_WGS):
+            return "persistent"
+        if t.step_mode == "persistent" and atomic and (self.world == 1 or dp_fused):
+            return "lag"  # shape without a persistent kernel (or host polling): lagged steps
         if t.step_mode == "auto" and atomic and (self.world == 1 or (dp_fused and not shared)):
             return "lag"
         return "ticket"
+
+    def persistent_supported(self) -> bool:
+        """Shapes with a persistent per-fit kernel (csrc/hedge_fit.h): every
+        8-unit net; the 32-unit nets up to 3 inputs (RPH_WIDE_FIT_SHAPES)."""
+        return self.spec.hidden == 8 or self.spec.nin <= 3
 
     def check(self):
         """Raise if a persistent fit timed out waiting for co-resident workgroups."""

@@ -119,6 +119,8 @@ def _bind(lib):
         "rph_train_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_train_lag_step": (C.c_int, [C.POINTER(TrainDesc), C.c_int, C.c_int, VP]),
         "rph_train_lag_finalize": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
+        "rph_train_lag_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
+        "rph_train_ticket_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
@@ -233,6 +235,18 @@ def train_fit(desc: TrainDesc, epochs: int, stream=None):
 def train_lag_step(desc: TrainDesc, k: int, epoch: int, stream=None):
     """Lagged-update step kernel k of a fit (csrc/hedge_lag.h)."""
     _check(_lib.rph_train_lag_step(C.byref(desc), int(k), int(epoch), stream_handle(stream)), "rph_train_lag_step")
+
+
+def train_lag_fit(desc: TrainDesc, epochs: int, stream=None):
+    """All steps + finalize of a lagged-schedule fit, launched from C++."""
+    load(required=True)
+    _check(_lib.rph_train_lag_fit(C.byref(desc), int(epochs), stream_handle(stream)), "rph_train_lag_fit")
+
+
+def train_ticket_fit(desc: TrainDesc, epochs: int, stream=None):
+    """All steps of a ticketed fit (fused update), launched from C++."""
+    load(required=True)
+    _check(_lib.rph_train_ticket_fit(C.byref(desc), int(epochs), stream_handle(stream)), "rph_train_ticket_fit")
 
 
 def train_lag_finalize(desc: TrainDesc, K: int, stream=None):

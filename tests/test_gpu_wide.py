@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 WIDE = [(1, 32, 2, 0), (3, 32, 2, 0), (1, 32, 1, 1), (2, 32, 2, 0), (5, 32, 6, 0)]
 
 
-@pytest.mark.parametrize("mode", ["lag", "ticket"])
+@pytest.mark.parametrize("mode", ["lag", "ticket", "persistent"])
 @pytest.mark.parametrize("shape", WIDE)
 def test_wide_fp32_mfma_matches_torch(dev, shape, mode):  # noqa: F811
     from rphedge.models.hedge_mlp import NetSpec
@@ -34,14 +34,16 @@ def test_wide_fp32_mfma_matches_torch(dev, shape, mode):  # noqa: F811
     np.testing.assert_allclose(vg, vc, rtol=2e-3, atol=2e-4)
 
 
+@pytest.mark.parametrize("mode", ["auto", "persistent"])
 @pytest.mark.parametrize("shape", WIDE)
-def test_wide_bf16_mfma_matches_torch(dev, shape):  # noqa: F811
+def test_wide_bf16_mfma_matches_torch(dev, shape, mode):  # noqa: F811
     from rphedge.models.hedge_mlp import NetSpec
     from rphedge.ops import layout as L
 
     nin, h, nout, head = shape
     spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
-    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE,
+                                                                   step_mode=mode)
     assert og[L.O_T] == oc[L.O_T] == 16
     np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=3e-2)
     # fitted values: bf16 operand rounding only
