@@ -31,9 +31,13 @@ namespace rph {
 // (the reference's 8-unit nets).  Used by the per-step kernel below and by the
 // persistent per-fit kernel (hedge_fit.h).
 // ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD, int WPE = 1, int PFD = 1>
+template <int NIN, int H, int NO, int HEAD, int WPE = 1, int PFD = 1, bool LDSW = (WPE > 1)>
 struct NarrowBody {
   static constexpr int WAVES_PER_SIMD = WPE;
+  // LDSW: weights are re-read from LDS every path iteration instead of being
+  // hoisted into registers (needed at 2 waves/SIMD; at 1 wave/SIMD it keeps
+  // the wide-packet nets - basket 5-8-6, R = 256 - out of scratch spills)
+  static constexpr bool LDS_WEIGHTS = LDSW;
   // path-data prefetch distance in loop iterations (1: the next path is loaded
   // while the current one computes; >1 keeps PFD loads in flight, so a thread's
   // later paths never wait on a fresh L2/MALL round trip)
@@ -91,7 +95,7 @@ struct NarrowBody {
       // overflow); WPE 2: an opaque zero offset makes every iteration re-read
       // them as LDS broadcasts, so the kernel fits 256 registers = 2 waves/SIMD
       const float* __restrict__ Wi = W;
-      if constexpr (WPE > 1) {
+      if constexpr (LDSW) {
         // opaque 16-byte-aligned base: every use is a ds_read_b128 broadcast
         // off ONE address register with an immediate offset
         uint32_t z = 0;
@@ -531,6 +535,8 @@ extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* st
                                  s, *d, k, epoch, perm); break;                                        \
       case 3: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 2, 3>>), dim3(d->num_wgs), dim3(256), 0, \
                                  s, *d, k, epoch, perm); break;                                        \
+      case 4: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 1, 1, true>>), dim3(d->num_wgs), dim3(256), \
+                                 0, s, *d, k, epoch, perm); break;                                     \
       default: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, \
                                   *d, k, epoch, perm);                                                 \
     }                                                                                                 \

@@ -86,9 +86,12 @@ class TrainConfig:
     #   "auto"       1 rank: persistent up to PERSISTENT_MAX_WGS workgroups, lag above;
     #                data parallel: lag (fused xGMI) where valid, else ticket
     step_mode: str = "auto"
-    # narrow lag kernel: bit 0 = 2 waves/SIMD with LDS weight re-reads,
-    # bit 1 = path-data prefetch 2 iterations deeper (3 loads in flight)
-    variant: int = 0
+    # narrow lag kernel: 0 = weights hoisted into registers (1 wave/SIMD);
+    # 1 = 2 waves/SIMD with LDS weight re-reads; 2/3 = 0/1 with the path-data
+    # prefetch 2 iterations deeper; 4 = LDS weight re-reads at 1 wave/SIMD;
+    # -1 = auto (4 for nets whose gradient packet is 256 wide - no scratch
+    # spills - else 0)
+    variant: int = -1
 
 
 @dataclass
@@ -204,6 +207,7 @@ class HipBackend:
         self.P, self.R = native.net_nparams(spec.nin, spec.hidden, spec.nout, spec.head)
         assert self.P == spec.nparams
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
+        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (4 if self.R > 128 else 0)
         work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
         self.num_wgs = int(max(1, min(tcfg.max_wgs, work)))
         dev = self.device
@@ -279,7 +283,7 @@ class HipBackend:
         d.acc = self.acc.data_ptr()
         d.deterministic = 1 if self.tcfg.deterministic else 0
         d.mfma_fp32 = 1 if self.tcfg.mfma_fp32 else 0
-        d.variant = int(self.tcfg.variant)
+        d.variant = self.variant
         d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
         d.num_wgs = self.num_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
@@ -421,6 +425,7 @@ class TorchBackend:
         self.world, self.rank = world, rank
         self.dtype = dtype
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
+        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (4 if self.R > 128 else 0)
         self.eval_wgs = 1
         self._order_cache = {}
 
