@@ -425,7 +425,6 @@ class TorchBackend:
         self.world, self.rank = world, rank
         self.dtype = dtype
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
-        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (4 if self.R > 128 else 0)
         self.eval_wgs = 1
         self._order_cache = {}
 
