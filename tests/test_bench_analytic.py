@@ -1,0 +1,68 @@
+"""bench.py driver contract (CPU plumbing preset, 1 and 4 gloo ranks) and the
+closed-form quality anchors (rphedge.analytic)."""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def test_heston_reduces_to_black_scholes():
+    from rphedge.analytic import black_scholes, heston_call
+
+    p, d = heston_call(100.0, 100.0, 0.08, 1.0, 2.0, 0.0225, 1e-4, -0.7, 0.0225)
+    bs, bd = black_scholes(100.0, 100.0, 0.08, 0.15, 1.0)
+    assert p == pytest.approx(bs, abs=2e-3)
+    assert d == pytest.approx(bd, abs=1e-3)
+
+
+def test_heston_literature_value():
+    """Albrecher et al. benchmark: S0=K=100, T=1, r=0, kappa=1.5768, theta=0.0398,
+    xi=0.5751, rho=-0.5711, v0=0.0175 -> 5.785155."""
+    from rphedge.analytic import heston_call, heston_price
+
+    p, _ = heston_call(100.0, 100.0, 0.0, 1.0, 1.5768, 0.0398, 0.5751, -0.5711, 0.0175)
+    assert p == pytest.approx(5.785155, abs=1e-4)
+    put, _ = heston_price(100.0, 110.0, 0.05, 1.0, 2.0, 0.04, 0.5, -0.7, 0.04, "PUT")
+    call, _ = heston_call(100.0, 110.0, 0.05, 1.0, 2.0, 0.04, 0.5, -0.7, 0.04)
+    assert put == pytest.approx(call - 100.0 + 110.0 * math.exp(-0.05), abs=1e-9)  # put-call parity
+
+
+def _bench(args, env=None, nproc=1):
+    e = dict(os.environ, **(env or {}))
+    e.setdefault("OMP_NUM_THREADS", "1")
+    if nproc == 1:
+        cmd = [sys.executable, "bench.py"] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", str(nproc)] + args
+    out = subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_cpu_preset_contract():
+    r = _bench(["--preset", "euro1_cpu", "--steps", "1", "--warmup", "0", "--epochs-first", "20"])
+    assert KEYS <= set(r)
+    assert r["n_gpus"] == 1 and r["steps"] == 1 and r["higher_is_better"] is True and r["scaling"] == "weak"
+    assert r["config"]["preset"] == "euro1_cpu" and r["config"]["parallelism"] == "dp1"
+    assert r["value"] > 0 and r["vs_baseline"] == pytest.approx(r["value"] / (512 / 0.006))
+    assert r["quality"]["anchor"]["analytic"] == "black_scholes"
+
+
+def test_bench_cpu_four_ranks():
+    """--gpus 4 under torch.distributed.run (gloo on CPU): weak scaling, the
+    global batch and path count grow with the world size; rank 0 prints once."""
+    r = _bench(["--preset", "euro1_cpu", "--steps", "1", "--warmup", "0", "--epochs-first", "10",
+                "--paths-log2", "12", "--batch-log2", "10", "--cpu"], nproc=4)
+    assert r["n_gpus"] == 4 and r["config"]["parallelism"] == "dp4"
+    assert r["config"]["paths_global"] == 4 * (1 << 12) and r["config"]["global_batch"] == 4 * (1 << 10)
+    assert math.isfinite(r["quality"]["V0"]) and abs(r["quality"]["V0"] - 10.39) < 1.5
