@@ -3,14 +3,19 @@
 One process per GPU.  The global path set ``[0, 2^m)`` is split into
 contiguous shards ``[r*n/W, (r+1)*n/W)``; Sobol points are index-addressable so
 every rank generates its own shard with no communication.  Per optimizer step
-the 512-byte gradient packet (grads + loss/metric partials) is summed with ONE
-RCCL all-reduce issued by the native runtime on the compute stream (captured
-into the same hipGraph as the step kernels); statistics and histograms use
-``torch.distributed`` collectives (nccl = RCCL on ROCm, gloo on CPU).
+the 512-byte gradient packet (grads + loss/metric partials) is summed over
+ranks INSIDE the step kernel (default ``RPH_DP=xgmi``): IPC-mapped peer
+mailboxes, system-scope stores over xGMI, bounded in-kernel polls, identical
+fixed-order sums on every rank (csrc/hedge_lag.h, csrc/hedge_core.h).
+:func:`select_transport` probes that path once and falls back to ONE RCCL
+all-reduce of the packet per step on the compute stream (graph-captured with
+the step kernels, ``RPH_DP=rccl``).  Statistics, quantile histograms and the
+bias-init P(OTM) use ``torch.distributed`` collectives (nccl = RCCL on ROCm;
+gloo on CPU and for ranks sharing one GPU).
 
-Sizing for xGMI: the per-step packet is latency-bound (one-shot/LL protocol),
-so the design lever is FEWER steps (large per-rank batches) rather than
-bandwidth; bucketing is moot at 512 B.
+Sizing for xGMI: the per-step packet is latency-bound (one-shot), so the design
+levers are one exchange per step with no extra launch, and large per-rank
+batches (fewer steps); bucketing is moot at 512 B.
 """
 from __future__ import annotations
 
@@ -70,7 +75,11 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
     if use_gpu:
         info.shared_device = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) > torch.cuda.device_count()
     if world > 1:
-        be = backend or os.environ.get("RPH_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        # RCCL refuses two ranks on one GPU ("duplicate GPU"): ranks sharing a
+        # card (single-GPU rehearsal of the DP path) bootstrap over gloo; the
+        # gradient exchange itself still runs in-kernel through IPC mailboxes
+        be = backend or os.environ.get("RPH_DIST_BACKEND") or (
+            "nccl" if use_gpu and not info.shared_device else "gloo")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {}
