@@ -174,8 +174,12 @@ __global__ __launch_bounds__(256) void k_sim_basket(const SimDesc d) {
   if (!ALIGNED && p >= d.n_local) return;
   const uint32_t g = gray_code((uint64_t)(d.path_offset + p));
   const float dt = (float)d.dt, sdt = sqrtf(dt);
-  float ly[NA], drift[NA], vol[NA], inv[NA];
+  float ly[NA], drift[NA], vol[NA], inv[NA], ch[NA * (NA + 1) / 2];
   const size_t n = (size_t)d.n_local;
+#pragma unroll
+  for (int a = 0, i = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b <= a; ++b, ++i) ch[i] = (float)d.chol[a * MAXIN + b];  // hoisted fp64 -> fp32
 #pragma unroll
   for (int a = 0; a < NA; ++a) {
     ly[a] = logf((float)d.s0[a]);
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(256) void k_sim_basket(const SimDesc d) {
     for (int a = 0; a < NA; ++a) {
       float z = 0.f;
 #pragma unroll
-      for (int b = 0; b <= a; ++b) z = fmaf((float)d.chol[a * MAXIN + b], w[b], z);
+      for (int b = 0; b <= a; ++b) z = fmaf(ch[a * (a + 1) / 2 + b], w[b], z);
       ly[a] += drift[a] + vol[a] * z;
     }
     if (t % d.reduction == 0) {
