@@ -237,8 +237,17 @@ class HedgeRun:
                                holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start,
                                restore_best_at_end=pf.restore_best_at_end, keep_paths=c.keep_paths,
                                poll_every=tr.poll_every, seed=tr.seed)
+        backend_q = None
+        if (self.backend_kind == "hip" and self.di.world == 1 and icfg.q99 and not icfg.shared_q99_model
+                and not icfg.poll_every and tr.concurrent_q99):
+            # second backend (own accumulators / state slots) for the pinball
+            # fit, run concurrently on a side stream (driver.BackwardInduction)
+            backend_q = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
+                                     world=1, rank=0, stream=None)
+            if not backend_q.concurrent_with(self.backend):
+                backend_q = None
         self.induction = BackwardInduction(self.paths, self.v_terminal, self.spec, self.w0, self.backend, icfg,
-                                           world=self.di.world, rank=self.di.rank)
+                                           world=self.di.world, rank=self.di.rank, backend_q=backend_q)
         return self
 
     # ------------------------------------------------------------------ run

@@ -71,6 +71,7 @@ class TrainingParams:
     mfma_precision: str = "bf16"     # 32-unit nets: "bf16" (32x32x16 MFMA) or "fp32" (exact 32x32x2 MFMA)
     step_mode: str = "auto"          # GPU step schedule: auto | lag | ticket | persistent (engine.TrainConfig)
     variant: int = -1                # narrow lag-kernel variant (-1: engine default; see engine.TrainConfig)
+    concurrent_q99: bool = True      # two networks: run the pinball fit concurrently with the MSE fit (GPU)
 
 
 @dataclass

@@ -104,8 +104,14 @@ class BackwardInduction:
     """Owns device buffers for one run; ``enqueue()`` is graph-capturable."""
 
     def __init__(self, paths: Paths, v_terminal: torch.Tensor, spec: NetSpec, w0: np.ndarray, backend,
-                 icfg: InductionConfig, world: int = 1, rank: int = 0):
+                 icfg: InductionConfig, world: int = 1, rank: int = 0, backend_q=None):
         self.paths, self.spec, self.backend, self.cfg = paths, spec, backend, icfg
+        # independent-network model parallelism: with two networks (corrected
+        # Q1 semantics) the pinball fit of a date does not depend on that date's
+        # MSE fit, so it runs on its own backend (own buffers) on a side stream,
+        # concurrently with the MSE fit + its eval; the blend joins them
+        self.backend_q = backend_q if (backend_q is not None and icfg.q99 and not icfg.shared_q99_model) else None
+        self._side = None
         self.world, self.rank = world, rank
         n, nc = paths.n_local, paths.n_coarse
         dev = paths.S.device
@@ -162,14 +168,30 @@ class BackwardInduction:
                     self.opt_q.copy_(self.opt_init)
             f_m, f_q = self.fits[t]
             s_m, s_q = self.stats[t]
+            join = None
+            if self.backend_q is not None:  # fork: Q99 fit on the side stream
+                main = torch.cuda.current_stream(self.values.device)
+                if self._side is None:
+                    self._side = torch.cuda.Stream(self.values.device)
+                fork = torch.cuda.Event()
+                fork.record(main)
+                self._side.wait_event(fork)
+                with torch.cuda.stream(self._side):
+                    self.backend_q.fit(self.w_q, self.opt_q, f_q, data, self._fcfg(first, L.LOSS_PINBALL),
+                                       seed=fit_seed(c.seed, t, 1), poll_every=0)
+                    join = torch.cuda.Event()
+                    join.record(self._side)
             be.fit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE),
                    seed=fit_seed(c.seed, t, 0), poll_every=c.poll_every)
             hold_out = [self.holdings[t, k] for k in range(self.spec.nhold)] if self.holdings is not None else None
             resid_out = self.residuals[t] if self.residuals is not None else None
             if c.q99:
                 be.eval(self.w_mse, data, s_m, v_out=self.gbuf)
-                be.fit(self.w_q, self.opt_q, f_q, data, self._fcfg(first, L.LOSS_PINBALL),
-                       seed=fit_seed(c.seed, t, 1), poll_every=c.poll_every)
+                if join is not None:
+                    torch.cuda.current_stream(self.values.device).wait_event(join)
+                else:
+                    be.fit(self.w_q, self.opt_q, f_q, data, self._fcfg(first, L.LOSS_PINBALL),
+                           seed=fit_seed(c.seed, t, 1), poll_every=c.poll_every)
                 hc = -c.cost_of_capital if c.holdings_blend_sign_rp else c.cost_of_capital
                 be.eval(self.w_mse, data, s_q, wts_b=self.w_q, g_base=self.gbuf, blend_c=c.cost_of_capital,
                         hold_c=hc, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out)

@@ -371,6 +371,22 @@ class HipBackend:
             return "lag"
         return "ticket"
 
+    def concurrent_with(self, other: "HipBackend") -> bool:
+        """Whether a fit of this backend may run concurrently (another stream)
+        with a fit of ``other`` without a co-residency deadlock: persistent
+        kernels need every workgroup resident, so two of them must fit the
+        device together (one workgroup per CU at one wave per SIMD)."""
+        a, b = self.step_mode(), other.step_mode()
+        cus = 256
+        try:
+            cus = int(torch.cuda.get_device_properties(self.device).multi_processor_count)
+        except Exception:
+            pass
+        need = (self.num_wgs if a == "persistent" else 0) + (other.num_wgs if b == "persistent" else 0)
+        if ("persistent" in (a, b)) and need > cus:
+            return False
+        return self.world == 1 and other.world == 1
+
     def persistent_supported(self) -> bool:
         """Shapes with a persistent per-fit kernel (csrc/hedge_fit.h): every
         8-unit net; the 32-unit nets up to 3 inputs (RPH_WIDE_FIT_SHAPES)."""

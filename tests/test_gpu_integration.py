@@ -94,3 +94,36 @@ def test_async_and_polled_early_stopping_agree():
     b = run_params(dict(p, poll_every=4))
     assert a.summary["epochs_mse"] == b.summary["epochs_mse"]
     assert a.phi == pytest.approx(b.phi, rel=1e-3)
+
+
+def test_concurrent_q99_fit_matches_sequential():
+    """Corrected semantics (two networks): the pinball fit runs on a side
+    stream concurrently with the MSE fit; the result equals the sequential
+    schedule (the fits are independent), in eager mode and replayed from a graph."""
+    import time
+
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.experiments import mts_parameters
+
+    out = {}
+    for conc in (False, True):
+        p = mts_parameters(verbose=False, concurrent_q99=conc, keep_paths=False)
+        run = HedgeRun(parse_params(p))
+        run.build()
+        assert (run.induction.backend_q is not None) == conc
+        run.run()  # warm (tables, templates)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = run.run()
+        out[conc] = (res, time.perf_counter() - t0)
+        if conc:
+            run.capture(include_simulation=False)
+            run.replay()
+            rg = run.collect()
+            assert rg.phi == pytest.approx(res.phi, rel=1e-5)
+    (rs, ts), (rc, tc) = out[False], out[True]
+    _record("concurrent_q99", {"seq_s": ts, "conc_s": tc, "phi_seq": rs.phi, "phi_conc": rc.phi})
+    assert rc.phi == pytest.approx(rs.phi, rel=1e-5)
+    assert rc.psi == pytest.approx(rs.psi, rel=1e-5)
+    assert rc.v0 == pytest.approx(rs.v0, rel=1e-5)
