@@ -1,25 +1,28 @@
-// rphedge — fused hedge-MLP training step (K9), Adam/early-stop update (K10),
-// minibatch chunk permutation (K11) and the value/holdings/residual epilogue
-// (K12) for gfx950.
+// rphedge — thread-per-path hedge-MLP training body for the reference's 8-unit
+// nets (K8/K9), the ticketed step kernel with the fused Adam/early-stop update
+// (K10), the minibatch chunk permutation (K11), the value/holdings/residual
+// epilogue (K12) and the C ABI launchers of every training schedule, for gfx950.
 //
 // Reference semantics (one backward-induction date):
 //   model(X1=[state_t, prices_{t+1}]) -> V = holdings(state_t) . prices_{t+1}
 //   fit MSE / 99% pinball, Adam(1e-3), batch 512, EarlyStopping(loss)
 //   (/root/reference/Replicating_Portfolio.py:149-221).
 //
-// Design (MI355X-first, see DESIGN.md §Training step):
-//   * thread-per-path fp32 forward+backward; weights are wave-uniform and are
-//     read through the scalar unit (s_load -> SGPR operands of v_fma);
-//   * per-thread register accumulation of the full gradient (R = next pow2 of
-//     P+4 floats), one in-wave recursive-halving reduce-scatter (DPP/swizzle,
-//     ~4R VALU), one LDS cross-wave sum, one deterministic [num_wgs][R] slab;
-//   * the last-arriving workgroup (agent-scope release/acquire ticket) sums
-//     the slab and — for world_size == 1 — applies Keras-Adam, the epoch-end
-//     EarlyStopping/LR-schedule bookkeeping and the weight ping-pong in the
-//     same launch: ONE kernel per optimizer step, graph-capturable.
-//   * world_size > 1: the slab sum goes to grad_out, RCCL all-reduces it on
-//     the same stream and k_hedge_update applies the identical update on every
-//     rank (bitwise-identical decisions => identical early stopping).
+// Design (MI355X-first, DESIGN.md §2, §4):
+//   * NarrowBody: thread-per-path fp32 forward+backward (the compiler packs the
+//     FMAs into v_pk_fma_f32); weights are wave-uniform, staged once in LDS and
+//     either hoisted into registers or re-read as ds_read_b128 broadcasts
+//     (variants); per-thread register accumulation of the full gradient
+//     (R = next pow2 of P+4 floats), one in-wave recursive-halving
+//     reduce-scatter (permlane32_swap / ds_swizzle / DPP), one LDS cross-wave sum;
+//   * the same body runs under three schedules: k_hedge_step_lag (hedge_lag.h,
+//     default above 64 workgroups: the update of step k-1 applied redundantly in
+//     every workgroup's prologue, no in-kernel sync), k_hedge_fit (hedge_fit.h,
+//     persistent per fit, default for small grids) and k_hedge_train_step below
+//     (ticketed: the last-arriving workgroup sums the float-atomic replicas or
+//     the deterministic slab, optionally exchanges the packet with the other
+//     ranks over xGMI, and applies Keras-Adam + EarlyStopping in the same
+//     launch; with an RCCL all-reduce instead, k_hedge_update applies it).
 #include "hedge_core.h"
 #include "hedge_fit.h"
 #include "hedge_lag.h"
