@@ -403,6 +403,7 @@ inline int validate_train(const TrainDesc* d, int mode, const char* who) {
   const int nhold = d->head == HEAD_COMPLEMENT ? 2 : d->nout;
   if (d->nin < 1 || d->nin > MAXIN || nhold < 1 || nhold > MAXHOLD) return rph_report(who, "network shape out of range");
   if (d->num_wgs < 1 || d->num_wgs > 65535) return rph_report(who, "num_wgs out of range");
+  if (!(d->alpha >= 0.f && d->alpha <= 1.f)) return rph_report(who, "LeakyReLU slope must be in [0, 1]");
   if (d->batch < 1 || d->n_local < d->batch || d->steps_per_epoch < 1 ||
       (long long)d->batch * d->steps_per_epoch < d->n_local)
     return rph_report(who, "batch / steps_per_epoch do not cover n_local");

@@ -608,6 +608,7 @@ extern "C" int rph_train_update(const TrainDesc* d, int step, int epoch, void* s
 extern "C" int rph_eval(const EvalDesc* d, void* stream) {
   if (!d->wa || !d->stats || d->n_local < 1 || d->num_wgs < 1 || d->nin < 1 || d->nin > MAXIN)
     return rph_report("rph_eval", "bad eval descriptor");
+  if (!(d->alpha >= 0.f && d->alpha <= 1.f)) return rph_report("rph_eval", "LeakyReLU slope must be in [0, 1]");
   for (int f = 0; f < d->nin; ++f)
     if (!d->feat[f]) return rph_report("rph_eval", "null feature pointer");
   hipStream_t s = (hipStream_t)stream;

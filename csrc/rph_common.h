@@ -171,7 +171,10 @@ RPH_INLINE uint32_t sobol_point(const uint32_t* __restrict__ sv_d, uint32_t shif
 RPH_INLINE uint32_t gray_code(uint64_t i) { return (uint32_t)(i ^ (i >> 1)); }
 
 // LeakyReLU (Keras-2 default alpha=0.3)
-RPH_INLINE float lrelu(float z, float alpha) { return z > 0.f ? z : alpha * z; }
+// For 0 <= alpha <= 1 (checked on the host, validate_train), max(z, alpha z)
+// equals the select bit for bit and costs 2 VALU ops (mul + max, the mul packs)
+// instead of 3 (cmp + mul + cndmask).
+RPH_INLINE float lrelu(float z, float alpha) { return fmaxf(z, alpha * z); }
 RPH_INLINE float lrelu_d(float z, float alpha) { return z > 0.f ? 1.f : alpha; }
 
 // ---------------------------------------------------------------------------

@@ -164,6 +164,10 @@ def test_launcher_rejects_bad_descriptors():
     with pytest.raises(RuntimeError, match="batch"):
         native.train_lag_step(d, 0, 0, stream=0)
     d.steps_per_epoch = 8
+    d.alpha = 1.5  # the kernels compute LeakyReLU as max(z, alpha z)
+    with pytest.raises(RuntimeError, match="slope"):
+        native.train_lag_fit(d, 1, stream=0)
+    d.alpha = 0.3
     with pytest.raises(RuntimeError, match="null state"):
         native.train_fit(d, 1, stream=0)
 
