@@ -292,13 +292,27 @@ RPH_INLINE float ld_agent(const float* p) {
 }
 
 constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contention / 8)
+// lagged schedule, 32-unit nets: every workgroup re-reads the whole packet of
+// the previous step in its prologue, R = 1280+ floats x replicas — fewer
+// replicas trade atomic contention for prologue read traffic
+#ifndef RPH_WIDE_NREP
+#define RPH_WIDE_NREP 8
+#endif
+constexpr int WIDE_NREP = RPH_WIDE_NREP;
 
-// sum of the ACC_REPLICAS float-atomic replicas of packet entry i (fixed order)
+// sum of the first NREP (<= ACC_REPLICAS, power of two) float-atomic replicas
+// of packet entry i, pairwise in fixed order
+template <int NREP = ACC_REPLICAS>
 RPH_INLINE float sum_replicas(const float* buf, int R, int i) {
-  float rr[ACC_REPLICAS];
+  static_assert(NREP >= 1 && NREP <= ACC_REPLICAS && (NREP & (NREP - 1)) == 0, "replicas: power of two <= 8");
+  float rr[NREP];
 #pragma unroll
-  for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
-  return ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+  for (int rp = 0; rp < NREP; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
+#pragma unroll
+  for (int w = NREP / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int j = 0; j < w; ++j) rr[j] = rr[2 * j] + rr[2 * j + 1];
+  return rr[0];
 }
 
 // ---------------------------------------------------------------------------

@@ -148,14 +148,14 @@ RPH_INLINE void lag_advance_seq(const TrainDesc& d, float seq_base_bits, uint32_
 // vs 'handoff-flag').  A rank can be at most one kernel ahead of a peer, so
 // slot seq % DP_SLOTS is never overwritten while it is read; a stale granule
 // carries an older tag.  Bounded spins; fail fast on dp_error.
-template <int R>
+template <int R, int NREP>
 RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* local_acc, float* red, bool pusher) {
   const int tid = threadIdx.x;
   const int W = d.dp_world, me = d.dp_rank;
   const int slot = (int)(seq % DP_SLOTS);
   if (pusher) {
     for (int i = tid; i < R; i += 256) {
-      const float v = sum_replicas(local_acc, R, i);
+      const float v = sum_replicas<NREP>(local_acc, R, i);
       const unsigned long long g = ((unsigned long long)seq << 32) | (unsigned long long)__float_as_uint(v);
 #pragma unroll
       for (int p = 0; p < 8; ++p)
@@ -285,15 +285,10 @@ RPH_INLINE int lag_apply(LagState<P>& st, const float* red, const TrainDesc& d, 
   return stopped != 0.f ? 1 : 0;
 }
 
-// summed packet of accumulator `buf` (8 replicas) into LDS red[0..R)
-template <int R>
+// summed packet of accumulator `buf` (NREP replicas) into LDS red[0..R)
+template <int R, int NREP>
 RPH_INLINE void lag_sums(const float* buf, float* red) {
-  for (int i = threadIdx.x; i < R; i += 256) {
-    float rr[ACC_REPLICAS];
-#pragma unroll
-    for (int rp = 0; rp < ACC_REPLICAS; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
-    red[i] = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
-  }
+  for (int i = threadIdx.x; i < R; i += 256) red[i] = sum_replicas<NREP>(buf, R, i);
 }
 
 template <class B>
@@ -302,6 +297,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   constexpr int P = B::P;
   constexpr int R = B::R;
   constexpr int NR = B::NR;
+  constexpr int NREP = B::NREP;  // float-atomic replicas in use (contention vs prologue read traffic)
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ __attribute__((aligned(16))) float red[NR * 256 + 8];
@@ -323,11 +319,11 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   B::load(d, s, perm, B::first(wid), lane, pre);
   const bool dp = d.dp_world > 1;
   const float* prev = d.acc + (size_t)((k + 2) % 3) * ACC_REPLICAS * R;  // accumulator of step k-1
-  if (k > 0 && !dp) lag_sums<R>(prev, red);
+  if (k > 0 && !dp) lag_sums<R, NREP>(prev, red);
   if (stopped0 != 0.f) return;  // early-stopped fit: the remaining steps are no-ops
   __syncthreads();
   const bool w0 = blockIdx.x == 0;
-  if (k > 0 && dp && lag_dp_exchange<R>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)k, prev, red, w0))
+  if (k > 0 && dp && lag_dp_exchange<R, NREP>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)k, prev, red, w0))
     return;  // a peer timed out (dp_error is set; the host raises)
   RPH_STAMP(1);
   if (k > 0) {
@@ -354,7 +350,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
     // persist the updated state and re-arm the accumulator of step k+1 now, so
     // no optimizer state stays live (in registers) across the partial
     float* z = d.acc + (size_t)((k + 1) % 3) * ACC_REPLICAS * R;
-    for (int i = tid; i < ACC_REPLICAS * R; i += 256) st_agent(z + i, 0.f);
+    for (int i = tid; i < NREP * R; i += 256) st_agent(z + i, 0.f);
     lag_store<P>(st, d.lag + (size_t)((k + 1) & 1) * LAG_FLOATS);
   }
   __syncthreads();
@@ -371,14 +367,14 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   for (int j = 0; j < NR; ++j) {
     const int i = tid + 256 * j;
     if (i < R)
-      __hip_atomic_fetch_add(buf + (blockIdx.x % ACC_REPLICAS) * R + i, val[j], __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add(buf + (blockIdx.x % NREP) * R + i, val[j], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
   RPH_STAMP(4);
 }
 
 // Update of the last step + canonical write-back.  One workgroup.
-template <int P, int R>
+template <int P, int R, int NREP>
 __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, const int K) {
   __shared__ __attribute__((aligned(16))) float red[((R + 255) / 256) * 256 + 8];
   const bool run = d.fit->stopped == 0.f && K > 0;
@@ -388,9 +384,9 @@ __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, c
     lag_load<P>(st, d, d.lag + (size_t)(K & 1) * LAG_FLOATS, d.fit);
     const float* prev = d.acc + (size_t)((K - 1) % 3) * ACC_REPLICAS * R;
     if (d.dp_world > 1) {
-      bad = lag_dp_exchange<R>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)K, prev, red, true);
+      bad = lag_dp_exchange<R, NREP>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)K, prev, red, true);
     } else {
-      lag_sums<R>(prev, red);
+      lag_sums<R, NREP>(prev, red);
     }
   }
   // leave all three accumulators zeroed for the next fit (its kernel 0 adds

@@ -49,6 +49,7 @@ struct NarrowBody {
   static constexpr int P = S::P;
   static constexpr int R = S::R;
   static constexpr int NR = (R + 255) / 256;  // packet entries per thread (1)
+  static constexpr int NREP = ACC_REPLICAS;   // lagged schedule: float-atomic replicas
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
   struct Frags {};  // (weights are read from LDS)
@@ -166,7 +167,7 @@ struct NarrowBody {
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
       }
     }
-    RPH_STAMP(2);
+    RPH_STAMP(5);  // path loop done
     // ---- in-wave reduce-scatter, cross-wave LDS sum ------------------------
     wave_reduce_scatter<R>(g, lane);
     constexpr int PER = R / 64;
@@ -558,10 +559,17 @@ extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
     using S = NetShape<A, B, C, E>;                                                          \
-    hipLaunchKernelGGL((k_hedge_lag_finalize<S::P, S::R>), dim3(1), dim3(256), 0, s, *d, K); \
+    hipLaunchKernelGGL((k_hedge_lag_finalize<S::P, S::R, ACC_REPLICAS>), dim3(1), dim3(256), 0, s, *d, K); \
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)
+#undef X
+#define X(A, B, C, E)                                                                        \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
+    using S = NetShape<A, B, C, E>;                                                          \
+    hipLaunchKernelGGL((k_hedge_lag_finalize<S::P, S::R, WIDE_NREP>), dim3(1), dim3(256), 0, s, *d, K); \
+    return (int)hipGetLastError();                                                           \
+  }
   RPH_WIDE_SHAPES(X)
 #undef X
   return -1;

@@ -192,6 +192,7 @@ struct WideBody {
   static constexpr int P = S::P;
   static constexpr int R = S::R;  // packet width, multiple of 256
   static constexpr int NR = R / 256;
+  static constexpr int NREP = WIDE_NREP;  // lagged schedule: float-atomic replicas
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int RV = G::RV;
   static constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * IMG_PITCH * 2;
@@ -334,7 +335,7 @@ struct WideBody {
       }
       outer_mfma<F32>(img, a1, dz2, r, h, gw2);
     }
-    RPH_STAMP(2);
+    RPH_STAMP(5);  // path loop done
 
     // ---- per-wave packet -> LDS, cross-wave sum -----------------------------
     half_reduce_scatter<RV>(g, lane);

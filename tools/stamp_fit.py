@@ -77,7 +77,7 @@ def run(batch_log2=18, n_log2=20, nin=1, nout=2, hidden=8, epochs=64, max_wgs=25
         med = lambda a, b: us(np.median(s[:, b] - s[:, a]))  # noqa: E731
         t0 = s[:, 0].min()
         out.update({"start_spread_us": us(s[:, 0].max() - t0), "prologue_us": med(0, 1), "update_us": med(1, 2),
-                    "partial_us": med(2, 3), "publish_us": med(3, 4),
+                    "paths_us": med(2, 5), "reduce_us": med(5, 3), "publish_us": med(3, 4),
                     "last_end_after_start_us": us(s[:, 4].max() - t0)})
         be.stamps = None
     return out

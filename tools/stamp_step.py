@@ -43,7 +43,7 @@ def run(batch_log2=16, n_log2=20, nin=1, nout=2, reps=20, det=False, max_wgs=256
         ph = lambda a, b: np.median(s[:, b] - s[:, a]) * 10.0 / 1000.0  # noqa: E731  (us)
         rows.append({
             "dispatch_spread_us": float((s[:, 0].max() - t0) * 0.01),
-            "prologue_us": float(ph(0, 1)), "paths_us": float(ph(1, 2)), "reduce_us": float(ph(2, 3)),
+            "prologue_us": float(ph(0, 1)), "paths_reduce_us": float(ph(1, 3)),
             "publish_drain_us": float(ph(3, 4)), "ticket_us": float(ph(4, 5)),
             "last_fetch_us": float((s[last, 6] - s[last, 5]) * 0.01),
             "last_update_us": float((s[last, 7] - s[last, 6]) * 0.01),
