@@ -399,6 +399,9 @@ class HedgeRun:
 # reference-compatible entry points
 # ---------------------------------------------------------------------------
 def _print_dates(run: HedgeRun, res: RunResult):
+    """Per-date log of the reference (RP:194, :122); ``verbose=2`` adds the
+    Keras-style per-epoch training log of every fit (``fit(verbose=1)`` in
+    "European Options.ipynb" cell 13) from the on-device epoch-loss history."""
     if not run.cfg.verbose or not run.di.is_main:
         return
     ind = res.induction
@@ -406,6 +409,15 @@ def _print_dates(run: HedgeRun, res: RunResult):
     dtc = run.grid.dt_coarse
     for d in ind.dates:
         t = d.index
+        if int(run.cfg.verbose) >= 2:
+            for name, fs in (("mse", d.fit_mse), ("q99", d.fit_q99)):
+                if not fs:
+                    continue
+                hist = fs["history"]
+                for e, loss in enumerate(hist):
+                    print(f"[t={t * dtc:.4f} {name}] Epoch {e + 1}/{len(hist)} - loss: {loss:.4e}")
+                print(f"[t={t * dtc:.4f} {name}] mae: {fs['mae']:.4e} - mape: {fs['mape']:.4f}"
+                      f"{' - early stop' if fs['stopped'] and len(hist) else ''}")
         y = float(p.asset(t + 1).double().mean()) * (1.0 if run.kind == "pension" else run.cfg.Y)
         line = f">> Y_({(t + 1) * dtc:.2f}) = {y:.3f}"
         if p.nfrac is not None:

@@ -246,3 +246,14 @@ def test_nan_gradient_guard_cpu():
            FitConfig(epochs=3, patience=100, early_stopping=False), seed=1)
     assert np.all(np.isfinite(current_weights(spec, w)))
     assert float(o[L.O_NAN]) == 3.0   # one poisoned batch per epoch
+
+
+def test_verbose_epoch_log(capsys):
+    """verbose=2: Keras-style per-epoch loss lines for every fit (EO cell 13 log)."""
+    from rphedge.api import run_params
+
+    p = _small(verbose=2, epochs_first=4, epochs_rest=2, early_stopping=False)
+    run_params(p)
+    out = capsys.readouterr().out
+    assert "Epoch 4/4 - loss:" in out and "mse]" in out and "q99]" in out
+    assert "mae:" in out and "reduction =" in out
