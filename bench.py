@@ -28,6 +28,7 @@ one-run-per-step timing, simulation inside the graph):
   heston30    Heston stochastic vol, 30 dates (10 Euler substeps each), 2^20 paths per GPU
   euro252     European call, 252-step GBM, 2^21 paths per GPU (16M paths at 8 GPUs)
   basket5     basket-of-5 European call, 252 steps, 2^23 paths per GPU (64M at 8 GPUs)
+  euro30_mfma euro30 with the 32-unit hedge MLP on the matrix cores (bf16 MFMA, "bf16 hedge-MLP")
   euro1_cpu   European call, 1-step GBM, 2^14 (>= 10k) paths, CPU torch backend (plumbing)
 Per-GPU path counts are the 8-GPU configs divided by 8 (weak scaling), so a
 1-GPU run measures exactly the per-GPU shard of the 8-GPU job.
@@ -64,6 +65,9 @@ PRESETS = {
                     batch_log2=18, lr=1e-2, lr_rest=1e-3,
                     extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
                     label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
+    "euro30_mfma": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
+                        batch_log2=18, lr=5e-3, lr_rest=1e-3, lr_decay=0.1, hidden=32,
+                        label="European call, 30-step GBM, 1M paths per GPU, 32-unit hedge MLP on bf16 MFMA"),
     "euro1_cpu": dict(model="gbm_log", dates=1, substeps=1, paths_log2=14, epochs_first=200, epochs_rest=0,
                       batch_log2=11, lr=1e-2, lr_rest=1e-3, cpu=True,
                       label="European call, 1-step GBM, 16k (>=10k) Sobol paths, CPU plumbing"),
@@ -84,11 +88,11 @@ def parse(argv=None):
     ap.add_argument("--batch-log2", type=int, default=None, help="per-GPU minibatch (global = N x this)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--lr-rest", type=float, default=None)
-    ap.add_argument("--lr-decay", type=float, default=0.02, help="per-date geometric LR decay factor (last/first epoch)")
-    ap.add_argument("--hidden", type=int, default=8, help="hidden width (8 = reference net; 32 = MFMA kernel)")
+    ap.add_argument("--lr-decay", type=float, default=None, help="per-date geometric LR decay factor (last/first epoch)")
+    ap.add_argument("--hidden", type=int, default=None, help="hidden width (8 = reference net; 32 = MFMA kernel)")
     ap.add_argument("--mfma-precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--variant", type=int, default=-1, help="narrow lag-kernel variant (-1: engine default)")
-    ap.add_argument("--max-wgs", type=int, default=256, help="workgroups per training step")
+    ap.add_argument("--max-wgs", type=int, default=0, help="workgroups per training step (0: engine default)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -97,6 +101,10 @@ def parse(argv=None):
     for k in ("paths_log2", "dates", "substeps", "epochs_first", "epochs_rest", "batch_log2", "lr", "lr_rest"):
         if getattr(a, k) is None:
             setattr(a, k, pre[k])
+    if a.lr_decay is None:
+        a.lr_decay = pre.get("lr_decay", 0.02)
+    if a.hidden is None:
+        a.hidden = pre.get("hidden", 8)
     if pre.get("cpu"):
         a.cpu = True
     return a

@@ -139,6 +139,78 @@ RPH_INLINE void outer_mfma(void* img, const float (&a1)[16], const float (&dz2)[
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- bf16 path: one conversion per activation, shared by the layer MFMA and
+// the dW2 transpose image.  Registers 8s..8s+7 of an accumulator-layout tile
+// are packed pairwise (v_cvt_pk_bf16_f32) into fragment s = the B operand of
+// a product over the unit index (k order = accumulator order).
+RPH_INLINE void pack_bf16(const float (&x)[16], bf16x8 (&b)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[s][j] = (__bf16)x[8 * s + j];
+}
+
+RPH_INLINE f32x16 layer_mfma_bf16(const WFrag<false>& w, const bf16x8 (&b)[2]) {
+  f32x16 acc = {};
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.f[0], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.f[1], b[1], acc, 0, 0, 0);
+  return acc;
+}
+
+// dW2 += A1ᵀ·dZ2 over the 32 paths of the tile, bf16.  Each lane stores its
+// packed registers 4g..4g+3 (units 8g+4h..+3 of path r, 8 bytes) into a
+// [path][unit] image (TR_PITCH-byte rows, padded against write conflicts) and
+// the MFMA operands (unit r, 8 consecutive paths) come back with the gfx950
+// transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): lane 4q+p
+// of each 16-lane group addresses image row r0+q, units c0+4p..+3, and lane i
+// of the group receives unit c0+i of rows r0..r0+3.  EXEC is all ones here
+// (the tile loop is wave-uniform), as the transposing read requires.
+constexpr int TR_PITCH = 72;  // bytes per image row (32 bf16 + 8 B pad)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+RPH_INLINE void outer_mfma_tr(unsigned char* img, const bf16x8 (&a1b)[2], const bf16x8 (&dzb)[2], int r, int h,
+                              int lane, f32x16& acc) {
+  unsigned char* IA = img;
+  unsigned char* IB = img + 32 * TR_PITCH;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int off = r * TR_PITCH + (8 * g4 + 4 * h) * 2;
+    const bf16x8& sa = a1b[g4 >> 1];
+    const bf16x8& sb = dzb[g4 >> 1];
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const bf16x4 va = {sa[4 * (g4 & 1) + 0], sa[4 * (g4 & 1) + 1], sa[4 * (g4 & 1) + 2], sa[4 * (g4 & 1) + 3]};
+    const bf16x4 vb = {sb[4 * (g4 & 1) + 0], sb[4 * (g4 & 1) + 1], sb[4 * (g4 & 1) + 2], sb[4 * (g4 & 1) + 3]};
+    *(bf16x4*)(IA + off) = va;
+    *(bf16x4*)(IB + off) = vb;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int grp = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c0 = 16 * (grp & 1), hh = grp >> 1;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 fa, fb;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int off = (16 * s + 8 * hh + 4 * t + q) * TR_PITCH + (c0 + 4 * p) * 2;
+      const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IA + off));
+      const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IB + off));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        fa[4 * t + e] = __builtin_bit_cast(__bf16, ra[e]);
+        fb[4 * t + e] = __builtin_bit_cast(__bf16, rb[e]);
+      }
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
+  }
+  // the next tile rewrites the images: its writes must follow these reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Per-lane register vector of the small gradients (units of this lane half)
 template <int NIN, int NO>
 struct SmallGrad {
@@ -195,7 +267,7 @@ struct WideBody {
   static constexpr int NREP = WIDE_NREP;  // lagged schedule: float-atomic replicas
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int RV = G::RV;
-  static constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * IMG_PITCH * 2;
+  static constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * TR_PITCH;
   static constexpr int SCRATCH_FLOATS = ((4 * IMG_BYTES > 4 * R * 4) ? 4 * IMG_BYTES : 4 * R * 4) / 4 + 8;
   static_assert(R % 256 == 0, "wide packet must be a multiple of 256");
   struct Frags {
@@ -230,7 +302,7 @@ struct WideBody {
 
   // wl: weights in LDS; scratch: SCRATCH_FLOATS of LDS; pre: first tile (loaded).
   // Returns in val[k] the workgroup sum of packet entry tid + 256 k.
-  RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ wl,
+  RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ wl_in,
                                  const Frags& fr, float* scratch, Pre& pre, float (&val)[NR]) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -255,24 +327,38 @@ struct WideBody {
       const bool valid = pre.valid;
       if (T + nwaves < ntiles) load(d, step, perm, T + nwaves, lane, pre);  // software pipelining
 
+      // weights are re-read from LDS every tile through an opaque zero offset:
+      // hoisted, the ~100 per-lane layer-1/2/3 weights overflowed into AGPRs and
+      // came back with v_accvgpr_read every tile
+      const float* __restrict__ wl = wl_in;
+      {
+        uint32_t zo = 0;
+        asm volatile("" : "+v"(zo));
+        wl = (const float*)__builtin_assume_aligned(wl_in + (zo & ~3u), 16);
+      }
       // ---- forward --------------------------------------------------------
-      float z1[16], a1[16];
+      // (z1, z2 are not kept: for 0 <= alpha <= 1, lrelu'(z) = [a > 0 ? 1 : alpha]
+      // with a = lrelu(z), so the activations alone carry the backward mask)
+      float a1[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int u = unit_of(q, h);
         float acc = wl[S::OB1 + u];
 #pragma unroll
         for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], wl[S::OW1 + f * WH + u], acc);
-        z1[q] = acc;
         a1[q] = lrelu(acc, alpha);
       }
-      const f32x16 z2acc = layer_mfma<F32>(fr.w2t, a1);
-      float z2[16], a2[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        z2[q] = z2acc[q] + wl[S::OB2 + unit_of(q, h)];
-        a2[q] = lrelu(z2[q], alpha);
+      bf16x8 a1b[2];
+      f32x16 z2acc;
+      if constexpr (F32) {
+        z2acc = layer_mfma<F32>(fr.w2t, a1);
+      } else {
+        pack_bf16(a1, a1b);
+        z2acc = layer_mfma_bf16(fr.w2t, a1b);
       }
+      float a2[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a2[q] = lrelu(z2acc[q] + wl[S::OB2 + unit_of(q, h)], alpha);
       float o[NO];
 #pragma unroll
       for (int k = 0; k < NO; ++k) {
@@ -322,18 +408,29 @@ struct WideBody {
           g[G::DW3 + q * NO + k] = fmaf(a2[q], dout[k], g[G::DW3 + q * NO + k]);
           da = fmaf(wl[S::OW3 + u * NO + k], dout[k], da);
         }
-        dz2[q] = da * lrelu_d(z2[q], alpha);
+        dz2[q] = a2[q] > 0.f ? da : alpha * da;
         g[G::DB2 + q] += dz2[q];
       }
-      const f32x16 da1 = layer_mfma<F32>(fr.w2, dz2);
+      bf16x8 dzb[2];
+      f32x16 da1;
+      if constexpr (F32) {
+        da1 = layer_mfma<F32>(fr.w2, dz2);
+      } else {
+        pack_bf16(dz2, dzb);
+        da1 = layer_mfma_bf16(fr.w2, dzb);
+      }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const float dz1 = da1[q] * lrelu_d(z1[q], alpha);
+        const float dz1 = a1[q] > 0.f ? da1[q] : alpha * da1[q];
         g[G::DB1 + q] += dz1;
 #pragma unroll
         for (int f = 0; f < NIN; ++f) g[G::DW1 + f * 16 + q] = fmaf(x[f], dz1, g[G::DW1 + f * 16 + q]);
       }
-      outer_mfma<F32>(img, a1, dz2, r, h, gw2);
+      if constexpr (F32) {
+        outer_mfma<F32>(img, a1, dz2, r, h, gw2);
+      } else {
+        outer_mfma_tr((unsigned char*)img, a1b, dzb, r, h, lane, gw2);
+      }
     }
     RPH_STAMP(5);  // path loop done
 

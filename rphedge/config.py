@@ -66,7 +66,7 @@ class TrainingParams:
     leaky_alpha: float = 0.3
     poll_every: int = 0              # host early-stop polling (0 = fully async / graph)
     deterministic: bool = False      # fixed-order gradient reduction (bitwise reproducible)
-    max_wgs: int = 256               # workgroups per training step
+    max_wgs: int = 0                 # workgroups per training step (0: engine default per net family)
     hidden: int = 8                  # hidden width: 8 = reference nets (VALU kernel), 32 = MFMA kernel
     mfma_precision: str = "bf16"     # 32-unit nets: "bf16" (32x32x16 MFMA) or "fp32" (exact 32x32x2 MFMA)
     step_mode: str = "auto"          # GPU step schedule: auto | lag | ticket | persistent (engine.TrainConfig)

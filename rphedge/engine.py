@@ -72,7 +72,9 @@ class TrainConfig:
     beta1: float = 0.9
     beta2: float = 0.999
     eps: float = 1e-7              # Keras epsilon
-    max_wgs: int = 256             # workgroups per training step
+    max_wgs: int = 0               # workgroups per training step; 0 = auto: 256 (one per CU), 512 for
+                                   # the 32-unit bf16 nets with <= 2 inputs (2 resident waves/SIMD:
+                                   # the MFMA tile chain is latency-bound, profiles/sweep_r1n_wide_wgs.jsonl)
     paths_per_thread: int = 1      # target work per thread per step
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
@@ -209,7 +211,10 @@ class HipBackend:
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
         self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (4 if self.R > 128 else 0)
         work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
-        self.num_wgs = int(max(1, min(tcfg.max_wgs, work)))
+        mw = int(tcfg.max_wgs)
+        if mw <= 0:
+            mw = 512 if (spec.hidden == 32 and not tcfg.mfma_fp32 and spec.nin <= 2) else 256
+        self.num_wgs = int(max(1, min(mw, work)))
         dev = self.device
         self.slab = torch.zeros(self.num_wgs, self.R, dtype=torch.float32, device=dev)
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
