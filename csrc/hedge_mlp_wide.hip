@@ -211,6 +211,28 @@ RPH_INLINE void outer_mfma_tr(unsigned char* img, const bf16x8 (&a1b)[2], const 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// o[k] = part[k](lane half 0) + part[k](lane half 1), in every lane, for k < NO.
+// Pairs (2m, 2m+1): one v_permlane32_swap leaves the sum of output 2m in the
+// low half and of 2m+1 in the high half, a second swap of that sum with itself
+// hands each half the other's; an odd last output takes one self-swap.
+template <int NO>
+RPH_INLINE void half_sum_outputs(const float (&part)[NO], float (&o)[NO]) {
+#pragma unroll
+  for (int m = 0; m + 1 < NO; m += 2) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(part[m]), __float_as_uint(part[m + 1]), false,
+                                                    false);
+    const float sm = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // lo: o[m], hi: o[m+1]
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(sm), __float_as_uint(sm), false, false);
+    o[m] = __uint_as_float(b[0]);
+    o[m + 1] = __uint_as_float(b[1]);
+  }
+  if constexpr (NO & 1) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(part[NO - 1]), __float_as_uint(part[NO - 1]),
+                                                    false, false);
+    o[NO - 1] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+}
+
 // Per-lane register vector of the small gradients (units of this lane half)
 template <int NIN, int NO>
 struct SmallGrad {
@@ -360,12 +382,20 @@ struct WideBody {
 #pragma unroll
       for (int q = 0; q < 16; ++q) a2[q] = lrelu(z2acc[q] + wl[S::OB2 + unit_of(q, h)], alpha);
       float o[NO];
+      {
+        float part[NO];  // this lane half's 16 units
 #pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        float acc = 0.f;
+        for (int k = 0; k < NO; ++k) {
+          float acc = 0.f;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc = fmaf(a2[q], wl[S::OW3 + unit_of(q, h) * NO + k], acc);
-        o[k] = acc + __shfl_xor(acc, 32, 64) + wl[S::OB3 + k];  // both halves: full sum over 32 units
+          for (int q = 0; q < 16; ++q) acc = fmaf(a2[q], wl[S::OW3 + unit_of(q, h) * NO + k], acc);
+          part[k] = acc;
+        }
+        // full sums over the two lane halves with v_permlane32_swap (VALU, on
+        // the forward->loss->backward critical path) instead of ds_bpermute
+        half_sum_outputs<NO>(part, o);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) o[k] += wl[S::OB3 + k];
       }
       float hold[NHOLD];
       if (HEAD == HEAD_COMPLEMENT) {
