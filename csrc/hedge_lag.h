@@ -166,28 +166,6 @@ RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* lo
   }
   int bad = 0;
   const unsigned long long* mb = (const unsigned long long*)d.dp_mbox[me] + (size_t)slot * W * R;
-  // wait phase on ONE sentinel granule per peer (its last entry, polled by
-  // thread p of every workgroup) instead of every thread polling its entry's
-  // W granules: the fine-grained mailbox is read around the caches, and
-  // 256 workgroups x R x W polls per round would hammer a few HBM channels for
-  // the whole wait.  The per-entry tags below still decide correctness (entries
-  // of one peer may land in any order); they are almost always already there.
-  if (tid < W) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned it = 0;
-    while ((uint32_t)(__hip_atomic_load(const_cast<unsigned long long*>(mb + (size_t)tid * R + (R - 1)),
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32) != seq) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((++it & 63u) == 0u &&
-          (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||  // 2 s: a peer never arrived
-           __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
-        __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        bad = 1;
-        break;
-      }
-    }
-  }
-  if (__syncthreads_or(bad)) return 1;
   for (int i = tid; i < R; i += 256) {
     float vals[8];
     unsigned todo = (1u << W) - 1u;
