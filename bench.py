@@ -93,6 +93,8 @@ def parse(argv=None):
     ap.add_argument("--mfma-precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--variant", type=int, default=-1, help="narrow lag-kernel variant (-1: engine default)")
     ap.add_argument("--max-wgs", type=int, default=0, help="workgroups per training step (0: engine default)")
+    ap.add_argument("--feature-norm", default=None, choices=["none", "global", "date"],
+                    help="input standardisation fused into the kernels (default: preset)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -105,6 +107,8 @@ def parse(argv=None):
         a.lr_decay = pre.get("lr_decay", 0.02)
     if a.hidden is None:
         a.hidden = pre.get("hidden", 8)
+    if a.feature_norm is None:
+        a.feature_norm = pre.get("feature_norm", "date")
     if pre.get("cpu"):
         a.cpu = True
     return a
@@ -118,7 +122,7 @@ def build_run(a, world: int):
                         epochs_rest=a.epochs_rest, patience_first=10 ** 6, patience_rest=10 ** 6,
                         lr=a.lr, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
                         chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision,
-                        variant=a.variant, max_wgs=a.max_wgs)
+                        variant=a.variant, max_wgs=a.max_wgs, feature_norm=a.feature_norm)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -242,7 +246,7 @@ def main(argv=None):
                             + PRESETS[a.preset]["label"],
                    "preset": a.preset,
                    "global_batch": cfg.train.batch_size, "seq_len": n_dates,
-                   "substeps": a.substeps, "option": {k: getattr(cfg, k) for k in
+                   "substeps": a.substeps, "feature_norm": a.feature_norm, "option": {k: getattr(cfg, k) for k in
                                                       ("Y", "K", "T", "r", "sigma", "kappa", "theta", "xi",
                                                        "rho", "v0", "n_assets", "basket_corr")
                                                       if cfg.model in ("heston", "basket") or

@@ -377,6 +377,7 @@ RPH_INLINE void dp_allreduce(const TrainDesc& d, float* red) {
 // all-reduced packet grad_out[LEN].
 template <int P, int LEN>
 __global__ __launch_bounds__(256) void k_hedge_update(const TrainDesc d, const int step, const int epoch) {
+  prefetch_kernarg<sizeof(TrainDesc) + 2 * sizeof(int)>();
   __shared__ float gs[LEN + 8];
   if (d.fit->stopped != 0.f) return;
   UpdPre<P> up;
@@ -423,8 +424,11 @@ inline int validate_train(const TrainDesc* d, int mode, const char* who) {
     return rph_report(who, "batch / steps_per_epoch do not cover n_local");
   if (d->chunk_log2 < 0 || d->chunk_log2 > 20) return rph_report(who, "chunk_log2 out of range");
   if (!d->wts || !d->opt || !d->fit || !d->target) return rph_report(who, "null state or target pointer");
-  for (int f = 0; f < d->nin; ++f)
+  for (int f = 0; f < d->nin; ++f) {
     if (!d->feat[f]) return rph_report(who, "null feature pointer");
+    if (!(d->fisd[f] > 0.f && d->fisd[f] < 3.0e38f && d->fmu[f] == d->fmu[f]))
+      return rph_report(who, "feature standardisation must be finite with fisd > 0");
+  }
   for (int k = 0; k < nhold - 1; ++k)
     if (!d->price[k]) return rph_report(who, "null price pointer");
   if (mode == 1 && (!d->lag || !d->acc)) return rph_report(who, "lagged step needs lag and acc buffers");

@@ -298,6 +298,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   constexpr int R = B::R;
   constexpr int NR = B::NR;
   constexpr int NREP = B::NREP;  // float-atomic replicas in use (contention vs prologue read traffic)
+  prefetch_kernarg<sizeof(TrainDesc) + 2 * sizeof(int) + sizeof(Perm)>();
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ __attribute__((aligned(16))) float red[NR * 256 + 8];
@@ -376,6 +377,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
 // Update of the last step + canonical write-back.  One workgroup.
 template <int P, int R, int NREP>
 __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, const int K) {
+  prefetch_kernarg<sizeof(TrainDesc) + sizeof(int)>();
   __shared__ __attribute__((aligned(16))) float red[((R + 255) / 256) * 256 + 8];
   const bool run = d.fit->stopped == 0.f && K > 0;
   LagState<P> st;

@@ -68,11 +68,12 @@ struct NarrowBody {
     p.valid = (jl < d.batch) && (j < d.n_local);
     const uint32_t q = p.valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
 #pragma unroll
-    for (int f = 0; f < NIN; ++f) p.x[f] = p.valid ? d.feat[f][q] : 0.f;
+    for (int f = 0; f < NIN; ++f) p.x[f] = d.feat[f][q];  // raw, unselected (q = 0 when invalid; invalid paths carry dV = 0):
+                                                   // no v_cndmask forcing an early vmcnt wait
 #pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = p.valid ? d.price[k][q] : 0.f;
+    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = d.price[k][q];
     p.pr[NHOLD - 1] = d.bond;
-    p.y = p.valid ? d.target[q] : 0.f;
+    p.y = d.target[q];
   }
 
   // W: weights in LDS; lds: SCRATCH_FLOATS of LDS; pre: the first path (loaded).
@@ -108,7 +109,7 @@ struct NarrowBody {
       }
       float x[NIN], pr[NHOLD];
 #pragma unroll
-      for (int f = 0; f < NIN; ++f) x[f] = q[0].x[f];
+      for (int f = 0; f < NIN; ++f) x[f] = (q[0].x[f] - d.fmu[f]) * d.fisd[f];
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) pr[k] = q[0].pr[k];
       const float y = q[0].y;
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
   using B = NarrowBody<NIN, H, NO, HEAD>;
   constexpr int R = B::R;
   constexpr int P = B::P;
+  prefetch_kernarg<sizeof(TrainDesc) + 2 * sizeof(int) + sizeof(Perm)>();
   __shared__ __attribute__((aligned(16))) float lds[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ int s_last;
@@ -331,6 +333,7 @@ template <int NIN, int H, int NO, int HEAD>
 __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   using S = NetShape<NIN, H, NO, HEAD>;
   constexpr int NHOLD = S::NHOLD;
+  prefetch_kernarg<sizeof(EvalDesc)>();
   RPH_DASSERT(d.n_local > 0 && d.num_wgs == (int)gridDim.x && d.wa != nullptr && d.stats != nullptr);
   __shared__ double sst[4][EVAL_NSTAT];
   constexpr int WBOFF = (S::P + 3) / 4 * 4;  // net B's weights 16-byte aligned (ds_read_b128)
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
     in.valid = p < d.n_local;
     const int pp = in.valid ? p : 0;
 #pragma unroll
-    for (int f = 0; f < NIN; ++f) in.x[f] = d.feat[f][pp];
+    for (int f = 0; f < NIN; ++f) in.x[f] = d.feat[f][pp];  // raw (ring): standardised where consumed
 #pragma unroll
     for (int k = 0; k < NHOLD - 1; ++k) {
       in.pt[k] = d.price_t[k][pp];
@@ -397,14 +400,16 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
     asm volatile("" : "+v"(zo));
     const float* __restrict__ WAi = (const float*)__builtin_assume_aligned(WA + (zo & ~3u), 16);
     const float* __restrict__ WBi = (const float*)__builtin_assume_aligned(WB + (zo & ~3u), 16);
-    float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], holdv[NHOLD];
-    net_forward<NIN, H, NO, HEAD>(WAi, cur.x, d.alpha, z1, a1, z2, a2, hold);
+    float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], holdv[NHOLD], xn[NIN];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) xn[f] = (cur.x[f] - d.fmu[f]) * d.fisd[f];
+    net_forward<NIN, H, NO, HEAD>(WAi, xn, d.alpha, z1, a1, z2, a2, hold);
 #pragma unroll
     for (int k = 0; k < NHOLD; ++k) holdv[k] = hold[k];
     if (has_b) {
       // V_t comes from net B (model2.predict, RP:218); reported holdings are
       // the blend hA + hold_c (hB - hA) (get_phi_psi_VaR, RP:114-115).
-      net_forward<NIN, H, NO, HEAD>(WBi, cur.x, d.alpha, z1, a1, z2, a2, holdv);
+      net_forward<NIN, H, NO, HEAD>(WBi, xn, d.alpha, z1, a1, z2, a2, holdv);
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) hold[k] = hold[k] + d.hold_c * (holdv[k] - hold[k]);
     }
@@ -617,6 +622,9 @@ extern "C" int rph_eval(const EvalDesc* d, void* stream) {
   if (!d->wa || !d->stats || d->n_local < 1 || d->num_wgs < 1 || d->nin < 1 || d->nin > MAXIN)
     return rph_report("rph_eval", "bad eval descriptor");
   if (!(d->alpha >= 0.f && d->alpha <= 1.f)) return rph_report("rph_eval", "LeakyReLU slope must be in [0, 1]");
+  for (int f = 0; f < d->nin; ++f)
+    if (!(d->fisd[f] > 0.f && d->fisd[f] < 3.0e38f && d->fmu[f] == d->fmu[f]))
+      return rph_report("rph_eval", "feature standardisation must be finite with fisd > 0");
   for (int f = 0; f < d->nin; ++f)
     if (!d->feat[f]) return rph_report("rph_eval", "null feature pointer");
   hipStream_t s = (hipStream_t)stream;

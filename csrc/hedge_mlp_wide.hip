@@ -315,11 +315,12 @@ struct WideBody {
     p.valid = (jl < d.batch) && (j < d.n_local);
     const uint32_t q = p.valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
 #pragma unroll
-    for (int f = 0; f < NIN; ++f) p.x[f] = p.valid ? d.feat[f][q] : 0.f;
+    for (int f = 0; f < NIN; ++f) p.x[f] = d.feat[f][q];  // raw, unselected (q = 0 when invalid; invalid paths carry dV = 0):
+                                                   // no v_cndmask forcing an early vmcnt wait
 #pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = p.valid ? d.price[k][q] : 0.f;
+    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = d.price[k][q];
     p.pr[NHOLD - 1] = d.bond;
-    p.y = p.valid ? d.target[q] : 0.f;
+    p.y = d.target[q];
   }
 
   // wl: weights in LDS; scratch: SCRATCH_FLOATS of LDS; pre: first tile (loaded).
@@ -342,7 +343,7 @@ struct WideBody {
     for (int T = first(wid); T < ntiles; T += nwaves) {
       float x[NIN], pr[NHOLD];
 #pragma unroll
-      for (int f = 0; f < NIN; ++f) x[f] = pre.x[f];
+      for (int f = 0; f < NIN; ++f) x[f] = (pre.x[f] - d.fmu[f]) * d.fisd[f];
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) pr[k] = pre.pr[k];
       const float y = pre.y;
@@ -495,6 +496,7 @@ __global__ __launch_bounds__(256) void k_hedge_train_step_wide(const TrainDesc d
   constexpr int P = B::P;
   constexpr int R = B::R;
   constexpr int NR = B::NR;
+  prefetch_kernarg<sizeof(TrainDesc) + 2 * sizeof(int) + sizeof(Perm)>();
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ int s_last;

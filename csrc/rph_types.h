@@ -105,6 +105,8 @@ struct TrainDesc {
   int variant;                   // kernel variant (narrow: 1 = 2 waves/SIMD, weights re-read from LDS)
   const FitState* fit_init;      // lagged schedule: fit-state template read by kernel 0, which also
                                  // writes it to `fit` (no separate template copy per fit); may be null
+  float fmu[MAXIN];              // input standardisation x' = (x - fmu) * fisd, fused into the feature
+  float fisd[MAXIN];             // loads (identity: 0 / 1; the host folds it into layer 1 on export)
 };
 
 constexpr int DP_SLOTS = 4;
@@ -129,6 +131,8 @@ struct EvalDesc {
   int n_local;
   int num_wgs;
   int nin, h, nout, head;
+  float fmu[MAXIN];              // input standardisation x' = (x - fmu) * fisd (identity: 0 / 1)
+  float fisd[MAXIN];
 };
 
 // Eval stats slab columns

@@ -55,12 +55,12 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(TrainDesc, bond), OFF(TrainDesc, inv_batch), OFF(TrainDesc, loss), OFF(TrainDesc, seed),
       OFF(TrainDesc, num_wgs), OFF(TrainDesc, head), OFF(TrainDesc, acc), OFF(TrainDesc, deterministic), OFF(TrainDesc, stamps),
       OFF(TrainDesc, dp_world), OFF(TrainDesc, dp_mbox), OFF(TrainDesc, dp_flags), OFF(TrainDesc, dp_counter), OFF(TrainDesc, dp_error),
-      OFF(TrainDesc, fit_init),
+      OFF(TrainDesc, fit_init), OFF(TrainDesc, fmu), OFF(TrainDesc, fisd),
       // EvalDesc
       (long long)sizeof(EvalDesc), OFF(EvalDesc, price_t), OFF(EvalDesc, price_t1), OFF(EvalDesc, target),
       OFF(EvalDesc, wa), OFF(EvalDesc, g_base), OFF(EvalDesc, v_out), OFF(EvalDesc, hold_out),
       OFF(EvalDesc, resid_out), OFF(EvalDesc, pred1_out), OFF(EvalDesc, stats), OFF(EvalDesc, bond_t),
-      OFF(EvalDesc, hold_c), OFF(EvalDesc, n_local), OFF(EvalDesc, head),
+      OFF(EvalDesc, hold_c), OFF(EvalDesc, n_local), OFF(EvalDesc, head), OFF(EvalDesc, fmu), OFF(EvalDesc, fisd),
       // SimDesc
       (long long)sizeof(SimDesc), OFF(SimDesc, path_offset), OFF(SimDesc, sv1), OFF(SimDesc, dims1),
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),

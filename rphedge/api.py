@@ -236,7 +236,8 @@ class HedgeRun:
                                shared_q99_model=pf.shared_q99_model,
                                holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start,
                                restore_best_at_end=pf.restore_best_at_end, keep_paths=c.keep_paths,
-                               poll_every=tr.poll_every, seed=tr.seed)
+                               poll_every=tr.poll_every, seed=tr.seed,
+                               feature_norm="none" if pf.raw_features else tr.feature_norm)
         backend_q = None
         if (self.backend_kind == "hip" and self.di.world == 1 and icfg.q99 and not icfg.shared_q99_model
                 and not icfg.poll_every and tr.concurrent_q99):
@@ -319,6 +320,12 @@ class HedgeRun:
         ind = self.induction
         _, spec, w, wq, vals = load_date(out_dir, date)
         assert spec.nparams == self.spec.nparams, "saved network shape differs from this configuration"
+        # saved weights are raw-input; the warm start continues in this run's
+        # standardised coordinates of the saved date
+        if ind.norms:
+            mu, isd = ind.norms[min(date, len(ind.norms) - 1)]
+            w = hm.unfold_input_norm(self.spec, w, mu, isd)
+            wq = hm.unfold_input_norm(self.spec, wq, mu, isd) if wq is not None else None
         set_weights(self.spec, ind.w_init, w)
         if wq is not None and ind.cfg.q99 and not ind.cfg.shared_q99_model:
             self._wq_resume = wq

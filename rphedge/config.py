@@ -35,6 +35,7 @@ class ParityFlags:
     local_residual_pnl: bool = True     # Q24: "P&L at T" is the one-step residual
     complement_head: bool = False       # Q13: European psi = 1 - phi head
     eo_discount_artifact: bool = False  # Q14: report V0*e^{-rT} as "discounted E[V(T)]"
+    raw_features: bool = False          # reference nets see raw (unstandardised) state features
 
     @classmethod
     def reference(cls) -> "ParityFlags":
@@ -42,7 +43,7 @@ class ParityFlags:
                    sv_c_overwrite=True, sv_reference_dynamics=True, sv_sqrt_nan=True,
                    fine_terminal_payoff=True, lr_schedule_first_only=True, warm_start=True,
                    restore_best_at_end=False, numpy_binomial=True, local_residual_pnl=True,
-                   complement_head=True, eo_discount_artifact=True)
+                   complement_head=True, eo_discount_artifact=True, raw_features=True)
 
 
 @dataclass
@@ -72,6 +73,8 @@ class TrainingParams:
     step_mode: str = "auto"          # GPU step schedule: auto | lag | ticket | persistent (engine.TrainConfig)
     variant: int = -1                # narrow lag-kernel variant (-1: engine default; see engine.TrainConfig)
     concurrent_q99: bool = True      # two networks: run the pinball fit concurrently with the MSE fit (GPU)
+    feature_norm: str = "date"       # input standardisation: none | global | date (driver.feature_norms);
+                                     # ParityFlags.raw_features forces none (reference)
 
 
 @dataclass

@@ -48,6 +48,10 @@ class InductionConfig:
     snapshot_weights: bool = True        # per-date weights for the saved-model format
     poll_every: int = 0                  # host early-stop polling (0 = async)
     seed: int = 1234
+    # input standardisation (fused into the kernels' feature loads):
+    # "none" = raw features (reference), "global" = one mean/std per feature
+    # pooled over all fitted dates, "date" = per-date mean/std
+    feature_norm: str = "none"
 
 
 @dataclass
@@ -135,6 +139,7 @@ class BackwardInduction:
         self.snap = torch.zeros(self.n_dates, 2, L.NETW_FLOATS, dtype=torch.float32, device=dev) \
             if icfg.snapshot_weights else None
         self.lr_first = tuple(keras_lr_schedule(icfg.epochs_first)) if icfg.lr_schedule_first else None
+        self.norms = feature_norms(paths, icfg.feature_norm, world)
 
     def _fcfg(self, first: bool, loss: int) -> FitConfig:
         c = self.cfg
@@ -145,8 +150,10 @@ class BackwardInduction:
 
     def date_data(self, t: int) -> DateData:
         p = self.paths
+        mu, isd = self.norms[t] if self.norms else ((), ())
         return DateData(feats=p.features(t), prices_next=p.prices(t + 1), bond_next=float(p.bond[t + 1]),
-                        target=self.values[t + 1], prices_now=p.prices(t), bond_now=float(p.bond[t]))
+                        target=self.values[t + 1], prices_now=p.prices(t), bond_now=float(p.bond[t]),
+                        fmu=mu, fisd=isd)
 
     def enqueue(self, start: int | None = None):
         """Enqueue dates ``start, start-1, ..., 0`` (default: all, from n-2).
@@ -221,6 +228,44 @@ class BackwardInduction:
         res.v0 = d0.mean_value
         res.holdings0 = d0.mean_holdings(self.spec.nhold)
         return res
+
+
+def feature_norms(paths: Paths, mode: str, world: int = 1) -> list:
+    """Per-date ``(fmu, fisd)`` tuples for :class:`DateData` (empty list = raw
+    inputs).  Moments are pooled over ranks (one host sync at build time);
+    a feature with (near-)zero spread at a date (e.g. S_0 on every path) keeps
+    unit scale so it maps to the constant 0."""
+    mode = (mode or "none").lower()
+    if mode == "none":
+        return []
+    if mode not in ("global", "date"):
+        raise ValueError(f"feature_norm must be none | global | date, got {mode!r}")
+    nd = paths.n_coarse - 1
+    nin = len(paths.features(0))
+    mom = torch.empty(nd, nin, 3, dtype=torch.float64, device=paths.S.device)
+    for t in range(nd):
+        for f, x in enumerate(paths.features(t)):
+            xd = x.double()
+            mom[t, f, 0] = xd.sum()
+            mom[t, f, 1] = (xd * xd).sum()
+            mom[t, f, 2] = float(xd.numel())
+    if world > 1:
+        from .parallel import dist as D
+
+        D.all_reduce_(mom)
+    m = mom.cpu().numpy()
+    if mode == "global":
+        m = np.broadcast_to(m.sum(axis=0, keepdims=True), m.shape)
+    out = []
+    for t in range(nd):
+        cnt = np.maximum(m[t, :, 2], 1.0)
+        mu = m[t, :, 0] / cnt
+        var = np.maximum(m[t, :, 1] / cnt - mu * mu, 0.0)
+        sd = np.sqrt(var)
+        ok = sd > 1e-6 * (np.abs(mu) + 1.0)
+        isd = np.where(ok, 1.0 / np.where(ok, sd, 1.0), 1.0)
+        out.append((tuple(float(v) for v in mu), tuple(float(v) for v in isd)))
+    return out
 
 
 def expected_value_trajectory(result: InductionResult, e_payoff: float, mu: float, r: float, dt: float) -> np.ndarray:

@@ -106,6 +106,23 @@ class DateData:
     target: torch.Tensor           # V_{t+1} [n_local]
     prices_now: list = field(default_factory=list)   # assets at t (for V_t)
     bond_now: float = 1.0
+    # input standardisation x' = (x - fmu) * fisd, fused into the kernels'
+    # feature loads (empty: identity = the reference's raw inputs)
+    fmu: tuple = ()
+    fisd: tuple = ()
+
+
+def _set_norm(d, data: DateData):
+    for i, (m, s) in enumerate(zip(data.fmu, data.fisd)):
+        d.fmu[i], d.fisd[i] = float(m), float(s)
+
+
+def _normalise(X: torch.Tensor, data: DateData) -> torch.Tensor:
+    if not data.fmu:
+        return X
+    mu = torch.tensor(data.fmu, dtype=X.dtype, device=X.device)
+    isd = torch.tensor(data.fisd, dtype=X.dtype, device=X.device)
+    return (X - mu) * isd
 
 
 def fit_seed(seed: int, date: int, net: int) -> int:
@@ -292,6 +309,7 @@ class HipBackend:
         d.stamps = self.stamps.data_ptr() if self.stamps is not None else None
         d.num_wgs = self.num_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
+        _set_norm(d, data)
         return d
 
     def fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig, seed: int, poll_every: int = 0):
@@ -430,6 +448,7 @@ class HipBackend:
         d.n_local = self.n_local
         d.num_wgs = self.eval_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
+        _set_norm(d, data)
         n.eval_(d, self.stream)
 
 
@@ -482,7 +501,7 @@ class TorchBackend:
         spec, dt = self.spec, self.dtype
         P = spec.nparams
         fit.copy_(fit_template(fcfg, self.device))
-        X = torch.stack([f.to(dt) for f in data.feats], dim=1)
+        X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
         pr = torch.stack([p.to(dt) for p in data.prices_next] +
                          [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
         y = data.target.to(dt)
@@ -583,7 +602,7 @@ class TorchBackend:
              v_out=None, hold_out=None, resid_out=None, pred1_out=None):
         spec, dt = self.spec, torch.float32
         P = spec.nparams
-        X = torch.stack([f.to(dt) for f in data.feats], dim=1)
+        X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
 
         def cw(t):
             cur = int(t[L.W_CUR].item())

@@ -81,6 +81,35 @@ class NetSpec:
         return np.concatenate([np.asarray(tensors[name], np.float32).reshape(-1) for name, _ in self.shapes()])
 
 
+def fold_input_norm(spec: NetSpec, w, fmu, fisd) -> np.ndarray:
+    """Weights on standardised inputs ``x' = (x - fmu) * fisd`` -> the same
+    function on raw inputs (first layer only): ``W1r = diag(fisd) W1``,
+    ``b1r = b1 - (fmu * fisd) @ W1``.  Saved models are always raw-input."""
+    if not len(fmu):
+        return np.asarray(w, np.float32).copy()
+    o, h, nin = spec.offsets, spec.hidden, spec.nin
+    w = np.asarray(w, np.float64).copy()
+    W1 = w[o["W1"]:o["b1"]].reshape(nin, h)
+    mu, isd = np.asarray(fmu, np.float64), np.asarray(fisd, np.float64)
+    b1 = w[o["b1"]:o["W2"]] - (mu * isd) @ W1
+    w[o["W1"]:o["b1"]] = (W1 * isd[:, None]).reshape(-1)
+    w[o["b1"]:o["W2"]] = b1
+    return w.astype(np.float32)
+
+
+def unfold_input_norm(spec: NetSpec, w, fmu, fisd) -> np.ndarray:
+    """Inverse of :func:`fold_input_norm` (raw-input weights -> standardised)."""
+    if not len(fmu):
+        return np.asarray(w, np.float32).copy()
+    o, h, nin = spec.offsets, spec.hidden, spec.nin
+    w = np.asarray(w, np.float64).copy()
+    W1r = w[o["W1"]:o["b1"]].reshape(nin, h)
+    mu, isd = np.asarray(fmu, np.float64), np.asarray(fisd, np.float64)
+    w[o["b1"]:o["W2"]] = w[o["b1"]:o["W2"]] + mu @ W1r
+    w[o["W1"]:o["b1"]] = (W1r / isd[:, None]).reshape(-1)
+    return w.astype(np.float32)
+
+
 PENSION = NetSpec(nin=3, hidden=8, nout=2, head=L.HEAD_FREE)
 EUROPEAN_REF = NetSpec(nin=1, hidden=8, nout=1, head=L.HEAD_COMPLEMENT,
                        layer_names=("LeakyReLU_1", "LeakyReLU_2", "Phi"))

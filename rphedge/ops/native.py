@@ -42,8 +42,13 @@ class TrainDesc(C.Structure):
         ("acc", VP), ("deterministic", C.c_int), ("stamps", VP),
         ("dp_world", C.c_int), ("dp_rank", C.c_int), ("dp_mbox", VP * 8), ("dp_flags", VP * 8),
         ("dp_counter", VP), ("dp_error", VP), ("mfma_fp32", C.c_int), ("lag", VP), ("variant", C.c_int),
-        ("fit_init", VP),
+        ("fit_init", VP), ("fmu", C.c_float * MAXIN), ("fisd", C.c_float * MAXIN),
     ]
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        for f in range(MAXIN):  # identity standardisation unless the backend sets one
+            self.fisd[f] = 1.0
 
 
 class EvalDesc(C.Structure):
@@ -54,8 +59,13 @@ class EvalDesc(C.Structure):
         ("bond_t", C.c_float), ("bond_t1", C.c_float), ("alpha", C.c_float), ("blend_c", C.c_float),
         ("hold_c", C.c_float),
         ("n_local", C.c_int), ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int),
-        ("head", C.c_int),
+        ("head", C.c_int), ("fmu", C.c_float * MAXIN), ("fisd", C.c_float * MAXIN),
     ]
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        for f in range(MAXIN):
+            self.fisd[f] = 1.0
 
 
 class SimDesc(C.Structure):
@@ -85,10 +95,10 @@ def _expected_layout() -> list[int]:
         T.counter.offset, T.grad_out.offset, T.bond.offset, T.inv_batch.offset, T.loss.offset, T.seed.offset,
         T.num_wgs.offset, T.head.offset, T.acc.offset, T.deterministic.offset, T.stamps.offset,
         T.dp_world.offset, T.dp_mbox.offset, T.dp_flags.offset, T.dp_counter.offset, T.dp_error.offset,
-        T.fit_init.offset,
+        T.fit_init.offset, T.fmu.offset, T.fisd.offset,
         C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
         E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
-        E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset,
+        E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset, E.fmu.offset, E.fisd.offset,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
         S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset,

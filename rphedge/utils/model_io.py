@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..engine import current_weights
+from ..models.hedge_mlp import fold_input_norm
 from ..ops import layout as L
 
 
@@ -56,12 +57,18 @@ def save_run(out_dir: str, run, res, save_values: bool = True):
                                            "head": spec.head, "alpha": spec.alpha,
                                            "layer_names": list(spec.layer_names)}}, f, indent=1, default=str)
     snap = res.induction.weights_snapshots
+    norms = getattr(run.induction, "norms", None) or []
     if snap is not None:
         s = snap.detach().cpu()
         for i in range(s.shape[0]):
-            tensors = {k: v for k, v in spec.unflatten(current_weights(spec, s[i, 0])).items()}
+            mu, isd = norms[i] if norms else ((), ())  # fold input standardisation: raw-input weights
+
+            def raw(k):
+                return spec.unflatten(fold_input_norm(spec, current_weights(spec, s[i, k]), mu, isd))
+
+            tensors = dict(raw(0))
             if run.cfg.train.q99:
-                tensors.update({"q99/" + k: v for k, v in spec.unflatten(current_weights(spec, s[i, 1])).items()})
+                tensors.update({"q99/" + k: v for k, v in raw(1).items()})
             _save_tensors(os.path.join(out_dir, f"weights_t{i:04d}.safetensors"), tensors)
     if save_values and res.induction.values is not None:
         np.save(os.path.join(out_dir, "values.npy"), res.induction.values.detach().cpu().numpy())

@@ -74,6 +74,7 @@ def test_saved_model_roundtrip(tmp_path):
     from rphedge.api import HedgeRun
     from rphedge.config import parse_params
     from rphedge.engine import current_weights
+    from rphedge.models.hedge_mlp import fold_input_norm, torch_forward, unfold_input_norm
     from rphedge.utils.model_io import load_date, save_run
 
     cfg = parse_params(_small())
@@ -84,8 +85,22 @@ def test_saved_model_roundtrip(tmp_path):
     assert "config.json" in files and "report.json" in files and "values.npy" in files
     assert sum(f.startswith("weights_t") for f in files) == run.paths.n_coarse - 1
     meta, spec, w, wq, vals = load_date(str(tmp_path), 0)
-    np.testing.assert_allclose(w, current_weights(spec, res.induction.weights_snapshots[0, 0]))
+    mu0, isd0 = run.induction.norms[0]
+    np.testing.assert_allclose(w, fold_input_norm(spec, current_weights(spec, res.induction.weights_snapshots[0, 0]),
+                                                  mu0, isd0), rtol=1e-6, atol=1e-7)
     assert wq is not None and vals.shape == (run.n_local,)
+    # saved weights are raw-input: same network outputs as the standardised
+    # weights on standardised features (last date, non-degenerate spread)
+    t = run.paths.n_coarse - 2
+    _, _, wt, _, _ = load_date(str(tmp_path), t)
+    mu, isd = run.induction.norms[t]
+    assert any(s != 1.0 for s in isd)
+    X = torch.stack(run.paths.features(t), dim=1).float()
+    wn = torch.from_numpy(current_weights(spec, res.induction.weights_snapshots[t, 0]))
+    raw = torch_forward(spec, torch.from_numpy(wt), X)
+    std = torch_forward(spec, wn, (X - torch.tensor(mu).float()) * torch.tensor(isd).float())
+    torch.testing.assert_close(raw, std, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(unfold_input_norm(spec, wt, mu, isd), wn.numpy(), rtol=1e-4, atol=1e-6)
     from safetensors.numpy import load_file
 
     t = load_file(str(tmp_path / "weights_t0000.safetensors"))

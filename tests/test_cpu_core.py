@@ -170,6 +170,39 @@ def test_launcher_rejects_bad_descriptors():
     d.alpha = 0.3
     with pytest.raises(RuntimeError, match="null state"):
         native.train_fit(d, 1, stream=0)
+    # dummy (never dereferenced) pointers past the null checks
+    d.wts = d.opt = d.fit = d.target = d.feat[0] = 4096
+    d.fisd[0] = 0.0
+    with pytest.raises(RuntimeError, match="standardisation"):
+        native.train_fit(d, 1, stream=0)
+    d.fisd[0], d.fmu[0] = 1.0, float("nan")
+    with pytest.raises(RuntimeError, match="standardisation"):
+        native.train_lag_fit(d, 1, stream=0)
+
+
+def test_feature_norms_modes():
+    """driver.feature_norms: per-date / pooled moments; degenerate spread
+    (every path at S_0 on date 0) keeps unit scale; parity forces raw."""
+    from rphedge.driver import feature_norms
+    from rphedge.ops import paths as P
+
+    g = P.Grid(1.0, 0.1, 0.1)
+    p = P.simulate_gbm(g, 1 << 12, 1.0, 0.08, 0.2, device="cpu", scheme="log")
+    assert feature_norms(p, "none") == []
+    nd = feature_norms(p, "date")
+    assert len(nd) == p.n_coarse - 1
+    assert nd[0] == ((pytest.approx(1.0),), (1.0,))
+    t = p.n_coarse - 2
+    x = p.features(t)[0].double()
+    assert nd[t][0][0] == pytest.approx(float(x.mean()), rel=1e-9)
+    assert nd[t][1][0] == pytest.approx(1.0 / float(x.std(unbiased=False)), rel=1e-6)
+    gl = feature_norms(p, "global")
+    assert all(v == gl[0] for v in gl) and gl[0][1][0] > 1.0
+    with pytest.raises(ValueError):
+        feature_norms(p, "bogus")
+    from rphedge.config import ParityFlags
+
+    assert ParityFlags.reference().raw_features and not ParityFlags().raw_features
 
 
 def test_keras_adam_matches_torch_optim_adam_cpu():

@@ -140,7 +140,7 @@ def test_mortality_statistics(dev):
     assert 110 < nT.std() < 160
 
 
-def _fit_pair(dev, spec, n, batch, epochs, loss, chunk_log2=0, lr=1e-2, **tkw):
+def _fit_pair(dev, spec, n, batch, epochs, loss, chunk_log2=0, lr=1e-2, norm=None, **tkw):
     from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
     from rphedge.models.hedge_mlp import init_weights
     from rphedge.ops import layout as L
@@ -157,6 +157,8 @@ def _fit_pair(dev, spec, n, batch, epochs, loss, chunk_log2=0, lr=1e-2, **tkw):
         be = be_cls(spec, n, tc, device=d)
         data = DateData(feats=[f.to(d) for f in feats], prices_next=[p.to(d) for p in prices], bond_next=1.02,
                         target=target.to(d), prices_now=[f.to(d) for f in feats[: spec.nhold - 1]], bond_now=1.0)
+        if norm is not None:
+            data.fmu, data.fisd = norm(spec.nin)
         w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
         be.fit(w, o, f, data, fc, seed=7)
         st = be.new_stats()
@@ -188,6 +190,28 @@ def test_train_step_matches_torch(dev, shape, mode):
     np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
     np.testing.assert_allclose(vg, vc, rtol=1e-3, atol=1e-4)
     np.testing.assert_allclose(rg, rc, rtol=1e-3, atol=1e-4)
+
+
+def _norm(nin):
+    return tuple(1.0 - 0.01 * f for f in range(nin)), tuple(7.0 + f for f in range(nin))
+
+
+@pytest.mark.parametrize("mode", ["lag", "ticket", "persistent"])
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (1, 32, 2, 0), (2, 32, 2, 0)])
+def test_feature_norm_matches_torch(dev, shape, mode):
+    """Input standardisation fused into the kernels' feature loads (train and
+    eval, narrow VALU and wide fp32-MFMA bodies) vs torch on standardised X."""
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    nin, h, nout, head = shape
+    spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 4096, 512, 2, L.LOSS_MSE,
+                                                                   step_mode=mode, norm=_norm, mfma_fp32=True)
+    np.testing.assert_allclose(wg, wc, rtol=2e-3, atol=3e-4)
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
+    np.testing.assert_allclose(vg, vc, rtol=1e-3, atol=2e-4)
+    np.testing.assert_allclose(rg, rc, rtol=1e-3, atol=2e-4)
 
 
 @pytest.mark.parametrize("det,split", [(False, False), (True, False), (False, True)])
