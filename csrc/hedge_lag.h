@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   constexpr int R = B::R;
   constexpr int NR = B::NR;
   constexpr int NREP = B::NREP;  // float-atomic replicas in use (contention vs prologue read traffic)
-  prefetch_kernarg<sizeof(TrainDesc) + 2 * sizeof(int) + sizeof(Perm)>();
+  const uint32_t kat = prefetch_kernarg_begin<sizeof(TrainDesc) + 2 * sizeof(int) + sizeof(Perm)>();
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ __attribute__((aligned(16))) float red[NR * 256 + 8];
@@ -318,6 +318,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   lag_load<P>(st, d, k == 0 ? nullptr : d.lag + (size_t)(k & 1) * LAG_FLOATS, fit0);
   typename B::Pre pre;
   B::load(d, s, perm, B::first(wid), lane, pre);
+  prefetch_kernarg_end(kat);
   const bool dp = d.dp_world > 1;
   const float* prev = d.acc + (size_t)((k + 2) % 3) * ACC_REPLICAS * R;  // accumulator of step k-1
   if (k > 0 && !dp) lag_sums<R, NREP>(prev, red);

@@ -31,33 +31,40 @@ namespace rph {
 // Without it the compiler's own kernarg loads form a chain of 4-6 dependent
 // scalar round trips (loads issued where each field is first needed, with
 // s_waitcnt between), which every workgroup pays at kernel start (~1 us of
-// an 11 us training step).  One asm block, so no SGPR is reused while a load
-// is still in flight.  Scalar LOADS only (the scalar cache is never written).
+// an 11 us training step).  Scalar LOADS only (the scalar cache is never
+// written).  All ten loads target ONE scratch SGPR (the values are never
+// read), so the register allocator has no reason to make the compiler's own
+// early kernarg loads wait first; the token keeps that SGPR reserved until
+// prefetch_kernarg_end, whose s_waitcnt (or any earlier compiler lgkmcnt(0)
+// wait) retires the loads.
 template <int BYTES>
-RPH_INLINE void prefetch_kernarg() {
+RPH_INLINE uint32_t prefetch_kernarg_begin() {
   static_assert(BYTES >= 4 && BYTES <= 640, "kernarg prefetch covers 1..10 lines");
 #define RPH_KO(i) ((i) * 64 < BYTES ? (i) * 64 : ((BYTES - 4) & ~3))
   auto kp = __builtin_amdgcn_kernarg_segment_ptr();
-  uint32_t a0, a1, a2, a3, a4, a5, a6, a7, a8, a9;
+  uint32_t t;
   asm volatile(
-      "s_load_dword %0, %10, %11\n\t"
-      "s_load_dword %1, %10, %12\n\t"
-      "s_load_dword %2, %10, %13\n\t"
-      "s_load_dword %3, %10, %14\n\t"
-      "s_load_dword %4, %10, %15\n\t"
-      "s_load_dword %5, %10, %16\n\t"
-      "s_load_dword %6, %10, %17\n\t"
-      "s_load_dword %7, %10, %18\n\t"
-      "s_load_dword %8, %10, %19\n\t"
-      "s_load_dword %9, %10, %20\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&s"(a0), "=&s"(a1), "=&s"(a2), "=&s"(a3), "=&s"(a4), "=&s"(a5), "=&s"(a6), "=&s"(a7), "=&s"(a8),
-        "=&s"(a9)
+      "s_load_dword %0, %1, %2\n\t"
+      "s_load_dword %0, %1, %3\n\t"
+      "s_load_dword %0, %1, %4\n\t"
+      "s_load_dword %0, %1, %5\n\t"
+      "s_load_dword %0, %1, %6\n\t"
+      "s_load_dword %0, %1, %7\n\t"
+      "s_load_dword %0, %1, %8\n\t"
+      "s_load_dword %0, %1, %9\n\t"
+      "s_load_dword %0, %1, %10\n\t"
+      "s_load_dword %0, %1, %11"
+      : "=&s"(t)
       : "s"(kp), "i"(RPH_KO(0)), "i"(RPH_KO(1)), "i"(RPH_KO(2)), "i"(RPH_KO(3)), "i"(RPH_KO(4)),
         "i"(RPH_KO(5)), "i"(RPH_KO(6)), "i"(RPH_KO(7)), "i"(RPH_KO(8)), "i"(RPH_KO(9)));
 #undef RPH_KO
-  (void)a0; (void)a1; (void)a2; (void)a3; (void)a4; (void)a5; (void)a6; (void)a7; (void)a8; (void)a9;
+  return t;
 }
+
+RPH_INLINE void prefetch_kernarg_end(uint32_t t) { asm volatile("s_waitcnt lgkmcnt(0)" : : "s"(t)); }
+
+template <int BYTES>
+RPH_INLINE void prefetch_kernarg() { prefetch_kernarg_end(prefetch_kernarg_begin<BYTES>()); }
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG (Salmon et al. 2011).  Used for binomial
