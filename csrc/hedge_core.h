@@ -302,12 +302,18 @@ constexpr int WIDE_NREP = RPH_WIDE_NREP;
 
 // sum of the first NREP (<= ACC_REPLICAS, power of two) float-atomic replicas
 // of packet entry i, pairwise in fixed order
-template <int NREP = ACC_REPLICAS>
+// AGENT: agent-scope loads (L2 bypass) - needed inside the persistent kernel,
+// where the replicas were written by the same launch.  Across a kernel
+// boundary (lagged schedule: step k reads step k-1's accumulator) the
+// boundary's acquire already invalidated the non-coherent L2, so plain loads
+// are correct and let the ~32 workgroups of an XCD share one L2 fill instead
+// of each fetching the packet from the memory side.
+template <int NREP = ACC_REPLICAS, bool AGENT = true>
 RPH_INLINE float sum_replicas(const float* buf, int R, int i) {
   static_assert(NREP >= 1 && NREP <= ACC_REPLICAS && (NREP & (NREP - 1)) == 0, "replicas: power of two <= 8");
   float rr[NREP];
 #pragma unroll
-  for (int rp = 0; rp < NREP; ++rp) rr[rp] = ld_agent(buf + rp * R + i);
+  for (int rp = 0; rp < NREP; ++rp) rr[rp] = AGENT ? ld_agent(buf + rp * R + i) : buf[rp * R + i];
 #pragma unroll
   for (int w = NREP / 2; w >= 1; w /= 2)
 #pragma unroll

@@ -286,9 +286,12 @@ RPH_INLINE int lag_apply(LagState<P>& st, const float* red, const TrainDesc& d, 
 }
 
 // summed packet of accumulator `buf` (NREP replicas) into LDS red[0..R)
-template <int R, int NREP>
+// PLAIN: cached loads of the previous launch's accumulator (see sum_replicas);
+// measured faster for the 128-float packets of the 8-unit nets, slower for the
+// 1280-float packets of the 32-unit nets (profiles/stamp_r1q_acc_loads.jsonl)
+template <int R, int NREP, bool PLAIN = false>
 RPH_INLINE void lag_sums(const float* buf, float* red) {
-  for (int i = threadIdx.x; i < R; i += 256) red[i] = sum_replicas<NREP>(buf, R, i);
+  for (int i = threadIdx.x; i < R; i += 256) red[i] = sum_replicas<NREP, !PLAIN>(buf, R, i);
 }
 
 template <class B>
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   prefetch_kernarg_end(kat);
   const bool dp = d.dp_world > 1;
   const float* prev = d.acc + (size_t)((k + 2) % 3) * ACC_REPLICAS * R;  // accumulator of step k-1
-  if (k > 0 && !dp) lag_sums<R, NREP>(prev, red);
+  if (k > 0 && !dp) lag_sums<R, NREP, B::ACC_PLAIN>(prev, red);
   if (stopped0 != 0.f) return;  // early-stopped fit: the remaining steps are no-ops
   __syncthreads();
   const bool w0 = blockIdx.x == 0;

@@ -50,6 +50,7 @@ struct NarrowBody {
   static constexpr int R = S::R;
   static constexpr int NR = (R + 255) / 256;  // packet entries per thread (1)
   static constexpr int NREP = ACC_REPLICAS;   // lagged schedule: float-atomic replicas
+  static constexpr bool ACC_PLAIN = true;      // lagged prologue: cached (L2-shared) accumulator loads
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
   struct Frags {};  // (weights are read from LDS)

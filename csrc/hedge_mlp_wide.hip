@@ -287,6 +287,7 @@ struct WideBody {
   static constexpr int R = S::R;  // packet width, multiple of 256
   static constexpr int NR = R / 256;
   static constexpr int NREP = WIDE_NREP;  // lagged schedule: float-atomic replicas
+  static constexpr bool ACC_PLAIN = false;  // lagged prologue: agent-scope accumulator loads (faster here)
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int RV = G::RV;
   static constexpr int IMG_BYTES = F32 ? 2 * WH * IMG_PITCH32 * 4 : 2 * WH * TR_PITCH;
