@@ -1,12 +1,27 @@
 """Training / evaluation engine: device-resident state + two backends.
 
-* :class:`HipBackend` — the MI355X path.  One fused HIP kernel per optimizer
-  step (``k_hedge_train_step``: forward + loss + backward + deterministic
-  gradient reduction + Keras-Adam + EarlyStopping/LR bookkeeping), optional
-  RCCL all-reduce of the 512-byte gradient packet on the same stream for DP,
-  and the ``k_hedge_eval`` epilogue.  Nothing synchronises with the host, so a
-  whole backward-induction run can be captured into ONE hipGraph
-  (:mod:`rphedge.driver`).
+* :class:`HipBackend` — the MI355X path.  Every optimizer step runs the same
+  fused body (forward + loss + backward + in-wave reduce-scatter + workgroup
+  sum: ``NarrowBody`` VALU for the 8-unit nets, ``WideBody`` MFMA for the
+  32-unit nets) under one of three schedules (:attr:`TrainConfig.step_mode`,
+  resolved by :meth:`HipBackend.step_mode`):
+
+  - ``lag`` — one ``k_hedge_step_lag`` launch per step; every workgroup
+    applies the Keras-Adam / LR / EarlyStopping update of the PREVIOUS step
+    redundantly in its prologue from float-atomic accumulators, so the kernel
+    boundary is the only global synchronisation (large grids; data parallel
+    with the in-kernel xGMI exchange);
+  - ``persistent`` — one ``k_hedge_fit`` launch per Keras fit with an
+    in-kernel barrier (small grids, e.g. the reference's batch 512);
+  - ``ticket`` — ``k_hedge_train_step`` with a last-arriver update
+    (deterministic slab reduction, ranks sharing a GPU, RCCL all-reduce of the
+    gradient packet on the compute stream between step and update kernels).
+
+  Whole fits are launched from the native runtime (``rph_train_*_fit``), the
+  ``k_hedge_eval`` epilogue produces values / holdings / residuals / stats, and
+  nothing synchronises with the host, so a whole backward-induction run is
+  captured into ONE hipGraph (:mod:`rphedge.driver`).  Input standardisation
+  (:attr:`DateData.fmu` / ``fisd``) is fused into the feature loads.
 * :class:`TorchBackend` — CPU (or any torch device) reference with identical
   semantics: same chunk permutation (Philox), same Adam formula, same early
   stopping; multi-process via ``torch.distributed`` (gloo).  It is the oracle
