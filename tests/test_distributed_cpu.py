@@ -85,3 +85,46 @@ def test_shard_ranges():
     assert [shard(1 << 20, 8, r) for r in (0, 7)] == [(0, 131072), (917504, 131072)]
     with pytest.raises(ValueError):
         shard(10, 3, 0)
+
+
+def _dying_worker(rank, world, port, out):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import time
+
+    from rphedge.api import HedgeRun
+    from rphedge.parallel import dist as D
+
+    di = D.init(device="cpu", timeout_s=20.0)
+    if rank == 1:
+        os._exit(3)  # fault injection: a rank dies before the first collective of the run
+    t0 = time.time()
+    try:
+        HedgeRun(_cfg(), dist_info=di).run()
+        status = "completed"
+    except Exception as e:  # gloo: peer closed / timeout
+        status = "raised: " + type(e).__name__
+    with open(out, "w") as f:
+        json.dump({"status": status, "elapsed": time.time() - t0}, f)
+    os._exit(0)  # (the process group cannot be shut down cleanly without its peer)
+
+
+def test_dead_rank_errors_out_cleanly():
+    """SURVEY §5.3 fault injection: a rank killed before a collective makes the
+    surviving rank raise (bounded by the process-group timeout) instead of
+    hanging or returning a silently wrong result."""
+    world, port = 2, _free_port()
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "dead.json")
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=_dying_worker, args=(r, world, port, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+        assert procs[1].exitcode == 3
+        assert procs[0].exitcode == 0
+        res = json.load(open(out))
+    assert res["status"].startswith("raised"), res
+    assert res["elapsed"] < 60
