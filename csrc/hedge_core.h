@@ -295,6 +295,12 @@ constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contentio
 // lagged schedule, 32-unit nets: every workgroup re-reads the whole packet of
 // the previous step in its prologue, R = 1280+ floats x replicas — fewer
 // replicas trade atomic contention for prologue read traffic
+// lagged schedule: the narrow nets use RPH_NARROW_NREP of the LAG_SLOTS
+// accumulator replica rows (rph_types.h)
+#ifndef RPH_NARROW_NREP
+#define RPH_NARROW_NREP 16
+#endif
+constexpr int NARROW_NREP = RPH_NARROW_NREP;
 #ifndef RPH_WIDE_NREP
 #define RPH_WIDE_NREP 8
 #endif
@@ -310,7 +316,7 @@ constexpr int WIDE_NREP = RPH_WIDE_NREP;
 // of each fetching the packet from the memory side.
 template <int NREP = ACC_REPLICAS, bool AGENT = true>
 RPH_INLINE float sum_replicas(const float* buf, int R, int i) {
-  static_assert(NREP >= 1 && NREP <= ACC_REPLICAS && (NREP & (NREP - 1)) == 0, "replicas: power of two <= 8");
+  static_assert(NREP >= 1 && NREP <= LAG_SLOTS && (NREP & (NREP - 1)) == 0, "replicas: power of two <= 16");
   float rr[NREP];
 #pragma unroll
   for (int rp = 0; rp < NREP; ++rp) rr[rp] = AGENT ? ld_agent(buf + rp * R + i) : buf[rp * R + i];

@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   B::load(d, s, perm, B::first(wid), lane, pre);
   prefetch_kernarg_end(kat);
   const bool dp = d.dp_world > 1;
-  const float* prev = d.acc + (size_t)((k + 2) % 3) * ACC_REPLICAS * R;  // accumulator of step k-1
+  const float* prev = d.acc + (size_t)((k + 2) % 3) * LAG_SLOTS * R;  // accumulator of step k-1
   if (k > 0 && !dp) lag_sums<R, NREP, B::ACC_PLAIN>(prev, red);
   if (stopped0 != 0.f) return;  // early-stopped fit: the remaining steps are no-ops
   __syncthreads();
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
     }
     // persist the updated state and re-arm the accumulator of step k+1 now, so
     // no optimizer state stays live (in registers) across the partial
-    float* z = d.acc + (size_t)((k + 1) % 3) * ACC_REPLICAS * R;
+    float* z = d.acc + (size_t)((k + 1) % 3) * LAG_SLOTS * R;
     for (int i = tid; i < NREP * R; i += 256) st_agent(z + i, 0.f);
     lag_store<P>(st, d.lag + (size_t)((k + 1) & 1) * LAG_FLOATS);
   }
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_hedge_step_lag(const
   RPH_STAMP(3);
 
   // ---- epilogue: fire-and-forget adds ----------------------------------------------
-  float* buf = d.acc + (size_t)(k % 3) * ACC_REPLICAS * R;
+  float* buf = d.acc + (size_t)(k % 3) * LAG_SLOTS * R;
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int i = tid + 256 * j;
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, c
   int bad = 0;
   if (run) {
     lag_load<P>(st, d, d.lag + (size_t)(K & 1) * LAG_FLOATS, d.fit);
-    const float* prev = d.acc + (size_t)((K - 1) % 3) * ACC_REPLICAS * R;
+    const float* prev = d.acc + (size_t)((K - 1) % 3) * LAG_SLOTS * R;
     if (d.dp_world > 1) {
       bad = lag_dp_exchange<R, NREP>(d, __float_as_uint(st.sc[LG_SEQ]) + (uint32_t)K, prev, red, true);
     } else {
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, c
   // leave all three accumulators zeroed for the next fit (its kernel 0 adds
   // into accumulator 0 without a memset); every lag kernel of this fit is done
   __syncthreads();
-  for (int i = threadIdx.x; i < 3 * ACC_REPLICAS * R; i += 256) st_agent(d.acc + i, 0.f);
+  for (int i = threadIdx.x; i < 3 * LAG_SLOTS * R; i += 256) st_agent(d.acc + i, 0.f);
   if (!run || bad) return;
   const int S = d.steps_per_epoch;
   const int kp = K - 1, ep = kp / S;

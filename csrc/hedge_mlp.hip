@@ -49,7 +49,7 @@ struct NarrowBody {
   static constexpr int P = S::P;
   static constexpr int R = S::R;
   static constexpr int NR = (R + 255) / 256;  // packet entries per thread (1)
-  static constexpr int NREP = ACC_REPLICAS;   // lagged schedule: float-atomic replicas
+  static constexpr int NREP = NARROW_NREP;    // lagged schedule: float-atomic replicas
   static constexpr bool ACC_PLAIN = true;      // lagged prologue: cached (L2-shared) accumulator loads
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
@@ -565,7 +565,7 @@ extern "C" int rph_train_lag_finalize(const TrainDesc* d, int K, void* stream) {
 #define X(A, B, C, E)                                                                        \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
     using S = NetShape<A, B, C, E>;                                                          \
-    hipLaunchKernelGGL((k_hedge_lag_finalize<S::P, S::R, ACC_REPLICAS>), dim3(1), dim3(256), 0, s, *d, K); \
+    hipLaunchKernelGGL((k_hedge_lag_finalize<S::P, S::R, NARROW_NREP>), dim3(1), dim3(256), 0, s, *d, K); \
     return (int)hipGetLastError();                                                           \
   }
   RPH_SHAPES(X)

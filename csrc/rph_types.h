@@ -14,6 +14,7 @@ constexpr int MAXIN = 8;       // max input features
 constexpr int MAXHOLD = 8;     // max hedging instruments (assets + bond)
 constexpr int MAXHIST = 1024;  // per-fit epoch-loss history
 constexpr int EVAL_NSTAT = 32; // doubles per workgroup in the eval stats slab
+constexpr int LAG_SLOTS = 16;  // lagged schedule: replica rows per rotating accumulator buffer
 
 enum Head : int { HEAD_FREE = 0, HEAD_COMPLEMENT = 1 };
 enum Loss : int { LOSS_MSE = 0, LOSS_PINBALL = 1 };

@@ -66,6 +66,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),
       OFF(SimDesc, inv_norm), OFF(SimDesc, v0), OFF(SimDesc, rho), OFF(SimDesc, l0), OFF(SimDesc, n0),
       OFF(SimDesc, seed), OFF(SimDesc, out), OFF(SimDesc, final2_out),
+      (long long)LAG_SLOTS,
   };
   const int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < cap; ++i) out[i] = v[i];

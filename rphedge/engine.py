@@ -253,7 +253,7 @@ class HipBackend:
         self.grad = torch.zeros(self.R, dtype=torch.float32, device=dev)
         self.acc = torch.zeros(8, self.R, dtype=torch.float32, device=dev)
         # persistent per-fit kernel: 3 rotating accumulator buffers + [arrivals, error] counters
-        self.acc_fit = torch.zeros(3, 8, self.R, dtype=torch.float32, device=dev)
+        self.acc_fit = torch.zeros(3, L.LAG_SLOTS, self.R, dtype=torch.float32, device=dev)
         self.fit_ctl = torch.zeros(4, dtype=torch.int32, device=dev)
         self.lag = torch.zeros(2, L.LAG_FLOATS, dtype=torch.float32, device=dev)
         self._acc_clean = False  # acc_fit known zero (set by a lagged fit's finalize)

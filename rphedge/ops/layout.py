@@ -10,6 +10,8 @@ NETW_FLOATS = 2 * PMAX + 4
 
 # lagged-update state slot (csrc/hedge_lag.h): w, m, v [PMAX] + 16 scalars
 LAG_FLOATS = 3 * PMAX + 16
+# lagged-update accumulators: 3 rotating buffers x LAG_SLOTS replica rows x R
+LAG_SLOTS = 16
 W_CUR = 2 * PMAX
 
 # OptState: m[PMAX], v[PMAX], t, lr, beta1, beta2, eps, nan_steps, pad0, pad1

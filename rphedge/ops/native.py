@@ -102,6 +102,7 @@ def _expected_layout() -> list[int]:
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
         S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset,
+        L.LAG_SLOTS,
     ]
 
 
