@@ -88,7 +88,7 @@ class TrainConfig:
     beta2: float = 0.999
     eps: float = 1e-7              # Keras epsilon
     max_wgs: int = 0               # workgroups per training step; 0 = auto: 256 (one per CU), 512 for
-                                   # the 32-unit bf16 nets with <= 2 inputs (2 resident waves/SIMD:
+                                   # the 1-input 32-unit bf16 net (2 resident waves/SIMD:
                                    # the MFMA tile chain is latency-bound, profiles/sweep_r1n_wide_wgs.jsonl)
     paths_per_thread: int = 1      # target work per thread per step
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
@@ -245,7 +245,10 @@ class HipBackend:
         work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
         mw = int(tcfg.max_wgs)
         if mw <= 0:
-            mw = 512 if (spec.hidden == 32 and not tcfg.mfma_fp32 and spec.nin <= 2) else 256
+            # 512 workgroups = 2 per CU only where two fit (the 1-input bf16
+            # net); the wider-input nets run 1 per CU, so a 512 grid starts in
+            # two waves (+15 us start spread, profiles/stamp_r1s_wide_wgs.jsonl)
+            mw = 512 if (spec.hidden == 32 and not tcfg.mfma_fp32 and spec.nin == 1) else 256
         self.num_wgs = int(max(1, min(mw, work)))
         dev = self.device
         self.slab = torch.zeros(self.num_wgs, self.R, dtype=torch.float32, device=dev)
