@@ -330,10 +330,13 @@ __global__ __launch_bounds__(256) void k_hedge_train_step(const TrainDesc d, con
 //   residual  = V_{t+1} - h . p_{t+1}       ("VaR", RP:120; Q24)
 // Per-workgroup fp64 statistics go to a [num_wgs][EVAL_NSTAT] slab.
 // ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD>
+// PA: the traded-asset prices at t ARE the leading features (GBM / basket:
+// same tensors, detected by pointer on the host) - loaded once per path.
+template <int NIN, int H, int NO, int HEAD, bool PA>
 __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
   using S = NetShape<NIN, H, NO, HEAD>;
   constexpr int NHOLD = S::NHOLD;
+  static_assert(!PA || NIN >= NHOLD - 1, "price alias needs a feature per traded asset");
   prefetch_kernarg<sizeof(EvalDesc)>();
   RPH_DASSERT(d.n_local > 0 && d.num_wgs == (int)gridDim.x && d.wa != nullptr && d.stats != nullptr);
   __shared__ double sst[4][EVAL_NSTAT];
@@ -377,7 +380,8 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
     for (int f = 0; f < NIN; ++f) in.x[f] = d.feat[f][pp];  // raw (ring): standardised where consumed
 #pragma unroll
     for (int k = 0; k < NHOLD - 1; ++k) {
-      in.pt[k] = d.price_t[k][pp];
+      if constexpr (PA) in.pt[k] = in.x[PA ? k : 0];  // (raw feature = raw price)
+      else in.pt[k] = d.price_t[k][pp];
       in.pt1[k] = has1 ? d.price_t1[k][pp] : 0.f;
     }
     in.tgt = (has1 && d.target) ? d.target[pp] : 0.f;
@@ -629,10 +633,19 @@ extern "C" int rph_eval(const EvalDesc* d, void* stream) {
   for (int f = 0; f < d->nin; ++f)
     if (!d->feat[f]) return rph_report("rph_eval", "null feature pointer");
   hipStream_t s = (hipStream_t)stream;
-#define X(A, B, C, E)                                                                        \
-  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                               \
-    hipLaunchKernelGGL((k_hedge_eval<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d);  \
-    return (int)hipGetLastError();                                                           \
+  const int nhold = d->head == HEAD_COMPLEMENT ? 2 : d->nout;
+  bool alias = d->nin >= nhold - 1;
+  for (int k = 0; alias && k < nhold - 1; ++k) alias = d->price_t[k] == d->feat[k];
+#define X(A, B, C, E)                                                                          \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                 \
+    if constexpr (A >= NetShape<A, B, C, E>::NHOLD - 1) {                                     \
+      if (alias) {                                                                             \
+        hipLaunchKernelGGL((k_hedge_eval<A, B, C, E, true>), dim3(d->num_wgs), dim3(256), 0, s, *d); \
+        return (int)hipGetLastError();                                                         \
+      }                                                                                        \
+    }                                                                                          \
+    hipLaunchKernelGGL((k_hedge_eval<A, B, C, E, false>), dim3(d->num_wgs), dim3(256), 0, s, *d); \
+    return (int)hipGetLastError();                                                             \
   }
   RPH_SHAPES(X)
   RPH_WIDE_SHAPES(X)

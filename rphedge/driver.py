@@ -243,12 +243,13 @@ def feature_norms(paths: Paths, mode: str, world: int = 1) -> list:
     nd = paths.n_coarse - 1
     nin = len(paths.features(0))
     mom = torch.empty(nd, nin, 3, dtype=torch.float64, device=paths.S.device)
-    for t in range(nd):
-        for f, x in enumerate(paths.features(t)):
-            xd = x.double()
-            mom[t, f, 0] = xd.sum()
-            mom[t, f, 1] = (xd * xd).sum()
-            mom[t, f, 2] = float(xd.numel())
+    for t in range(nd):  # one stack + one Welford var_mean launch per date
+        X = torch.stack(paths.features(t))
+        var, mean = torch.var_mean(X, dim=1, unbiased=False)
+        cnt = float(X.shape[1])
+        mom[t, :, 0] = mean.double() * cnt
+        mom[t, :, 1] = (var.double() + mean.double() ** 2) * cnt
+        mom[t, :, 2] = cnt
     if world > 1:
         from .parallel import dist as D
 

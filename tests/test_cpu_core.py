@@ -194,7 +194,7 @@ def test_feature_norms_modes():
     assert nd[0] == ((pytest.approx(1.0),), (1.0,))
     t = p.n_coarse - 2
     x = p.features(t)[0].double()
-    assert nd[t][0][0] == pytest.approx(float(x.mean()), rel=1e-9)
+    assert nd[t][0][0] == pytest.approx(float(x.mean()), rel=1e-6)  # (fp32 Welford)
     assert nd[t][1][0] == pytest.approx(1.0 / float(x.std(unbiased=False)), rel=1e-6)
     gl = feature_norms(p, "global")
     assert all(v == gl[0] for v in gl) and gl[0][1][0] > 1.0
