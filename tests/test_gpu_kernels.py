@@ -192,6 +192,25 @@ def test_train_step_matches_torch(dev, shape, mode):
     np.testing.assert_allclose(rg, rc, rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (5, 8, 6, 0)])
+def test_narrow_lag_variants_match_torch(dev, shape, variant):
+    """Every narrow lagged-step variant (weights in registers / re-read from
+    LDS, 1 or 2 waves per SIMD, prefetch depth 1 or 3) vs torch, on a grid of
+    several workgroups (batch 2^13 -> 32 WGs, 512 WGs requested)."""
+    from rphedge.models.hedge_mlp import NetSpec
+    from rphedge.ops import layout as L
+
+    nin, h, nout, head = shape
+    spec = NetSpec(nin=nin, hidden=h, nout=nout, head=head)
+    (wc, oc, fc, vc, rc, sc), (wg, og, fg, vg, rg, sg) = _fit_pair(dev, spec, 1 << 14, 1 << 13, 2, L.LOSS_MSE,
+                                                                   chunk_log2=6, step_mode="lag", variant=variant,
+                                                                   max_wgs=512)
+    np.testing.assert_allclose(wg, wc, rtol=2e-3, atol=2e-4)
+    np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
+    np.testing.assert_allclose(vg, vc, rtol=1e-3, atol=1e-4)
+
+
 def _norm(nin):
     return tuple(1.0 - 0.01 * f for f in range(nin)), tuple(7.0 + f for f in range(nin))
 
