@@ -59,7 +59,7 @@ PRESETS = {
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
-                    batch_log2=18, lr=2e-2, lr_rest=4e-3,
+                    batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
                     label="European call, 252-step GBM, 2M paths per GPU (16M at 8 GPUs)"),
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
