@@ -96,8 +96,10 @@ RPH_INLINE uint32_t perm_path(const Perm& perm, uint32_t j, int chunk_log2, int 
 template <int NIN, int H, int NO, int HEAD>
 RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], float alpha,
                             float (&z1)[H], float (&a1)[H], float (&z2)[H], float (&a2)[H],
-                            float (&hold)[NetShape<NIN, H, NO, HEAD>::NHOLD]) {
+                            float (&hold)[NetShape<NIN, H, NO, HEAD>::NHOLD],
+                            const float* __restrict__ W2 = nullptr /* source of the W2 block (default W) */) {
   using S = NetShape<NIN, H, NO, HEAD>;
+  if (W2 == nullptr) W2 = W;
 #pragma unroll
   for (int j = 0; j < H; ++j) {
     float acc = W[S::OB1 + j];
@@ -110,7 +112,7 @@ RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], 
   for (int j = 0; j < H; ++j) {
     float acc = W[S::OB2 + j];
 #pragma unroll
-    for (int i = 0; i < H; ++i) acc = fmaf(a1[i], W[S::OW2 + i * H + j], acc);
+    for (int i = 0; i < H; ++i) acc = fmaf(a1[i], W2[S::OW2 + i * H + j], acc);
     z2[j] = acc;
     a2[j] = lrelu(acc, alpha);
   }

@@ -34,7 +34,7 @@ namespace rph {
 // (the reference's 8-unit nets).  Used by the per-step kernel below and by the
 // persistent per-fit kernel (hedge_fit.h).
 // ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD, int WPE = 1, int PFD = 1, bool LDSW = (WPE > 1)>
+template <int NIN, int H, int NO, int HEAD, int WPE = 1, int PFD = 1, bool LDSW = (WPE > 1), bool HYB = false>
 struct NarrowBody {
   static constexpr int WAVES_PER_SIMD = WPE;
   // LDSW: weights are re-read from LDS every path iteration instead of being
@@ -100,14 +100,19 @@ struct NarrowBody {
       // WPE 1: the loop-invariant LDS weights are hoisted into registers (AGPR
       // overflow); WPE 2: an opaque zero offset makes every iteration re-read
       // them as LDS broadcasts, so the kernel fits 256 registers = 2 waves/SIMD
+      // HYB: only the W2 block (the most-used weights, forward and backward)
+      // is hoisted into registers, the rest is re-read from LDS, so the
+      // hoisted weights fit in VGPRs instead of overflowing to AGPRs (each
+      // AGPR-resident weight costs a v_accvgpr_read per use)
       const float* __restrict__ Wi = W;
-      if constexpr (LDSW) {
+      if constexpr (LDSW || HYB) {
         // opaque 16-byte-aligned base: every use is a ds_read_b128 broadcast
         // off ONE address register with an immediate offset
         uint32_t z = 0;
         asm volatile("" : "+v"(z));
         Wi = (const float*)__builtin_assume_aligned(W + (z & ~3u), 16);
       }
+      const float* __restrict__ W2s = HYB ? W : Wi;
       float x[NIN], pr[NHOLD];
 #pragma unroll
       for (int f = 0; f < NIN; ++f) x[f] = (q[0].x[f] - d.fmu[f]) * d.fisd[f];
@@ -120,7 +125,7 @@ struct NarrowBody {
       if (j0 + PF * stride < d.batch) load(d, step, perm, j0 + PF * stride, lane, q[PF - 1]);  // software pipelining
 
       float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
-      net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold);
+      net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold, W2s);
       float V = 0.f;
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
@@ -161,7 +166,7 @@ struct NarrowBody {
 #pragma unroll
         for (int j = 0; j < H; ++j) {
           g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
-          da = fmaf(Wi[S::OW2 + i * H + j], dz2[j], da);
+          da = fmaf(W2s[S::OW2 + i * H + j], dz2[j], da);
         }
         const float dz1 = da * lrelu_d(z1[i], alpha);
         g[S::OB1 + i] += dz1;
@@ -551,6 +556,8 @@ extern "C" int rph_train_lag_step(const TrainDesc* d, int k, int epoch, void* st
                                  s, *d, k, epoch, perm); break;                                        \
       case 4: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 1, 1, true>>), dim3(d->num_wgs), dim3(256), \
                                  0, s, *d, k, epoch, perm); break;                                     \
+      case 5: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E, 1, 1, false, true>>), dim3(d->num_wgs), \
+                                 dim3(256), 0, s, *d, k, epoch, perm); break;                          \
       default: hipLaunchKernelGGL((k_hedge_step_lag<NarrowBody<A, B, C, E>>), dim3(d->num_wgs), dim3(256), 0, s, \
                                   *d, k, epoch, perm);                                                 \
     }                                                                                                 \

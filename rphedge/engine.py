@@ -241,7 +241,13 @@ class HipBackend:
         self.P, self.R = native.net_nparams(spec.nin, spec.hidden, spec.nout, spec.head)
         assert self.P == spec.nparams
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
-        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (4 if self.R > 128 else 0)
+        # narrow-body variant (csrc/hedge_mlp.hip launcher): 5 = W2 hoisted in
+        # VGPRs + the rest from LDS, 2 waves/SIMD at 512 WGs (1-2 input nets:
+        # 9.83 -> 9.64 / 10.05 -> 9.69 us per 2^18 step; the 3-input net is
+        # slower that way), 4 = all weights from LDS (256-wide packets),
+        # 0 = all weights hoisted (profiles/stamp_r1u_hybrid.jsonl)
+        hyb = spec.hidden == 8 and spec.nin <= 2 and self.R <= 128
+        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (5 if hyb else 4 if self.R > 128 else 0)
         work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
         mw = int(tcfg.max_wgs)
         if mw <= 0:
@@ -249,6 +255,9 @@ class HipBackend:
             # net); the wider-input nets run 1 per CU, so a 512 grid starts in
             # two waves (+15 us start spread, profiles/stamp_r1s_wide_wgs.jsonl)
             mw = 512 if (spec.hidden == 32 and not tcfg.mfma_fp32 and spec.nin == 1) else 256
+            if (self.variant == 5 and tcfg.step_mode in ("auto", "lag") and not tcfg.deterministic
+                    and not tcfg.split_update):
+                mw = 512  # lagged steps: 2 workgroups (2 waves/SIMD) per CU
         self.num_wgs = int(max(1, min(mw, work)))
         dev = self.device
         self.slab = torch.zeros(self.num_wgs, self.R, dtype=torch.float32, device=dev)

@@ -192,7 +192,7 @@ def test_train_step_matches_torch(dev, shape, mode):
     np.testing.assert_allclose(rg, rc, rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (5, 8, 6, 0)])
 def test_narrow_lag_variants_match_torch(dev, shape, variant):
     """Every narrow lagged-step variant (weights in registers / re-read from
