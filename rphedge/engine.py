@@ -246,7 +246,9 @@ class HipBackend:
         # 9.83 -> 9.64 / 10.05 -> 9.69 us per 2^18 step; the 3-input net is
         # slower that way), 4 = all weights from LDS (256-wide packets),
         # 0 = all weights hoisted (profiles/stamp_r1u_hybrid.jsonl)
-        hyb = spec.hidden == 8 and spec.nin <= 2 and self.R <= 128
+        # (one rank only: with the in-kernel xGMI exchange every workgroup polls
+        # the mailbox, so data-parallel runs keep the 256-workgroup grid)
+        hyb = spec.hidden == 8 and spec.nin <= 2 and self.R <= 128 and world == 1
         self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (5 if hyb else 4 if self.R > 128 else 0)
         work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
         mw = int(tcfg.max_wgs)
