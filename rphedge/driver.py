@@ -242,14 +242,18 @@ def feature_norms(paths: Paths, mode: str, world: int = 1) -> list:
         raise ValueError(f"feature_norm must be none | global | date, got {mode!r}")
     nd = paths.n_coarse - 1
     nin = len(paths.features(0))
-    mom = torch.empty(nd, nin, 3, dtype=torch.float64, device=paths.S.device)
-    for t in range(nd):  # one stack + one Welford var_mean launch per date
-        X = torch.stack(paths.features(t))
-        var, mean = torch.var_mean(X, dim=1, unbiased=False)
-        cnt = float(X.shape[1])
-        mom[t, :, 0] = mean.double() * cnt
-        mom[t, :, 1] = (var.double() + mean.double() ** 2) * cnt
-        mom[t, :, 2] = cnt
+    # per (date, feature): fp64-accumulated full sums of x and x*x (fast full
+    # reductions on MI355X: torch.var_mean ran ~10x slower, a [nin, n] dim-1
+    # reduction ~100x; fp64 accumulation keeps the pooled DP moments equal to
+    # the one-process ones), gathered with two stacks
+    s1, s2 = [], []
+    for t in range(nd):
+        for x in paths.features(t):
+            s1.append(x.sum(dtype=torch.float64))
+            s2.append((x * x).sum(dtype=torch.float64))
+    cnt = float(paths.features(0)[0].numel())
+    mom = torch.stack([torch.stack(s1).view(nd, nin), torch.stack(s2).double().view(nd, nin),
+                       torch.full((nd, nin), cnt, dtype=torch.float64, device=paths.S.device)], dim=-1)
     if world > 1:
         from .parallel import dist as D
 
