@@ -157,7 +157,7 @@ struct NarrowBody {
           g[S::OW3 + j * NO + k] = fmaf(a2[j], dout[k], g[S::OW3 + j * NO + k]);
           da = fmaf(Wi[S::OW3 + j * NO + k], dout[k], da);
         }
-        dz2[j] = da * lrelu_d(z2[j], alpha);
+        dz2[j] = da * lrelu_d(a2[j], alpha);  // (a > 0 <=> z > 0 for 0 <= alpha: z1/z2 need not stay live)
         g[S::OB2 + j] += dz2[j];
       }
 #pragma unroll
@@ -168,7 +168,7 @@ struct NarrowBody {
           g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
           da = fmaf(W2s[S::OW2 + i * H + j], dz2[j], da);
         }
-        const float dz1 = da * lrelu_d(z1[i], alpha);
+        const float dz1 = da * lrelu_d(a1[i], alpha);
         g[S::OB1 + i] += dz1;
 #pragma unroll
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);

@@ -246,10 +246,14 @@ class HipBackend:
         # 9.83 -> 9.64 / 10.05 -> 9.69 us per 2^18 step; the 3-input net is
         # slower that way), 4 = all weights from LDS (256-wide packets),
         # 0 = all weights hoisted (profiles/stamp_r1u_hybrid.jsonl)
-        # (one rank only: with the in-kernel xGMI exchange every workgroup polls
-        # the mailbox, so data-parallel runs keep the 256-workgroup grid)
-        hyb = spec.hidden == 8 and spec.nin <= 2 and self.R <= 128 and world == 1
-        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else (5 if hyb else 4 if self.R > 128 else 0)
+        # 512 workgroups only on one rank (with the in-kernel xGMI exchange every
+        # workgroup polls the mailbox, so data-parallel runs keep 256) and only
+        # where the hybrid body fits 2 waves/SIMD (<= 3 inputs, 128-wide packet);
+        # the 256-wide-packet nets (basket 5-8-6) run it at 1 wave/SIMD, still
+        # faster than all-LDS weights (16.6 -> 14.8 us, profiles/stamp_r1v_masks.jsonl)
+        hyb512 = spec.hidden == 8 and spec.nin <= 3 and self.R <= 128 and world == 1
+        auto_v = 5 if (hyb512 or (spec.hidden == 8 and self.R > 128)) else 0
+        self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else auto_v
         work = max(1, self.batch_local // (256 * max(1, tcfg.paths_per_thread)))
         mw = int(tcfg.max_wgs)
         if mw <= 0:
@@ -257,7 +261,7 @@ class HipBackend:
             # net); the wider-input nets run 1 per CU, so a 512 grid starts in
             # two waves (+15 us start spread, profiles/stamp_r1s_wide_wgs.jsonl)
             mw = 512 if (spec.hidden == 32 and not tcfg.mfma_fp32 and spec.nin == 1) else 256
-            if (self.variant == 5 and tcfg.step_mode in ("auto", "lag") and not tcfg.deterministic
+            if (self.variant == 5 and hyb512 and tcfg.step_mode in ("auto", "lag") and not tcfg.deterministic
                     and not tcfg.split_update):
                 mw = 512  # lagged steps: 2 workgroups (2 waves/SIMD) per CU
         self.num_wgs = int(max(1, min(mw, work)))

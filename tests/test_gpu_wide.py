@@ -77,23 +77,26 @@ def test_wide_deterministic_bitwise(dev):  # noqa: F811
     assert np.array_equal(a[3], b[3])
 
 
-def test_wide_european_end_to_end(dev):  # noqa: F811
+@pytest.mark.parametrize("feature_norm", ["none", "date"])
+def test_wide_european_end_to_end(dev, feature_norm):  # noqa: F811
     """Full backward induction with a 1-32-32-2 net on the bf16 MFMA kernel:
     V0 and phi0 near Black-Scholes (same budget as the 8-unit test)."""
     from rphedge.api import HedgeRun
     from rphedge.config import ParityFlags, RunConfig, TrainingParams
 
     tr = TrainingParams(batch_size=1 << 14, epochs_first=60, epochs_rest=15, early_stopping=False, q99=False,
-                        lr_schedule_first=False, chunk_log2=6, lr=5e-3, hidden=32)
+                        lr_schedule_first=False, chunk_log2=6, lr=5e-3, hidden=32, feature_norm=feature_norm)
     cfg = RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1 / 12, dt=1 / 12,
                     n_paths=18, payoff="call", option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0,
                     keep_paths=True, verbose=False, train=tr, parity=ParityFlags())
     run = HedgeRun(cfg)
     assert run.spec.hidden == 32
     res = run.run()
-    # phi0 is stable; V0 (the net evaluated at the single point S0) scatters by
-    # +-0.5 between runs at this small budget (float-atomic summation order;
-    # tools/wide_e2e_check.py), so its band is wider than the 8-unit test's
+    # phi0 is stable; V0 (the net evaluated at the single point S0, i.e. its
+    # bond holding) scatters between runs at this small budget (float-atomic
+    # summation order): +-0.3 with raw inputs, 10.1-10.9 with an outlier at 8.8
+    # in 7 runs with standardised inputs (tools/wide_e2e_scatter.py,
+    # profiles/wide_e2e_scatter_r1.jsonl), whose P&L std is ~25 % lower
     assert abs(res.phi - 0.7285) < 0.03, res.phi
-    assert abs(res.v0 - 10.3896) < 0.8, res.v0
-    assert res.terminal_pnl["std"] < 1.3, res.terminal_pnl
+    assert abs(res.v0 - 10.3896) < (0.8 if feature_norm == "none" else 2.0), res.v0
+    assert res.terminal_pnl["std"] < (1.3 if feature_norm == "none" else 0.9), res.terminal_pnl
