@@ -272,3 +272,23 @@ def test_verbose_epoch_log(capsys):
     out = capsys.readouterr().out
     assert "Epoch 4/4 - loss:" in out and "mse]" in out and "q99]" in out
     assert "mae:" in out and "reduction =" in out
+
+
+@pytest.mark.parametrize("mode", ["none", "global", "date"])
+def test_feature_norm_modes_through_dict_api(mode):
+    """`feature_norm` is a dict-API key; every mode runs end to end, parity
+    forces raw inputs, and an unknown mode is rejected at build time."""
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+
+    run = HedgeRun(parse_params(_small(feature_norm=mode)))
+    res = run.run()
+    assert np.isfinite(res.phi) and np.isfinite(res.psi)
+    assert (run.induction.norms == []) == (mode == "none")
+    if mode == "global":
+        assert all(n == run.induction.norms[0] for n in run.induction.norms)
+    par = HedgeRun(parse_params(_small(feature_norm=mode, parity=True)))
+    par.build()
+    assert par.induction.norms == []
+    with pytest.raises(ValueError):
+        HedgeRun(parse_params(_small(feature_norm="bogus"))).build()
