@@ -293,6 +293,11 @@ RPH_INLINE float ld_agent(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// bound of one wait for the peers' packets (100 MHz s_memrealtime ticks):
+// generous, because ranks may enter their first step seconds apart (graph
+// upload, page faults); after a timeout dp_error makes every later wait exit
+constexpr unsigned long long DP_SPIN_TICKS = 2000000000ull;  // 20 s
+
 constexpr int ACC_REPLICAS = 8;  // float-atomic accumulator replicas (contention / 8)
 // lagged schedule, 32-unit nets: every workgroup re-reads the whole packet of
 // the previous step in its prologue, R = 1280+ floats x replicas — fewer
@@ -363,13 +368,15 @@ RPH_INLINE void dp_allreduce(const TrainDesc& d, float* red) {
     // wait for rank `tid`'s packet in MY mailbox
     uint32_t* f = d.dp_flags[me] + slot * W + tid;
     unsigned it = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
       __builtin_amdgcn_s_sleep(2);
       ++it;
-      // a peer never arrived (~seconds), or an earlier step already timed out:
-      // fail fast instead of spinning again in every later step
-      if (it > (1u << 23) ||
-          ((it & 255u) == 0u && __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+      // a peer never arrived (DP_SPIN_TICKS), or an earlier step already timed
+      // out: fail fast instead of spinning again in every later step
+      if ((it & 255u) == 0u &&
+          (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS ||
+           __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }

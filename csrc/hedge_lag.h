@@ -186,7 +186,7 @@ RPH_INLINE int lag_dp_exchange(const TrainDesc& d, uint32_t seq, const float* lo
       if (todo == 0u) break;
       __builtin_amdgcn_s_sleep(1);
       if ((++it & 63u) == 0u &&
-          (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||  // 2 s: a peer never arrived
+          (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS ||  // a peer never arrived
            __hip_atomic_load(d.dp_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         __hip_atomic_store(d.dp_error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         bad = 1;
