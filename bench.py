@@ -120,7 +120,7 @@ def build_run(a, world: int):
     pre = PRESETS[a.preset]
     tr = TrainingParams(batch_size=(1 << a.batch_log2) * world, epochs_first=a.epochs_first,
                         epochs_rest=a.epochs_rest, patience_first=10 ** 6, patience_rest=10 ** 6,
-                        lr=a.lr, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
+                        lr=a.lr, lr_rest=a.lr_rest, lr_decay=a.lr_decay, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
                         chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision,
                         variant=a.variant, max_wgs=a.max_wgs, feature_norm=a.feature_norm)
     model = pre["model"]
@@ -166,25 +166,8 @@ def main(argv=None):
     run = HedgeRun(cfg, dist_info=di)
     rank = run.di.rank
     gpu = run.device.type == "cuda"
-    # lr schedule: first date a.lr, later dates a.lr_rest (constant per date; see FitConfig)
+    # lr schedule (TrainingParams.lr / lr_rest / lr_decay): geometric decay over each date's epochs
     run.build()
-    def sched(lr0, n):
-        n = max(n, 1)
-        if n <= 1 or a.lr_decay == 1.0:
-            return tuple([lr0] * n)
-        return tuple(lr0 * a.lr_decay ** (e / (n - 1)) for e in range(n))
-
-    sched_first = sched(a.lr, a.epochs_first)
-    sched_rest = sched(a.lr_rest, a.epochs_rest)
-    ind = run.induction
-    orig = ind._fcfg
-
-    def fcfg(first, loss):
-        f = orig(first, loss)
-        f.lr_schedule = sched_first if first else sched_rest
-        return f
-
-    ind._fcfg = fcfg
     use_graph = gpu and not a.no_graph and (world == 1 or os.environ.get("RPH_GRAPH_DP", "1") == "1")
     if use_graph:
         try:

@@ -70,6 +70,15 @@ class HedgeRun:
             raise ValueError("hip backend needs a GPU device")
         self.stream = stream
         self.grid = P.Grid(cfg.T, cfg.dt, cfg.rebalancing)
+        t_end = float(self.grid.times()[-1])
+        if t_end - cfg.T > 1e-6 * max(cfg.T, 1.0):
+            # ceil(T/dt) of the reference grid (C11) overshoots T when dt is a
+            # truncated decimal (e.g. 0.0333333333333333 for 1/30); ending
+            # short of T is the reference's own decimation (floor) convention
+            import warnings
+
+            warnings.warn(f"time grid ends at {t_end:.10g}, beyond T={cfg.T:g} (dt={cfg.dt!r}, "
+                          f"rebalancing={cfg.rebalancing!r}); pass dt / rebalancing at full precision", stacklevel=2)
         self.n_total = 2 ** int(cfg.n_paths)
         self.offset, self.n_local = D.shard(self.n_total, dist_info.world, dist_info.rank)
         self.timer = PhaseTimer(enabled=True, device=self.device)
@@ -232,6 +241,7 @@ class HedgeRun:
                                patience_first=tr.patience_first, patience_rest=tr.patience_rest,
                                early_stopping=tr.early_stopping,
                                lr_schedule_first=tr.lr_schedule_first and pf.lr_schedule_first_only,
+                               lr=tr.lr, lr_rest=tr.lr_rest, lr_decay=tr.lr_decay,
                                q99=tr.q99, quantile=tr.quantile, cost_of_capital=tr.cost_of_capital,
                                shared_q99_model=pf.shared_q99_model,
                                holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start,

@@ -56,7 +56,10 @@ class TrainingParams:
     patience_first: int = 50
     patience_rest: int = 7
     lr: float = 1e-3
-    lr_schedule_first: bool = True
+    lr_schedule_first: bool = True   # reference step schedule (RP:128-136) on the first date
+    lr_rest: float = 0.0             # learning rate of the later dates (0: keep the optimiser's current lr)
+    lr_decay: float = 1.0            # per-date geometric decay, last/first epoch (1: constant); applies to
+                                     # lr on the first date when lr_schedule_first is off, and to lr_rest
     early_stopping: bool = True
     cost_of_capital: float = 0.1
     quantile: float = 0.99

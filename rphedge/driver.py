@@ -23,7 +23,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from .engine import DateData, FitConfig, TrainConfig, fit_seed, fit_summary, keras_lr_schedule, reduce_stats
+from .engine import (DateData, FitConfig, TrainConfig, fit_seed, fit_summary, geometric_lr_schedule,
+                     keras_lr_schedule, reduce_stats)
 from .models.hedge_mlp import NetSpec
 from .ops import layout as L
 from .ops.paths import Paths
@@ -37,6 +38,9 @@ class InductionConfig:
     patience_rest: int = 7
     early_stopping: bool = True
     lr_schedule_first: bool = True
+    lr: float = 1e-3                     # first-date lr of the geometric schedule (lr_decay != 1)
+    lr_rest: float = 0.0                 # later dates (0: keep the optimiser's current lr)
+    lr_decay: float = 1.0                # geometric decay per date, last/first epoch
     q99: bool = True
     quantile: float = 0.99
     cost_of_capital: float = 0.1
@@ -138,14 +142,20 @@ class BackwardInduction:
         self.stats = [[backend.new_stats(), backend.new_stats()] for _ in range(self.n_dates)]
         self.snap = torch.zeros(self.n_dates, 2, L.NETW_FLOATS, dtype=torch.float32, device=dev) \
             if icfg.snapshot_weights else None
-        self.lr_first = tuple(keras_lr_schedule(icfg.epochs_first)) if icfg.lr_schedule_first else None
+        if icfg.lr_schedule_first:
+            self.lr_first = tuple(keras_lr_schedule(icfg.epochs_first))
+        else:
+            self.lr_first = geometric_lr_schedule(icfg.lr, icfg.epochs_first, icfg.lr_decay) \
+                if icfg.lr_decay != 1.0 else None
+        self.lr_rest = geometric_lr_schedule(icfg.lr_rest or icfg.lr, icfg.epochs_rest, icfg.lr_decay) \
+            if (icfg.lr_rest > 0 or icfg.lr_decay != 1.0) else None
         self.norms = feature_norms(paths, icfg.feature_norm, world)
 
     def _fcfg(self, first: bool, loss: int) -> FitConfig:
         c = self.cfg
         return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
                          patience=c.patience_first if first else c.patience_rest,
-                         loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else None,
+                         loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else self.lr_rest,
                          restore_best=True, restore_at_end=c.restore_best_at_end, early_stopping=c.early_stopping)
 
     def date_data(self, t: int) -> DateData:

@@ -61,6 +61,17 @@ def keras_lr_schedule(epochs: int) -> list:
     return out
 
 
+def geometric_lr_schedule(lr0: float, epochs: int, decay: float = 1.0) -> tuple:
+    """Per-epoch learning rates ``lr0 * decay**(e / (epochs-1))``: decays from
+    ``lr0`` to ``lr0 * decay`` over one date's fit (``decay = 1``: constant).
+    Throughput-mode counterpart of the reference's step schedule for the large
+    global batches; ``TrainingParams.lr_rest`` / ``lr_decay``."""
+    n = max(int(epochs), 1)
+    if n == 1 or decay == 1.0:
+        return tuple([float(lr0)] * n)
+    return tuple(float(lr0) * decay ** (e / (n - 1)) for e in range(n))
+
+
 @dataclass
 class FitConfig:
     epochs: int = 100

@@ -56,6 +56,41 @@ def test_parity_shared_model_has_identical_nets():
     assert run2.induction.w_q is not run2.induction.w_mse
 
 
+def test_lr_rest_and_decay_schedules_through_dict_api():
+    """lr / lr_rest / lr_decay build the per-epoch schedules of every date's fit
+    (the throughput presets of bench.py use them); defaults keep the reference
+    behaviour (step schedule on the first date, current lr afterwards)."""
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.engine import geometric_lr_schedule, keras_lr_schedule
+
+    g = geometric_lr_schedule(5e-2, 5, 0.1)
+    np.testing.assert_allclose(g, [5e-2 * 0.1 ** (e / 4) for e in range(5)], rtol=1e-12)
+    assert geometric_lr_schedule(1e-3, 3) == (1e-3,) * 3
+    run = HedgeRun(parse_params(_small(lr=5e-2, lr_rest=4e-3, lr_decay=0.1, lr_schedule_first=False)))
+    run.build()
+    ind = run.induction
+    assert ind._fcfg(True, 0).lr_schedule == geometric_lr_schedule(5e-2, 20, 0.1)
+    assert ind._fcfg(False, 0).lr_schedule == geometric_lr_schedule(4e-3, 5, 0.1)
+    ref = HedgeRun(parse_params(_small()))
+    ref.build()
+    assert list(ref.induction._fcfg(True, 0).lr_schedule) == keras_lr_schedule(20)
+    assert ref.induction._fcfg(False, 0).lr_schedule is None
+
+
+def test_example_configs_end_their_grid_at_maturity():
+    """Every shipped config's coarse grid ends at T (a truncated 1/30 once made
+    the reference-convention grid overshoot by one date)."""
+    import glob
+
+    from rphedge.ops.paths import Grid
+
+    for p in sorted(glob.glob(os.path.join(ROOT, "examples", "*.json"))):
+        d = json.load(open(p))
+        g = Grid(d["T"], d["dt"], d["rebalancing"])
+        assert abs(float(g.times()[-1]) - d["T"]) < 1e-9 * d["T"], p
+
+
 def test_lambda_fine_index_quirk():
     """Q3: with parity the lambda feature at coarse index i is lambda on the fine grid at i."""
     from rphedge.ops import paths as P
