@@ -41,7 +41,7 @@ def _bench(args, env=None, nproc=1):
         cmd = [sys.executable, "bench.py"] + args
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", str(nproc)] + args
+               "--master-addr", "127.0.0.1", "--master-port", str(29531 + nproc), "bench.py", "--gpus", str(nproc)] + args
     out = subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -58,11 +58,13 @@ def test_bench_cpu_preset_contract():
     assert r["quality"]["anchor"]["analytic"] == "black_scholes"
 
 
-def test_bench_cpu_four_ranks():
-    """--gpus 4 under torch.distributed.run (gloo on CPU): weak scaling, the
-    global batch and path count grow with the world size; rank 0 prints once."""
+@pytest.mark.parametrize("nproc", [4, 8])
+def test_bench_cpu_multi_rank(nproc):
+    """--gpus N under torch.distributed.run (gloo on CPU; N=8 is the driver's
+    scaling-node world size): weak scaling, the global batch and path count
+    grow with the world size; rank 0 prints once."""
     r = _bench(["--preset", "euro1_cpu", "--steps", "1", "--warmup", "0", "--epochs-first", "10",
-                "--paths-log2", "12", "--batch-log2", "10", "--cpu"], nproc=4)
-    assert r["n_gpus"] == 4 and r["config"]["parallelism"] == "dp4"
-    assert r["config"]["paths_global"] == 4 * (1 << 12) and r["config"]["global_batch"] == 4 * (1 << 10)
+                "--paths-log2", "12", "--batch-log2", "10", "--cpu"], nproc=nproc)
+    assert r["n_gpus"] == nproc and r["config"]["parallelism"] == f"dp{nproc}"
+    assert r["config"]["paths_global"] == nproc * (1 << 12) and r["config"]["global_batch"] == nproc * (1 << 10)
     assert math.isfinite(r["quality"]["V0"]) and abs(r["quality"]["V0"] - 10.39) < 1.5
