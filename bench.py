@@ -147,19 +147,47 @@ def anchor(cfg) -> dict:
     return {"analytic": "black_scholes", "price": p, "delta": dlt}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def self_launch(n: int, argv=None) -> int:
+    """``bench.py --gpus N`` without a torch.distributed environment: run N
+    ranks (one process per GPU) under ``torch.distributed.run`` as a CHILD
+    process and return its exit code.  Nothing here touches the GPU (the
+    parent never initialises HIP), so the ranks own their devices; rank 0 of
+    the child prints the JSON line to the inherited stdout."""
+    import subprocess
+
+    args = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + args
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (mailboxes, RCCL) on this driver
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
     a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return self_launch(a.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
-        if a.gpus > 1 and world == 1:
-            print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
-            return 2
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; measuring the {world} launched ranks",
+              file=sys.stderr)
     from rphedge.parallel import dist as D
     from rphedge.api import HedgeRun
 
-    di = D.init() if world > 1 else None
+    di = D.init(device="cpu" if a.cpu else None) if world > 1 else None
+    probe = None
     if di is not None and not a.cpu:
         D.select_transport(di)  # in-kernel xGMI exchange if a probe fit is clean, else RCCL
+        probe = di.probe
     cfg = build_run(a, world)
     if a.cpu and di is None:
         di = D.DistInfo(device=torch.device("cpu"))
@@ -239,7 +267,9 @@ def main(argv=None):
                    "steps_per_epoch": run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,
                    "step_schedule": run.backend.step_mode() if hasattr(run.backend, "step_mode") else "torch",
-                   "dp_transport": (run.di.dp_mode if world > 1 else None)},
+                   "dp_transport": (("gloo" if a.cpu else run.di.dp_mode) if world > 1 else None),
+                   "dp_probe": probe, "dist_world": D.dist_world(),
+                   "launch": "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1 else "single"},
         "quality": {"terminal_pnl_std": res.terminal_pnl["std"], "terminal_pnl_mean": res.terminal_pnl["mean"],
                     "V0": res.v0, "phi0": res.phi, "psi0": res.psi,
                     "anchor": anchor(cfg),
@@ -253,6 +283,7 @@ def main(argv=None):
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    run.close()
     D.shutdown()
     return 0
 

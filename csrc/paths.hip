@@ -83,17 +83,66 @@ __global__ __launch_bounds__(256) void k_sim_scan(const SimDesc d) {
     d.out[p] = (float)d.s0[0] * inv0;
     if (d.out2) d.out2[p] = (float)v;
     const Real rho = (Real)d.rho, rhoc = sqrt((Real)1 - rho * rho);
+    // Andersen (2008) QE constants (uniform over the launch): variance moments
+    // m = theta + (v - theta) e^{-kappa dt}, s^2 = v*qc1 + qc2; log-price
+    // central discretisation gamma1 = gamma2 = 1/2 (K1..K4) with the
+    // martingale-corrected K0* (E[S_{t+dt}] = S_t e^{mu dt} exactly)
+    const Real kap = (Real)d.kappa, th = (Real)d.theta, xi = (Real)d.xi;
+    const Real ekd = exp(-kap * dt);
+    const Real qc1 = xi * xi * ekd * ((Real)1 - ekd) / kap;
+    const Real qc2 = th * xi * xi * ((Real)1 - ekd) * ((Real)1 - ekd) / ((Real)2 * kap);
+    const Real qK1 = (Real)0.5 * dt * (kap * rho / xi - (Real)0.5) - rho / xi;
+    const Real qK2 = (Real)0.5 * dt * (kap * rho / xi - (Real)0.5) + rho / xi;
+    const Real qK3 = (Real)0.5 * dt * ((Real)1 - rho * rho);
+    const Real qA = qK2 + (Real)0.5 * qK3;
+    const Real qK0u = -rho * kap * th * dt / xi;  // uncorrected K0 (when the correction does not exist)
+    const bool qe = MODEL == SIM_HESTON && d.scheme == HESTON_QE;
+    const Real tau = (Real)d.sv_tscale * dt;  // SV_REF corrected: calibration-day time step
     for (int t = 1; t < d.n_fine; ++t) {
       const Real z1 = ndtri_u30<Real>(sobol_point<ALIGNED>(d.sv1 + (size_t)t * 32, d.shift1[t], g));
-      const Real z2 = ndtri_u30<Real>(sobol_point<ALIGNED>(d.sv2 + (size_t)t * 32, d.shift2[t], g));
+      const uint32_t x2 = sobol_point<ALIGNED>(d.sv2 + (size_t)t * 32, d.shift2[t], g);
       if (MODEL == SIM_SV_REF) {
-        // RP:285  vt = vt + a(b - vt) + c sqrt(vt dt) W_SV   (no dt on the drift: Q5)
-        const Real arg = v * dt;
-        const Real sq = d.parity ? sqrt(arg) : sqrt(arg > (Real)0 ? arg : (Real)0);  // parity: NaN like numpy
-        v = v + (Real)d.a * ((Real)d.b - v) + (Real)d.c * sq * z2;
-        // RP:287  logY += (mu - vt^2/2) dt + vt sqrt(dt) W1   (vt used as a volatility)
-        ly += (mu - (Real)0.5 * v * v) * dt + v * sdt * z1;
+        const Real z2 = ndtri_u30<Real>(x2);
+        if (d.sv_tscale > 0.0) {
+          // corrected CIR-on-sigma: rates in calibration-day units, full
+          // truncation, price shock with the start-of-step volatility
+          const Real vp = v > (Real)0 ? v : (Real)0;
+          ly += (mu - (Real)0.5 * vp * vp) * dt + vp * sdt * z1;
+          v = v + (Real)d.a * ((Real)d.b - vp) * tau + (Real)d.c * sqrt(vp * tau) * z2;
+        } else {
+          // RP:285  vt = vt + a(b - vt) + c sqrt(vt dt) W_SV   (no dt on the drift: Q5)
+          const Real arg = v * dt;
+          const Real sq = d.parity ? sqrt(arg) : sqrt(arg > (Real)0 ? arg : (Real)0);  // parity: NaN like numpy
+          v = v + (Real)d.a * ((Real)d.b - v) + (Real)d.c * sq * z2;
+          // RP:287  logY += (mu - vt^2/2) dt + vt sqrt(dt) W1   (vt used as a volatility)
+          ly += (mu - (Real)0.5 * v * v) * dt + v * sdt * z1;
+        }
+      } else if (qe) {
+        const Real m = th + (v - th) * ekd;
+        const Real s2 = v * qc1 + qc2;
+        const Real psi = s2 / (m * m);
+        Real vn, k0;
+        if (psi <= (Real)1.5) {  // quadratic branch: v' = a (b + Z)^2
+          const Real z2 = ndtri_u30<Real>(x2);
+          const Real ip = (Real)2 / psi;
+          const Real b2 = ip - (Real)1 + sqrt(ip) * sqrt(ip - (Real)1);
+          const Real qa = m / ((Real)1 + b2);
+          const Real bz = sqrt(b2) + z2;
+          vn = qa * bz * bz;
+          const Real den = (Real)1 - (Real)2 * qA * qa;
+          k0 = den > (Real)0 ? -qA * b2 * qa / den + (Real)0.5 * log(den) - (qK1 + (Real)0.5 * qK3) * v : qK0u;
+        } else {  // exponential branch: point mass p at 0, exponential tail (inverse CDF of the uniform)
+          const Real p = (psi - (Real)1) / (psi + (Real)1);
+          const Real beta = ((Real)1 - p) / m;
+          const Real u = (Real)x2 * (Real)9.313225746154785e-10;
+          vn = u <= p ? (Real)0 : log(((Real)1 - p) / ((Real)1 - u)) / beta;
+          k0 = beta > qA ? -log(p + beta * ((Real)1 - p) / (beta - qA)) - (qK1 + (Real)0.5 * qK3) * v : qK0u;
+        }
+        const Real var = qK3 * (v + vn);
+        ly += mu * dt + k0 + qK1 * v + qK2 * vn + sqrt(var > (Real)0 ? var : (Real)0) * z1;
+        v = vn;
       } else {
+        const Real z2 = ndtri_u30<Real>(x2);
         const Real vp = v > (Real)0 ? v : (Real)0;
         const Real sv = sqrt(vp * dt);
         ly += (mu - (Real)0.5 * vp) * dt + sv * (rho * z2 + rhoc * z1);

@@ -168,7 +168,16 @@ struct SimDesc {
   float* out3;                   // third coarse output (lambda)             [n_coarse][n_local]
   float* final_out;              // terminal fine value(s) [na][n_local]
   float* final2_out;             // terminal fine N-fraction [n_local]
+  // SV_REF: time scale of the calibrated (a, b, c) in fine steps; 0 = the
+  // reference recursion (no dt on the mean reversion, Q5), > 0 = corrected
+  // CIR-on-sigma with every rate in calibration-day units: a(b-v) dt*tscale,
+  // c sqrt(v dt*tscale) (tscale = 252 trading days per year)
+  double sv_tscale;
+  int scheme;                    // HESTON: 0 full-truncation Euler, 1 Andersen QE (martingale-corrected)
+  int pad0;
 };
+
+enum HestonScheme : int { HESTON_EULER = 0, HESTON_QE = 1 };
 
 enum SimModel : int {
   SIM_GBM_ARITH = 0,   // Y_t = Y_{t-1}(1 + mu dt + sigma sqrt(dt) Z)   (RP:64-65)

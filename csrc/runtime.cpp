@@ -65,7 +65,8 @@ extern "C" int rph_layout(long long* out, int cap) {
       (long long)sizeof(SimDesc), OFF(SimDesc, path_offset), OFF(SimDesc, sv1), OFF(SimDesc, dims1),
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),
       OFF(SimDesc, inv_norm), OFF(SimDesc, v0), OFF(SimDesc, rho), OFF(SimDesc, l0), OFF(SimDesc, n0),
-      OFF(SimDesc, seed), OFF(SimDesc, out), OFF(SimDesc, final2_out),
+      OFF(SimDesc, seed), OFF(SimDesc, out), OFF(SimDesc, final2_out), OFF(SimDesc, sv_tscale),
+      OFF(SimDesc, scheme),
       (long long)LAG_SLOTS,
   };
   const int n = (int)(sizeof(v) / sizeof(v[0]));

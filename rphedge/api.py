@@ -133,7 +133,8 @@ class HedgeRun:
             if self.kind == "european":
                 if c.model == "heston":
                     p = P.simulate_sv(g, self.n_local, c.Y, c.r, c.v0, model="heston", kappa=c.kappa,
-                                      theta=c.theta, xi=c.xi, rho=c.rho, norm=c.Y, fp64=fp64, **kw)
+                                      theta=c.theta, xi=c.xi, rho=c.rho, norm=c.Y, fp64=fp64,
+                                      scheme=c.heston_scheme, **kw)
                 else:
                     scheme = "arith" if c.model == "gbm" else "log"
                     p = P.simulate_gbm(g, self.n_local, c.Y, c.r, c.sigma, scheme=scheme, norm=c.Y, fp64=fp64,
@@ -155,7 +156,9 @@ class HedgeRun:
                     sv_c = c.sv_c
                     p = P.simulate_sv(g, self.n_local, c.Y, c.mu, c.s0, model=c.model, a=c.a, b=c.b, c=sv_c,
                                       kappa=c.kappa, theta=c.theta, xi=c.xi, rho=c.rho, fp64=fp64,
-                                      parity_nan=c.parity.sv_sqrt_nan, **kw)
+                                      parity_nan=c.parity.sv_sqrt_nan, scheme=c.heston_scheme,
+                                      sv_tscale=0.0 if c.parity.sv_reference_dynamics else c.sv_days_per_year,
+                                      **kw)
                 else:
                     p = P.simulate_gbm(g, self.n_local, c.Y, c.mu, c.sigma, scheme=("log" if c.model == "gbm_log"
                                                                                    else "arith"),
@@ -231,6 +234,8 @@ class HedgeRun:
             tcfg.variant = int(tr.variant)
         kw = {}
         if self.backend_kind == "hip" and self.di.world > 1:
+            if self.di.probe is None and self.di.dp_mode == "xgmi":
+                D.select_transport(self.di)  # once per process group (collective); may fall back to RCCL
             self.mailbox = D.make_mailbox(self.di, self.spec.red_width)
             kw["mailbox"] = self.mailbox
         self.backend = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
@@ -319,6 +324,14 @@ class HedgeRun:
     def replay(self):
         self.graph.replay(self.stream or torch.cuda.current_stream(self.device))
 
+    def close(self):
+        """Release the run's cross-rank resources (collective when data
+        parallel: every rank's kernels finish before any mailbox is freed)."""
+        mb = getattr(self, "mailbox", None)
+        self.mailbox = None
+        if mb is not None:
+            D.close_mailbox(mb)
+
     def resume(self, out_dir: str, date: int) -> RunResult:
         """Restart the backward scan at ``date-1`` from a saved run directory
         (weights of ``date`` as the warm start, Q18, and ``values[date]``).
@@ -341,8 +354,15 @@ class HedgeRun:
             self._wq_resume = wq
         if vals is None:
             raise ValueError("values.npy missing: cannot resume the backward induction")
+        # values.npy holds the GLOBAL path set (save_run gathers the shards):
+        # every rank takes its own contiguous shard
+        if vals.shape[0] == self.n_total:
+            vals = vals[self.offset:self.offset + self.n_local]
+        else:
+            raise ValueError(f"values.npy has {vals.shape[0]} paths; this run has {self.n_total} "
+                             f"({self.n_local} on this rank)")
         t0 = time.perf_counter()
-        ind.values[date].copy_(torch.from_numpy(vals).to(ind.values.device))
+        ind.values[date].copy_(torch.from_numpy(np.ascontiguousarray(vals)).to(ind.values.device))
         ind.w_mse.copy_(ind.w_init)
         ind.opt_mse.copy_(ind.opt_init)
         if ind.cfg.q99:
@@ -419,12 +439,29 @@ def _print_dates(run: HedgeRun, res: RunResult):
     """Per-date log of the reference (RP:194, :122); ``verbose=2`` adds the
     Keras-style per-epoch training log of every fit (``fit(verbose=1)`` in
     "European Options.ipynb" cell 13) from the on-device epoch-loss history."""
-    if not run.cfg.verbose or not run.di.is_main:
+    if not run.cfg.verbose:
         return
     ind = res.induction
     p = run.paths
     dtc = run.grid.dt_coarse
+    w = run.di.world
+
+    def gmean(x: torch.Tensor) -> float:
+        s = float(x.double().sum())
+        return (D.all_reduce_scalar(s, device=run.device) if w > 1 else s) / float(run.n_total)
+
+    # collectives (global means, distributed quantiles) on EVERY rank, in the
+    # same order; only the printing is rank 0's
+    rows = []
     for d in ind.dates:
+        t = d.index
+        y = gmean(p.asset(t + 1)) * (1.0 if run.kind == "pension" else run.cfg.Y)
+        nm = gmean(p.nfrac[t + 1]) if p.nfrac is not None else None
+        q = risk.quantile(ind.residuals[t], (0.98, 0.99), w) if ind.residuals is not None else None
+        rows.append((d, y, nm, q))
+    if not run.di.is_main:
+        return
+    for d, y, nm, q in rows:
         t = d.index
         if int(run.cfg.verbose) >= 2:
             for name, fs in (("mse", d.fit_mse), ("q99", d.fit_q99)):
@@ -435,13 +472,11 @@ def _print_dates(run: HedgeRun, res: RunResult):
                     print(f"[t={t * dtc:.4f} {name}] Epoch {e + 1}/{len(hist)} - loss: {loss:.4e}")
                 print(f"[t={t * dtc:.4f} {name}] mae: {fs['mae']:.4e} - mape: {fs['mape']:.4f}"
                       f"{' - early stop' if fs['stopped'] and len(hist) else ''}")
-        y = float(p.asset(t + 1).double().mean()) * (1.0 if run.kind == "pension" else run.cfg.Y)
         line = f">> Y_({(t + 1) * dtc:.2f}) = {y:.3f}"
-        if p.nfrac is not None:
-            line += f", N_({(t + 1) * dtc:.2f}) = {float(p.nfrac[t + 1].double().mean()):.3f}"
+        if nm is not None:
+            line += f", N_({(t + 1) * dtc:.2f}) = {nm:.3f}"
         print(line)
-        if ind.residuals is not None:
-            q = risk.quantile(ind.residuals[t], (0.98, 0.99), run.di.world)
+        if q is not None:
             print(f"VaR: {q[0]:4f} (98%),  {q[1]:4f} (99%)  | epochs {d.fit_mse['epochs']}"
                   f"{'/' + str(d.fit_q99['epochs']) if d.fit_q99 else ''}  loss {d.fit_mse['last_loss']:.3e}")
 
@@ -457,6 +492,7 @@ def run_params(params: dict, sv: bool = False) -> RunResult:
         from .utils.model_io import save_run
 
         save_run(cfg.save_dir, run, res)
+    run.close()
     return res
 
 

@@ -1,7 +1,10 @@
 """Pseudo-random Brownian helpers (C42, ``brownian_motion.py:6-24``).
 
-Kept for API completeness (the reference never imports them): ``get_dW`` draws
-T iid N(0,1) increments, ``get_W`` is their cumulative sum starting at 0.
+Kept for API completeness (the reference never imports them).  Same draws as
+the reference: ``get_dW`` reseeds numpy's legacy global MT19937 stream with
+``random_state`` and samples T iid N(0,1) increments from it (so the values
+AND the global-RNG side effect match ``np.random.seed(s); np.random.normal``);
+``get_W`` is the cumulative sum shifted to start at 0 (same length T).
 """
 from __future__ import annotations
 
@@ -10,11 +13,11 @@ import numpy as np
 
 def get_dW(T: int, random_state: int | None = None) -> np.ndarray:
     """Sample T times from a normal distribution (Brownian increments)."""
-    rng = np.random.default_rng(random_state)
-    return rng.normal(0.0, 1.0, T)
+    np.random.seed(random_state)          # legacy global RandomState, as brownian_motion.py:12
+    return np.random.normal(0.0, 1.0, T)
 
 
 def get_W(T: int, random_state: int | None = None) -> np.ndarray:
-    """Simulated Brownian motion W_0 = 0, W_t = sum of the first t increments."""
+    """Simulated Brownian motion at unit time steps: W_0 = 0, W_t = dW_1 + ... + dW_t."""
     dW = get_dW(T, random_state)
-    return np.insert(np.cumsum(dW)[:-1], 0, 0.0)
+    return np.insert(dW.cumsum(), 0, 0.0)[:-1]

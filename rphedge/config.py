@@ -25,7 +25,8 @@ class ParityFlags:
     holdings_blend_sign_rp: bool = False  # Q2: phi1 + c(phi1 - phi2) (RP) instead of phi1 + c(phi2 - phi1)
     lambda_fine_index: bool = False     # Q3: lambda not subsampled (fine index t_i)
     sv_c_overwrite: bool = False        # Q4: params['c'] is read twice (vol-of-vol := mortality c)
-    sv_reference_dynamics: bool = True  # Q5: reference SV recursion (no dt on mean reversion, vt as vol)
+    sv_reference_dynamics: bool = False  # Q5: reference SV recursion (no dt on mean reversion, post-update vt
+                                         # in the price step); False = CIR-on-sigma in calibration-day units
     sv_sqrt_nan: bool = False           # numpy sqrt(negative) -> NaN propagation
     fine_terminal_payoff: bool = True   # payoff from the last FINE point even if the coarse grid misses it
     lr_schedule_first_only: bool = True  # Q17: LR schedule + patience 50 only on the first date
@@ -111,6 +112,8 @@ class RunConfig:
     xi: float = 0.3
     rho: float = -0.7
     v0: float = 0.0256
+    heston_scheme: str = "qe"        # qe (Andersen QE, martingale-corrected) | euler (full truncation)
+    sv_days_per_year: float = 252.0  # corrected CIR-on-sigma: calibration steps per year (daily data)
     # extensions
     model: str = "gbm"               # gbm | gbm_log | sv_ref | heston | basket
     payoff: str = "guarantee"        # guarantee | call | put | basket_call

@@ -57,3 +57,4 @@ HEAD_FREE, HEAD_COMPLEMENT = 0, 1
 LOSS_MSE, LOSS_PINBALL = 0, 1
 
 SIM_GBM_ARITH, SIM_GBM_LOG, SIM_SV_REF, SIM_HESTON, SIM_BASKET, SIM_MORTALITY = range(6)
+HESTON_EULER, HESTON_QE = 0, 1   # SimDesc.scheme (csrc/rph_types.h HestonScheme)

@@ -81,6 +81,7 @@ class SimDesc(C.Structure):
         ("kappa", C.c_double), ("theta", C.c_double), ("xi", C.c_double), ("rho", C.c_double),
         ("l0", C.c_double), ("lc", C.c_double), ("eta", C.c_double), ("n0", C.c_int), ("seed", C.c_uint32),
         ("out", VP), ("out2", VP), ("out3", VP), ("final_out", VP), ("final2_out", VP),
+        ("sv_tscale", C.c_double), ("scheme", C.c_int), ("pad0", C.c_int),
     ]
 
 
@@ -101,7 +102,7 @@ def _expected_layout() -> list[int]:
         E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset, E.fmu.offset, E.fisd.offset,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
-        S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset,
+        S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset, S.sv_tscale.offset, S.scheme.offset,
         L.LAG_SLOTS,
     ]
 

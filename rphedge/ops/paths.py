@@ -148,8 +148,20 @@ def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, s
 def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model: str = "sv_ref",
                 a=0.0, b=0.0, c=0.0, kappa=0.0, theta=0.0, xi=0.0, rho=0.0, norm: float = 1.0,
                 device="cuda", offset: int = 0, fp64: bool = False, parity_nan: bool = False,
-                seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None, out: Paths | None = None) -> Paths:
-    """Reference CIR-on-sigma SV (RP:282-289) or full-truncation Heston (K4)."""
+                seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None, out: Paths | None = None,
+                scheme: str = "qe", sv_tscale: float = 0.0) -> Paths:
+    """Reference CIR-on-sigma SV (RP:282-289) or Heston (K4).
+
+    ``scheme`` (Heston): "qe" = Andersen quadratic-exponential variance step
+    with the martingale-corrected log-price step (default: no visible
+    discretisation bias at 10 steps per date), "euler" = full-truncation Euler.
+    ``sv_tscale`` (SV_REF): 0 = the reference recursion (Q5); > 0 = corrected
+    CIR-on-sigma with the calibrated daily (a, b, c) applied over
+    ``dt * sv_tscale`` calibration days per fine step."""
+    if scheme not in ("qe", "euler"):
+        raise ValueError(f"heston scheme must be qe | euler, got {scheme!r}")
+    if model == "heston" and scheme == "qe" and not (kappa > 0 and xi > 0):
+        scheme = "euler"  # QE needs a mean-reverting, stochastic variance
     dev = torch.device(device)
     S = out.S if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
     V = out.vol if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
@@ -166,11 +178,14 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
         d.s0[0], d.mu[0], d.inv_norm[0] = s0, mu, 1.0 / norm
         d.v0, d.a, d.b, d.c = v0, a, b, c
         d.kappa, d.theta, d.xi, d.rho = kappa, theta, xi, rho
+        d.sv_tscale = float(sv_tscale) if model == "sv_ref" else 0.0
+        d.scheme = L.HESTON_QE if scheme == "qe" else L.HESTON_EULER
         d.out, d.out2, d.final_out = S.data_ptr(), V.data_ptr(), fin.data_ptr()
         native.simulate(d, stream)
     else:
         s_np, v_np, f_np = _cpu_sv(grid, n_local, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset,
-                                   parity_nan, seed1, seed2)
+                                   parity_nan, seed1, seed2, scheme=scheme,
+                                   sv_tscale=float(sv_tscale) if model == "sv_ref" else 0.0)
         S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
         V.copy_(torch.from_numpy(v_np.astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
@@ -307,9 +322,48 @@ def _cpu_gbm(grid, n, s0, mu, sigma, scheme, offset, seed):
     return out, fin
 
 
-def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, parity_nan, seed1, seed2):
+def _u30(table_dims, seed, n_local, offset, dims):
+    tab = sobol_table(table_dims, seed)
+    return tab.points_u30(np.arange(offset, offset + n_local, dtype=np.uint64), dims=dims).astype(np.int64)
+
+
+def _qe_step(v, z1, x2, dt, mu, kappa, theta, xi, rho):
+    """One Andersen (2008) QE step (martingale-corrected K0*) — numpy twin of
+    the k_sim_scan HESTON_QE branch.  Returns (d log S, v_next)."""
+    ekd = math.exp(-kappa * dt)
+    m = theta + (v - theta) * ekd
+    s2 = v * xi * xi * ekd * (1 - ekd) / kappa + theta * xi * xi * (1 - ekd) ** 2 / (2 * kappa)
+    psi = s2 / (m * m)
+    k1 = 0.5 * dt * (kappa * rho / xi - 0.5) - rho / xi
+    k2 = 0.5 * dt * (kappa * rho / xi - 0.5) + rho / xi
+    k3 = 0.5 * dt * (1 - rho * rho)
+    A = k2 + 0.5 * k3
+    k0u = -rho * kappa * theta * dt / xi
+    quad = psi <= 1.5
+    with np.errstate(invalid="ignore", divide="ignore"):
+        z2 = ndtri_u30_f64(x2)
+        ip = 2.0 / psi
+        b2 = ip - 1 + np.sqrt(ip) * np.sqrt(np.maximum(ip - 1, 0.0))
+        qa = m / (1 + b2)
+        vq = qa * (np.sqrt(b2) + z2) ** 2
+        den = 1 - 2 * A * qa
+        k0q = np.where(den > 0, -A * b2 * qa / den + 0.5 * np.log(np.maximum(den, 1e-300)) - (k1 + 0.5 * k3) * v, k0u)
+        p = (psi - 1) / (psi + 1)
+        beta = (1 - p) / m
+        u = x2 * 2.0 ** -30
+        ve = np.where(u <= p, 0.0, np.log((1 - p) / np.maximum(1 - u, 1e-300)) / beta)
+        k0e = np.where(beta > A, -np.log(p + beta * (1 - p) / (beta - A)) - (k1 + 0.5 * k3) * v, k0u)
+    vn = np.where(quad, vq, ve)
+    k0 = np.where(quad, k0q, k0e)
+    dly = mu * dt + k0 + k1 * v + k2 * vn + np.sqrt(np.maximum(k3 * (v + vn), 0.0)) * z1
+    return dly, vn
+
+
+def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, parity_nan, seed1, seed2,
+            scheme="euler", sv_tscale=0.0):
     W1 = _normals(grid.n_fine, seed1, n, offset, grid.n_fine)
-    W2 = _normals(grid.n_fine, seed2, n, offset, grid.n_fine)
+    X2 = _u30(grid.n_fine, seed2, n, offset, grid.n_fine)
+    W2 = ndtri_u30_f64(X2)
     dt = grid.dt
     ly = np.full(n, math.log(s0))
     v = np.full(n, float(v0))
@@ -317,13 +371,21 @@ def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, 
     V = np.empty((grid.n_coarse, n))
     S[0], V[0] = s0, v0
     rhoc = math.sqrt(1 - rho * rho)
+    tau = sv_tscale * dt
     with np.errstate(invalid="ignore"):
         for t in range(1, grid.n_fine):
-            if model == "sv_ref":
+            if model == "sv_ref" and sv_tscale > 0:
+                vp = np.maximum(v, 0.0)
+                ly = ly + (mu - 0.5 * vp * vp) * dt + vp * math.sqrt(dt) * W1[:, t]
+                v = v + a * (b - vp) * tau + c * np.sqrt(vp * tau) * W2[:, t]
+            elif model == "sv_ref":
                 arg = v * dt
                 sq = np.sqrt(arg) if parity_nan else np.sqrt(np.maximum(arg, 0.0))
                 v = v + a * (b - v) + c * sq * W2[:, t]
                 ly = ly + (mu - 0.5 * v * v) * dt + v * math.sqrt(dt) * W1[:, t]
+            elif scheme == "qe":
+                dly, v = _qe_step(v, W1[:, t], X2[:, t], dt, mu, kappa, theta, xi, rho)
+                ly = ly + dly
             else:
                 vp = np.maximum(v, 0.0)
                 sv = np.sqrt(vp * dt)

@@ -36,6 +36,7 @@ class DistInfo:
     initialized_here: bool = False
     dp_mode: str = "xgmi"        # xgmi: fused IPC all-reduce in the step kernel; rccl: RCCL + update kernel
     shared_device: bool = False  # several local ranks on ONE GPU (single-GPU rehearsal of the DP path)
+    probe: dict | None = None    # select_transport's probe result (per-rank ok flags, chosen transport)
 
     @property
     def is_main(self) -> bool:
@@ -70,8 +71,12 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count())) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(dev)
+    # the IPC-mapped xGMI mailboxes only reach peers on this node: the in-kernel
+    # exchange is the default only when every rank is local (one node, <= 8 GPUs)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    one_node = local_world == world
     info = DistInfo(rank=rank, world=world, local_rank=local, device=dev,
-                    dp_mode=os.environ.get("RPH_DP", "xgmi" if world <= 8 else "rccl"))
+                    dp_mode=os.environ.get("RPH_DP", "xgmi" if (world <= 8 and one_node) else "rccl"))
     if use_gpu:
         info.shared_device = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) > torch.cuda.device_count()
     if world > 1:
@@ -106,27 +111,54 @@ def _store():
     return c10d._get_default_store() if hasattr(c10d, "_get_default_store") else dist.distributed_c10d._get_default_store()
 
 
+_MBOX_GEN = [0]  # mailboxes created by this process (every rank creates them in the same order)
+
+
 def make_mailbox(info: DistInfo, R: int, tag: str = "rph_mbox"):
-    """IPC mailbox for the fused xGMI all-reduce (None on 1 rank / CPU / rccl mode)."""
+    """IPC mailbox for the fused xGMI all-reduce (None on 1 rank / CPU / rccl mode).
+
+    Collective: every rank calls it in the same order.  The store key carries
+    a per-process generation counter, so a second run in the same process (a
+    sweep, repeated API calls) never picks up a peer's handle from an earlier
+    run; the barrier after the exchange means no rank closes (frees) an old
+    mailbox a peer might still be opening."""
     if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
         return None
     from ..ops.native import IpcMailbox
 
-    mb = IpcMailbox(info.rank, info.world, R, _store(), info.device, tag=tag)
+    _MBOX_GEN[0] += 1
+    err = None
+    try:
+        mb = IpcMailbox(info.rank, info.world, R, _store(), info.device, tag=f"{tag}_g{_MBOX_GEN[0]}")
+    except Exception as e:  # still join the barrier: the peers must not pair it with a later collective
+        mb, err = None, e
+    barrier()
+    if err is not None:
+        raise err
     # ranks sharing one GPU cannot use schedules whose EVERY workgroup waits for
     # the peers (a peer's kernel may find no free CU): engine picks "ticket"
     mb.shared_device = info.shared_device
     return mb
 
 
-def _probe_xgmi(info: DistInfo) -> bool:
-    """Tiny data-parallel fit over the fused xGMI exchange (the default lagged
-    schedule): no peer timeout, and bitwise-identical weights on every rank."""
+def close_mailbox(mb):
+    """Collective teardown of a mailbox: every rank's kernels are done with
+    every peer buffer before any rank frees its own."""
+    if mb is None:
+        return
+    if mb.own is not None and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    barrier()
+    mb.close()
+
+
+def _probe_xgmi_local(info: DistInfo, mb) -> tuple[bool, torch.Tensor | None]:
+    """This rank's half of the probe: a tiny data-parallel fit over the fused
+    xGMI exchange (the default lagged schedule).  Returns (ok, weights)."""
     from ..engine import DateData, FitConfig, HipBackend, TrainConfig
     from ..models.hedge_mlp import NetSpec, init_weights
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
-    mb = make_mailbox(info, spec.red_width, tag="rph_probe")
     try:
         n = 1 << 12
         g = torch.Generator().manual_seed(100 + info.rank)          # different data per rank
@@ -138,34 +170,61 @@ def _probe_xgmi(info: DistInfo) -> bool:
         w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
         be.fit(w, o, f, data, FitConfig(epochs=4, patience=10 ** 6, early_stopping=False), seed=5)
         torch.cuda.synchronize(info.device)
-        if int(mb.error[0].item()) != 0:
-            return False
         wv = w[: spec.nparams].double()
-        mx, mn = wv.clone(), wv.clone()
-        all_reduce_(mx, "max")
-        all_reduce_(mn, "min")
-        return bool(torch.equal(mx, mn)) and bool(torch.isfinite(wv).all())
+        return int(mb.error[0].item()) == 0 and bool(torch.isfinite(wv).all()), wv
     except Exception:
-        return False
-    finally:
-        mb.close()
+        return False, None
 
 
 def select_transport(info: DistInfo) -> str:
     """Probe-then-choose, like a collective library's transport selection: keep
     the in-kernel xGMI exchange when a tiny DP fit over it is clean on every
     rank, otherwise fall back to an RCCL all-reduce of the packet (+ update
-    kernel).  Runs once, outside any timed region; all ranks agree."""
+    kernel).  Runs once, outside any timed region; all ranks agree.
+
+    Every rank issues the SAME collective sequence whatever its local outcome
+    (min of the ok flags, then max/min of the weights, then min of the
+    equality flag), so a failure seen by only some ranks cannot pair
+    mismatched collectives."""
     if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
         return info.dp_mode
-    ok = torch.tensor([1.0 if _probe_xgmi(info) else 0.0], dtype=torch.float64, device=info.device)
+    from ..models.hedge_mlp import NetSpec
+
+    P = NetSpec(nin=1, hidden=8, nout=2, head=0).nparams
+    mb = None
+    try:
+        mb = make_mailbox(info, NetSpec(nin=1, hidden=8, nout=2, head=0).red_width, tag="rph_probe")
+        ok_l, wv = _probe_xgmi_local(info, mb)
+    except Exception:
+        ok_l, wv = False, None
+    ok = torch.tensor([1.0 if ok_l else 0.0], dtype=torch.float64, device=info.device)
     all_reduce_(ok, "min")
-    if float(ok.item()) < 1.0:
+    w = wv if (wv is not None and wv.numel() == P) else torch.zeros(P, dtype=torch.float64, device=info.device)
+    mx, mn = w.clone(), w.clone()
+    all_reduce_(mx, "max")
+    all_reduce_(mn, "min")
+    same = torch.tensor([1.0 if bool(torch.equal(mx, mn)) else 0.0], dtype=torch.float64, device=info.device)
+    all_reduce_(same, "min")
+    try:
+        close_mailbox(mb)
+    except Exception:
+        pass
+    all_ok = float(ok.item()) >= 1.0 and float(same.item()) >= 1.0
+    info.probe = {"local_ok": bool(ok_l), "all_ok": bool(float(ok.item()) >= 1.0),
+                  "bitwise_equal_weights": bool(float(same.item()) >= 1.0), "chosen": "xgmi" if all_ok else "rccl"}
+    if not all_ok:
         from ..ops.native import NcclComm
 
         info.dp_mode = "rccl"
         info.comm = NcclComm(info.rank, info.world, _store(), tag="rph_fallback")
     return info.dp_mode
+
+
+def dist_world() -> int:
+    """World size of the initialised process group (1 without one)."""
+    import torch.distributed as dist
+
+    return dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
 
 
 def shard(n_total: int, world: int, rank: int) -> tuple[int, int]:

@@ -46,7 +46,28 @@ def load_weights(path: str, spec, prefix: str = "") -> np.ndarray:
     return spec.flatten({k: t[prefix + k] for k, _ in spec.shapes()})
 
 
+def _gather_values(run, values: torch.Tensor) -> np.ndarray:
+    """[n_coarse, n_total] on rank 0 from every rank's contiguous shard
+    (collective when data parallel; shards are equal-sized, rank-ordered)."""
+    w = run.di.world
+    if w <= 1:
+        return values.detach().cpu().numpy()
+    import torch.distributed as dist
+
+    v = values.detach().contiguous()
+    if dist.get_backend() == "gloo":
+        v = v.cpu()
+    parts = [torch.empty_like(v) for _ in range(w)]
+    dist.all_gather(parts, v)
+    return torch.cat([p.cpu() for p in parts], dim=1).numpy()
+
+
 def save_run(out_dir: str, run, res, save_values: bool = True):
+    """Write the run directory (rank 0).  Collective when data parallel: the
+    per-rank value shards are gathered so ``values.npy`` holds every path."""
+    vals = None
+    if save_values and res.induction.values is not None:
+        vals = _gather_values(run, res.induction.values)
     if run.di.rank != 0:
         return
     os.makedirs(out_dir, exist_ok=True)
@@ -70,8 +91,8 @@ def save_run(out_dir: str, run, res, save_values: bool = True):
             if run.cfg.train.q99:
                 tensors.update({"q99/" + k: v for k, v in raw(1).items()})
             _save_tensors(os.path.join(out_dir, f"weights_t{i:04d}.safetensors"), tensors)
-    if save_values and res.induction.values is not None:
-        np.save(os.path.join(out_dir, "values.npy"), res.induction.values.detach().cpu().numpy())
+    if vals is not None:
+        np.save(os.path.join(out_dir, "values.npy"), vals)
     rep = {"phi0": res.phi, "psi0": res.psi, "V0": res.v0, "VaR": res.var, "terminal_pnl": res.terminal_pnl,
            "Errors": res.errors.tolist(), "P_E_Values": res.p_e_values.tolist(), "summary": res.summary,
            "dates": [{"index": d.index, "time": d.time, "fit_mse": {k: v for k, v in d.fit_mse.items()

@@ -2,19 +2,28 @@
 
 ``RPH_PROFILE=1`` dumps the phase table as JSON at interpreter exit (SURVEY
 §5.1).  Kernel-level evidence comes from ``rocprofv3 --kernel-trace --stats``:
-every kernel has a distinct name (k_sim_scan / k_hedge_train_step /
-k_hedge_eval / k_radix_hist / ...)."""
+every kernel has a distinct name (k_sim_scan / k_hedge_step_lag /
+k_hedge_eval / k_radix_hist / ...).
+
+Timers register through a weak set, so a sweep that creates one run after
+another does not keep every run's timer (and its recorded GPU events) alive;
+the exit dump reports the timers still alive plus the summaries of the ones
+collected earlier (bounded).
+"""
 from __future__ import annotations
 
 import atexit
 import json
 import os
 import time
+import weakref
 from contextlib import contextmanager
 
 import torch
 
-_ALL = []
+_LIVE: "weakref.WeakSet[PhaseTimer]" = weakref.WeakSet()
+_DONE: list = []          # summaries of collected timers (RPH_PROFILE=1 only)
+_DONE_MAX = 1024
 
 
 class PhaseTimer:
@@ -23,7 +32,14 @@ class PhaseTimer:
         self.device = device
         self.cpu = {}
         self.events = {}
-        _ALL.append(self)
+        _LIVE.add(self)
+
+    def __del__(self):
+        if os.environ.get("RPH_PROFILE") == "1" and len(_DONE) < _DONE_MAX:
+            try:
+                _DONE.append(self.summary())
+            except Exception:
+                pass
 
     @contextmanager
     def phase(self, name: str):
@@ -54,11 +70,15 @@ class PhaseTimer:
         return out
 
 
+def live_timers() -> int:
+    return len(_LIVE)
+
+
 def _dump():
-    if os.environ.get("RPH_PROFILE") == "1" and _ALL:
+    if os.environ.get("RPH_PROFILE") == "1" and (_LIVE or _DONE):
         path = os.environ.get("RPH_PROFILE_OUT", "rph_profile.json")
         with open(path, "w") as f:
-            json.dump([t.summary() for t in _ALL], f, indent=1)
+            json.dump(list(_DONE) + [t.summary() for t in list(_LIVE)], f, indent=1)
 
 
 atexit.register(_dump)

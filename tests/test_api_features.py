@@ -199,6 +199,17 @@ def test_brownian_helpers():
     W = get_W(50, 1)
     assert dW.shape == (50,) and W[0] == 0.0
     np.testing.assert_allclose(W[1:], np.cumsum(dW)[:-1])
+    # the reference's draws: np.random.seed(1); np.random.normal(0, 1, T)
+    # (legacy MT19937 stream; pinned values of seed 1)
+    np.testing.assert_allclose(dW[:3], [1.6243453636632417, -0.6117564136500754, -0.5281717522634557], rtol=0,
+                               atol=1e-15)
+    np.testing.assert_allclose(W[:3], [0.0, 1.6243453636632417, 1.0125889500131663], rtol=0, atol=1e-14)
+    # reseeds the global stream like the reference (side effect included)
+    get_dW(5, 7)
+    a = np.random.normal()
+    np.random.seed(7)
+    np.random.normal(0.0, 1.0, 5)
+    assert a == np.random.normal()
 
 
 def test_cli_calibrate_and_info():
@@ -327,3 +338,19 @@ def test_feature_norm_modes_through_dict_api(mode):
     assert par.induction.norms == []
     with pytest.raises(ValueError):
         HedgeRun(parse_params(_small(feature_norm="bogus"))).build()
+
+
+def test_phase_timer_does_not_leak():
+    import gc
+
+    from rphedge.utils import profiling
+
+    gc.collect()
+    n0 = profiling.live_timers()
+    for _ in range(20):
+        t = profiling.PhaseTimer(enabled=True, device="cpu")
+        with t.phase("x"):
+            pass
+    del t
+    gc.collect()
+    assert profiling.live_timers() == n0

@@ -34,11 +34,13 @@ def test_heston_literature_value():
     assert put == pytest.approx(call - 100.0 + 110.0 * math.exp(-0.05), abs=1e-9)  # put-call parity
 
 
-def _bench(args, env=None, nproc=1):
+def _bench(args, env=None, nproc=1, bare=False):
     e = dict(os.environ, **(env or {}))
     e.setdefault("OMP_NUM_THREADS", "1")
-    if nproc == 1:
-        cmd = [sys.executable, "bench.py"] + args
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    if nproc == 1 or bare:
+        cmd = [sys.executable, "bench.py"] + (["--gpus", str(nproc)] if bare else []) + args
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(29531 + nproc), "bench.py", "--gpus", str(nproc)] + args
@@ -67,4 +69,21 @@ def test_bench_cpu_multi_rank(nproc):
                 "--paths-log2", "12", "--batch-log2", "10", "--cpu"], nproc=nproc)
     assert r["n_gpus"] == nproc and r["config"]["parallelism"] == f"dp{nproc}"
     assert r["config"]["paths_global"] == nproc * (1 << 12) and r["config"]["global_batch"] == nproc * (1 << 10)
+    assert r["config"]["dist_world"] == nproc
     assert math.isfinite(r["quality"]["V0"]) and abs(r["quality"]["V0"] - 10.39) < 1.5
+
+
+@pytest.mark.parametrize("nproc", [2, 4, 8])
+def test_bench_bare_gpus_self_launches(nproc):
+    """``python bench.py --gpus N`` with no torch.distributed environment (the
+    driver's scaling invocation) spawns the N ranks itself; the JSON line and
+    its keys are the same as under an external torch.distributed.run."""
+    args = ["--preset", "euro1_cpu", "--steps", "1", "--warmup", "0", "--epochs-first", "6",
+            "--paths-log2", "11", "--batch-log2", "9", "--cpu"]
+    r = _bench(args, nproc=nproc, bare=True)
+    assert r["n_gpus"] == nproc and r["config"]["dist_world"] == nproc
+    assert r["config"]["paths_global"] == nproc * (1 << 11)
+    if nproc == 4:
+        t = _bench(args, nproc=nproc)
+        assert set(r) == set(t) and set(r["config"]) == set(t["config"]) and set(r["quality"]) == set(t["quality"])
+        assert r["quality"]["V0"] == t["quality"]["V0"]  # same global paths, same ranks: same result

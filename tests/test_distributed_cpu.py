@@ -128,3 +128,57 @@ def test_dead_rank_errors_out_cleanly():
         res = json.load(open(out))
     assert res["status"].startswith("raised"), res
     assert res["elapsed"] < 60
+
+
+def _params(save_dir):
+    from rphedge.experiments import mts_parameters
+
+    return mts_parameters(n_paths=10, dt=0.1, rebalancing=1.0, epochs_first=8, epochs_rest=3, verbose=True,
+                          device="cpu", save_dir=save_dir, batch_size=1024, shuffle=False)
+
+
+def _verbose_save_resume_worker(rank, world, port, out, save_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from rphedge.api import HedgeRun, run_params
+    from rphedge.config import parse_params
+    from rphedge.parallel import dist as D
+
+    D.init(device="cpu", timeout_s=60.0)
+    res = run_params(_params(save_dir))          # verbose: per-date quantiles are collectives on every rank
+    run = HedgeRun(parse_params(_params(None)))
+    r2 = run.resume(save_dir, 5)                 # restart at date 4 from the gathered values.npy
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump({"phi": res.phi, "psi": res.psi, "resumed_phi": r2.phi}, f)
+    D.shutdown()
+
+
+def test_dp_verbose_save_and_resume_two_ranks():
+    """verbose per-date reports run their distributed quantiles on
+    every rank (no rank-0-only collective), values.npy holds every rank's
+    shard, and a data-parallel resume trains each rank on its own shard: the
+    2-rank resume equals the 1-process resume of the same saved run."""
+    world, port = 2, _free_port()
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "res.json")
+        save = os.path.join(td, "run")
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=_verbose_save_resume_worker, args=(r, world, port, out, save))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(240)
+            assert p.exitcode == 0
+        dp = json.load(open(out))
+        vals = np.load(os.path.join(save, "values.npy"))
+        assert vals.shape[1] == 1 << 10            # gathered: both shards
+        from rphedge.api import HedgeRun
+        from rphedge.config import parse_params
+        from rphedge.parallel import dist as D
+
+        run = HedgeRun(parse_params(_params(None)), dist_info=D.DistInfo(device=torch.device("cpu")))
+        r1 = run.resume(save, 5)
+    assert dp["resumed_phi"] == pytest.approx(r1.phi, rel=2e-3)

@@ -104,13 +104,34 @@ def test_sv_and_heston_vs_numpy(dev):
 
     g = P.Grid(T=2.0, dt=1 / 50, rebalancing=0.25)
     for model, kw in [("sv_ref", dict(a=0.0034, b=0.154, c=0.0158)),
-                      ("heston", dict(kappa=2.0, theta=0.04, xi=0.3, rho=-0.7))]:
+                      ("sv_ref", dict(a=0.0034, b=0.154, c=0.0158, sv_tscale=252.0)),
+                      ("heston", dict(kappa=2.0, theta=0.04, xi=0.3, rho=-0.7, scheme="euler")),
+                      ("heston", dict(kappa=2.0, theta=0.04, xi=0.3, rho=-0.7, scheme="qe")),
+                      ("heston", dict(kappa=1.0, theta=0.04, xi=0.9, rho=-0.5, scheme="qe"))]:  # QE exp. branch
         gp = P.simulate_sv(g, 2048, 1.0, 0.09, 0.16 if model == "sv_ref" else 0.04, model=model, device=dev,
                            fp64=True, **kw)
         cp = P.simulate_sv(g, 2048, 1.0, 0.09, 0.16 if model == "sv_ref" else 0.04, model=model, device="cpu",
                            **kw)
         np.testing.assert_allclose(gp.S.cpu().numpy(), cp.S.numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(gp.vol.cpu().numpy(), cp.vol.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_heston_qe_price_matches_semi_analytic(dev):
+    """BASELINE config #3 quality anchor: the heston30 paths (30 dates x 10
+    substeps, 2^20 Sobol paths, fp32, Andersen QE) price the call within 3
+    standard errors of the semi-closed-form Heston price 10.1546 (full-
+    truncation Euler sat 1.3 % above it)."""
+    from rphedge.analytic import heston_call
+    from rphedge.ops import paths as P
+
+    g = P.Grid(T=1.0, dt=1 / 300, rebalancing=1 / 30)
+    kw = dict(kappa=2.0, theta=0.04, xi=0.5, rho=-0.7)
+    ref, _ = heston_call(100.0, 100.0, 0.05, 1.0, kw["kappa"], kw["theta"], kw["xi"], kw["rho"], 0.04)
+    p = P.simulate_sv(g, 1 << 20, 100.0, 0.05, 0.04, model="heston", norm=100.0, device=dev, scheme="qe", **kw)
+    pay = (p.S_final.double() * 100.0 - 100.0).clamp_min(0.0) * math.exp(-0.05)
+    se = float(pay.std()) / math.sqrt(pay.numel())
+    assert abs(float(pay.mean()) - ref) < 3 * se, (float(pay.mean()), ref, se)
+    assert abs(ref - 10.1546) < 1e-3
 
 
 def test_basket_vs_numpy(dev):
