@@ -172,6 +172,21 @@ def self_launch(n: int, argv=None) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def delta_anchor(run, cfg) -> dict | None:
+    """Black–Scholes delta hedge on the same simulated grid and paths (GBM
+    European presets): its self-financing P&L std and one-step residual std
+    are the analytic floor the learnt hedge is compared against (x S0)."""
+    if cfg.model not in ("gbm", "gbm_log") or run.kind != "european":
+        return None
+    from rphedge import analytic
+
+    p = run.paths
+    a = analytic.bs_delta_hedge(p.S, p.bond, cfg.K / cfg.Y, cfg.r, cfg.sigma, cfg.T, run.grid.times(),
+                                cfg.option_type, payoff=run.v_terminal, world=run.di.world)
+    return {"pnl_std": a["pnl_std"] * cfg.Y, "pnl_mean": a["pnl_mean"] * cfg.Y,
+            "residual_std_last": a["residual_std_last"] * cfg.Y, "price": a["price"] * cfg.Y}
+
+
 def main(argv=None):
     a = parse(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -271,8 +286,11 @@ def main(argv=None):
                    "dp_probe": probe, "dist_world": D.dist_world(),
                    "launch": "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1 else "single"},
         "quality": {"terminal_pnl_std": res.terminal_pnl["std"], "terminal_pnl_mean": res.terminal_pnl["mean"],
+                    "terminal_pnl_kind": res.terminal_pnl.get("kind"),
+                    "terminal_residual_std": res.terminal_residual["std"],
+                    "terminal_residual_mean": res.terminal_residual["mean"],
                     "V0": res.v0, "phi0": res.phi, "psi0": res.psi,
-                    "anchor": anchor(cfg),
+                    "anchor": anchor(cfg), "delta_hedge_anchor": delta_anchor(run, cfg),
                     "mc_discounted_payoff": res.summary["E_payoff"] * run.scale * math.exp(-cfg.r * cfg.T),
                     "reference_terminal_pnl_std_52step": 1.7504, "reference_V0": 11.352},
         "paths_per_sec_full_run": n_total / (ms / 1000.0),

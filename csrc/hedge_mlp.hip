@@ -353,6 +353,12 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
     if (has_b) wl[WBOFF + i] = d.wb->w[0][i];
   }
   __syncthreads();
+  if (blockIdx.x == 0) {  // per-date weight snapshots (saved-model format, P&L scan)
+    for (int i = threadIdx.x; i < S::P; i += 256) {
+      if (d.snap_a) d.snap_a->w[0][i] = wl[i];
+      if (d.snap_b) d.snap_b->w[0][i] = has_b ? wl[WBOFF + i] : wl[i];
+    }
+  }
   const float* __restrict__ WA = wl;
   const float* __restrict__ WB = has_b ? wl + WBOFF : wl;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -479,6 +485,129 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
     else if (i == ES_RESMAX) v = fmax(fmax(sst[0][i], sst[1][i]), fmax(sst[2][i], sst[3][i]));
     else v = sst[0][i] + sst[1][i] + sst[2][i] + sst[3][i];
     d.stats[(size_t)blockIdx.x * EVAL_NSTAT + i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Self-financing hedge P&L scan (PnlDesc, rph_types.h): one thread per path
+// (PPT paths per thread), dates in lockstep per workgroup so each date's
+// network(s) are staged once in LDS.  Wealth starts at V_0, holds the traded-
+// asset holdings of date t's network and keeps the remainder in the bank
+// account; P&L_T = W_T - liability.  Per-workgroup fp64 statistics in the
+// eval-stats layout (ES_V = W_T, ES_RES = P&L).  Not a hot path (one pass per
+// run, a few hundred VALU flops per path and date); the corrected counterpart
+// of the reference's one-step "P&L" (Q24, Replicating_Portfolio.py:120).
+// ---------------------------------------------------------------------------
+constexpr int PNL_PPT = 4;
+
+template <int NIN, int H, int NO, int HEAD>
+__global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
+  using S = NetShape<NIN, H, NO, HEAD>;
+  constexpr int NHOLD = S::NHOLD;
+  constexpr int NA = NHOLD - 1;  // traded assets (the last holding is the bank account)
+  constexpr int WBOFF = (S::P + 3) / 4 * 4;
+  prefetch_kernarg<sizeof(PnlDesc)>();
+  RPH_DASSERT(d.n_local > 0 && d.num_wgs == (int)gridDim.x && d.snap != nullptr && d.stats != nullptr);
+  __shared__ __attribute__((aligned(16))) float wl[WBOFF + S::P + 4];
+  __shared__ double sred[4][8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const long long base = (long long)blockIdx.x * 256 * PNL_PPT + tid;
+  const bool has_b = d.has_b != 0;
+  float wealth[PNL_PPT];
+#pragma unroll
+  for (int j = 0; j < PNL_PPT; ++j) {
+    const long long p = base + (long long)j * 256;
+    wealth[j] = p < d.n_local ? (d.w0 ? d.w0[p] : d.wealth0) : 0.f;
+  }
+  for (int t = 0; t < d.n_dates; ++t) {
+    __syncthreads();  // every thread is done with date t-1's weights
+    const NetWeights* wt = d.snap + (size_t)t * 2;
+    for (int i = tid; i < S::P; i += 256) {
+      wl[i] = wt[0].w[0][i];
+      if (has_b) wl[WBOFF + i] = wt[1].w[0][i];
+    }
+    __syncthreads();
+    float mu[NIN], isd[NIN];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) {
+      mu[f] = d.fmu[t * MAXIN + f];
+      isd[f] = d.fisd[t * MAXIN + f];
+    }
+    const float grow = (float)(d.bond[t + 1] / d.bond[t]);
+#pragma unroll
+    for (int j = 0; j < PNL_PPT; ++j) {
+      const long long p = base + (long long)j * 256;
+      if (p >= d.n_local) continue;
+      uint32_t zo = 0;  // opaque zero: weights stay in LDS (broadcast reads), not hoisted into VGPRs
+      asm volatile("" : "+v"(zo));
+      const float* __restrict__ WA = (const float*)__builtin_assume_aligned(wl + (zo & ~3u), 16);
+      const float* __restrict__ WB = (const float*)__builtin_assume_aligned(wl + WBOFF + (zo & ~3u), 16);
+      float x[NIN];
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) x[f] = (d.feat[f][(long long)t * d.feat_ts[f] + p] - mu[f]) * isd[f];
+      float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], hb[NHOLD];
+      net_forward<NIN, H, NO, HEAD>(WA, x, d.alpha, z1, a1, z2, a2, hold);
+      if (has_b) {
+        net_forward<NIN, H, NO, HEAD>(WB, x, d.alpha, z1, a1, z2, a2, hb);
+#pragma unroll
+        for (int k = 0; k < NHOLD; ++k) hold[k] = hold[k] + d.hold_c * (hb[k] - hold[k]);
+      }
+      float w = wealth[j] * grow;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const float s0 = d.price[a][(long long)t * d.price_ts[a] + p];
+        const float s1 = d.price[a][(long long)(t + 1) * d.price_ts[a] + p];
+        w = fmaf(hold[a], s1 - s0 * grow, w);
+      }
+      wealth[j] = w;
+    }
+  }
+  // P&L and per-workgroup fp64 statistics
+  double sv = 0, sv2 = 0, sp = 0, sp2 = 0, sa = 0, cnt = 0;
+  float pmin = INFINITY, pmax = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < PNL_PPT; ++j) {
+    const long long p = base + (long long)j * 256;
+    if (p >= d.n_local) continue;
+    const float pnl = wealth[j] - d.payoff[p];
+    if (d.pnl_out) d.pnl_out[p] = pnl;
+    sv += wealth[j];
+    sv2 += (double)wealth[j] * wealth[j];
+    sp += pnl;
+    sp2 += (double)pnl * pnl;
+    sa += fabsf(pnl);
+    cnt += 1.0;
+    pmin = fminf(pmin, pnl);
+    pmax = fmaxf(pmax, pnl);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    sv += __shfl_xor(sv, o, 64);
+    sv2 += __shfl_xor(sv2, o, 64);
+    sp += __shfl_xor(sp, o, 64);
+    sp2 += __shfl_xor(sp2, o, 64);
+    sa += __shfl_xor(sa, o, 64);
+    cnt += __shfl_xor(cnt, o, 64);
+    pmin = fminf(pmin, __shfl_xor(pmin, o, 64));
+    pmax = fmaxf(pmax, __shfl_xor(pmax, o, 64));
+  }
+  if (lane == 0) {
+    sred[wid][0] = sv; sred[wid][1] = sv2; sred[wid][2] = sp; sred[wid][3] = sp2;
+    sred[wid][4] = sa; sred[wid][5] = cnt; sred[wid][6] = pmin; sred[wid][7] = pmax;
+  }
+  __syncthreads();
+  if (tid < EVAL_NSTAT) {
+    double v = 0.0;
+    auto sum4 = [&](int k) { return (sred[0][k] + sred[1][k]) + (sred[2][k] + sred[3][k]); };
+    if (tid == ES_V) v = sum4(0);
+    else if (tid == ES_V2) v = sum4(1);
+    else if (tid == ES_RES) v = sum4(2);
+    else if (tid == ES_RES2) v = sum4(3);
+    else if (tid == ES_ABSRES) v = sum4(4);
+    else if (tid == ES_COUNT) v = sum4(5);
+    else if (tid == ES_RESMIN) v = fmin(fmin(sred[0][6], sred[1][6]), fmin(sred[2][6], sred[3][6]));
+    else if (tid == ES_RESMAX) v = fmax(fmax(sred[0][7], sred[1][7]), fmax(sred[2][7], sred[3][7]));
+    d.stats[(size_t)blockIdx.x * EVAL_NSTAT + tid] = v;
   }
 }
 
@@ -652,6 +781,31 @@ extern "C" int rph_eval(const EvalDesc* d, void* stream) {
       }                                                                                        \
     }                                                                                          \
     hipLaunchKernelGGL((k_hedge_eval<A, B, C, E, false>), dim3(d->num_wgs), dim3(256), 0, s, *d); \
+    return (int)hipGetLastError();                                                             \
+  }
+  RPH_SHAPES(X)
+  RPH_WIDE_SHAPES(X)
+#undef X
+  return -1;
+}
+
+extern "C" int rph_pnl(const PnlDesc* d, void* stream) {
+  const int nhold = d->head == HEAD_COMPLEMENT ? 2 : d->nout;
+  if (!d->snap || !d->stats || !d->payoff || !d->fmu || !d->fisd || !d->bond || d->n_local < 1 || d->n_dates < 1 ||
+      d->nin < 1 || d->nin > MAXIN || nhold < 2 || nhold > MAXHOLD)
+    return rph_report("rph_pnl", "bad P&L descriptor");
+  if (!(d->alpha >= 0.f && d->alpha <= 1.f)) return rph_report("rph_pnl", "LeakyReLU slope must be in [0, 1]");
+  for (int f = 0; f < d->nin; ++f)
+    if (!d->feat[f] || d->feat_ts[f] < 0) return rph_report("rph_pnl", "null feature pointer / negative stride");
+  for (int k = 0; k < nhold - 1; ++k)
+    if (!d->price[k] || d->price_ts[k] < d->n_local) return rph_report("rph_pnl", "null price pointer / bad stride");
+  const long long per_wg = 256LL * PNL_PPT;
+  if ((long long)d->num_wgs * per_wg < d->n_local || (long long)(d->num_wgs - 1) * per_wg >= d->n_local)
+    return rph_report("rph_pnl", "num_wgs does not match n_local / (256 * PNL_PPT)");
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                          \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                 \
+    hipLaunchKernelGGL((k_hedge_pnl<A, B, C, E>), dim3(d->num_wgs), dim3(256), 0, s, *d);     \
     return (int)hipGetLastError();                                                             \
   }
   RPH_SHAPES(X)

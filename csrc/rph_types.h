@@ -134,6 +134,39 @@ struct EvalDesc {
   int nin, h, nout, head;
   float fmu[MAXIN];              // input standardisation x' = (x - fmu) * fisd (identity: 0 / 1)
   float fisd[MAXIN];
+  // per-date weight snapshots for the saved-model format and the P&L scan:
+  // workgroup 0 copies the P current weights of wa / wb into w[0] of these
+  // NetWeights blocks (may be null) - no separate copy launch per date
+  NetWeights* snap_a;
+  NetWeights* snap_b;
+};
+
+// Self-financing hedge P&L scan (k_hedge_pnl): one forward pass over the
+// rebalancing dates with the per-date networks.  Wealth starts at V_0 (the
+// fitted date-0 value), holds phi_t (the traded-asset holdings of date t's
+// network, blended hA + hold_c (hB - hA) when a second network is given) and
+// keeps the rest in the bank account:
+//   W_{t+1} = sum_a phi_a,t S_a,t+1 + (W_t - sum_a phi_a,t S_a,t) B_{t+1} / B_t
+//   P&L_T   = W_T - V_T(payoff)
+// Element (t, p) of feature f lives at feat[f][t * feat_ts[f] + p] (the
+// time-major coarse grids), likewise for the traded prices.
+struct PnlDesc {
+  const float* feat[MAXIN];
+  long long feat_ts[MAXIN];
+  const float* price[MAXHOLD];   // traded assets (bond excluded)
+  long long price_ts[MAXHOLD];
+  const NetWeights* snap;        // [n_dates][2] per-date networks (A at [t][0], B at [t][1])
+  const float* fmu;              // [n_dates][MAXIN] per-date standardisation
+  const float* fisd;
+  const double* bond;            // [n_dates + 1] B_t on the coarse grid
+  const float* w0;               // initial wealth per path (values[0]); null: wealth0 scalar
+  const float* payoff;           // terminal liability per path (values[n_dates])
+  float* pnl_out;                // per-path P&L (may be null)
+  double* stats;                 // [num_wgs][EVAL_NSTAT]: ES_V = W_T, ES_RES = P&L, ...
+  float alpha, hold_c, wealth0;
+  int has_b;
+  int n_local, n_dates, num_wgs;
+  int nin, h, nout, head;
 };
 
 // Eval stats slab columns

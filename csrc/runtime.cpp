@@ -61,6 +61,11 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(EvalDesc, wa), OFF(EvalDesc, g_base), OFF(EvalDesc, v_out), OFF(EvalDesc, hold_out),
       OFF(EvalDesc, resid_out), OFF(EvalDesc, pred1_out), OFF(EvalDesc, stats), OFF(EvalDesc, bond_t),
       OFF(EvalDesc, hold_c), OFF(EvalDesc, n_local), OFF(EvalDesc, head), OFF(EvalDesc, fmu), OFF(EvalDesc, fisd),
+      OFF(EvalDesc, snap_a), OFF(EvalDesc, snap_b),
+      // PnlDesc
+      (long long)sizeof(PnlDesc), OFF(PnlDesc, feat_ts), OFF(PnlDesc, price), OFF(PnlDesc, price_ts),
+      OFF(PnlDesc, snap), OFF(PnlDesc, bond), OFF(PnlDesc, pnl_out), OFF(PnlDesc, stats), OFF(PnlDesc, alpha),
+      OFF(PnlDesc, has_b), OFF(PnlDesc, n_dates), OFF(PnlDesc, head),
       // SimDesc
       (long long)sizeof(SimDesc), OFF(SimDesc, path_offset), OFF(SimDesc, sv1), OFF(SimDesc, dims1),
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),

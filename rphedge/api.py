@@ -47,6 +47,8 @@ class RunResult:
     timings: dict = field(default_factory=dict)
     config: dict = field(default_factory=dict)
     paths: object = None                   # ops.paths.Paths of this rank (plots, C32)
+    terminal_residual: dict = field(default_factory=dict)   # one-step residual at the last date (Q24)
+    self_financing_pnl: dict | None = None                   # W_T - liability of the reported hedge
 
     def as_tuple(self):
         return self.phi, self.psi
@@ -408,12 +410,25 @@ class HedgeRun:
             # psi in unit bonds (B_0 = 1): parity head already counts unit bonds
             bond_unit = 1.0 if c.parity.complement_head else c.Y
             phi, psi = float(h0[0]), float(h0[-1] * bond_unit)
-        term = ind.terminal
-        tp = {"mean": term.residual_mean * scale, "std": term.residual_std * scale,
-              "min": float(term.stats[L.ES_RESMIN]) * scale, "max": float(term.stats[L.ES_RESMAX]) * scale}
+        def pnl_dict(dr):
+            return {"mean": dr.residual_mean * scale, "std": dr.residual_std * scale,
+                    "min": float(dr.stats[L.ES_RESMIN]) * scale, "max": float(dr.stats[L.ES_RESMAX]) * scale}
+
+        # one-step residual of the last date (the reference's "P&L at T", Q24)
+        # and the self-financing hedge P&L W_T - liability (corrected default)
+        resid = pnl_dict(ind.terminal)
+        sf = pnl_dict(ind.pnl) if ind.pnl is not None else None
+        if sf is not None:
+            sf["mean_terminal_wealth"] = ind.pnl.mean_value * scale
+        tp = dict(resid) if (c.parity.local_residual_pnl or sf is None) else dict(sf)
+        tp["kind"] = "one_step_residual" if (c.parity.local_residual_pnl or sf is None) else "self_financing"
         var = {}
         if ind.residuals is not None and c.keep_paths:
             var = risk.var_report(ind.residuals, scale=scale, world=w)
+            if ind.pnl_paths is not None:
+                q = risk.quantile(ind.pnl_paths, (0.01, 0.015, 0.02, 0.05), w)
+                var["self_financing_pnl_quantiles"] = {"q": [0.01, 0.015, 0.02, 0.05],
+                                                       "values": [float(x) * scale for x in q]}
         dtc = self.grid.dt_coarse
         pe = expected_value_trajectory(ind, self.stats0["E_payoff"], c.mu if self.kind == "pension" else c.r, c.r,
                                        dtc)
@@ -421,7 +436,8 @@ class HedgeRun:
         summary.update({"V0": ind.v0 * scale, "phi0": phi, "psi0": psi, "n_paths": self.n_total,
                         "n_dates": self.paths.n_coarse - 1, "reduction": self.grid.reduction,
                         "epochs_mse": [d.fit_mse["epochs"] for d in ind.dates],
-                        "terminal_pnl_std": tp["std"]})
+                        "terminal_pnl_std": tp["std"], "terminal_residual_std": resid["std"],
+                        "self_financing_pnl_std": sf["std"] if sf is not None else None})
         if self.kind == "european":
             from .utils.reports import black_scholes
 
@@ -429,7 +445,8 @@ class HedgeRun:
             summary["bs_price"], summary["bs_delta"] = bs
         return RunResult(phi=phi, psi=psi, v0=ind.v0 * scale, scale=scale, holdings0=h0, induction=ind,
                          errors=error_history(ind), p_e_values=pe, terminal_pnl=tp, var=var, summary=summary,
-                         timings=self.timer.summary(), config=c.to_dict(), paths=self.paths)
+                         timings=self.timer.summary(), config=c.to_dict(), paths=self.paths,
+                         terminal_residual=resid, self_financing_pnl=sf)
 
 
 # ---------------------------------------------------------------------------

@@ -33,7 +33,8 @@ class ParityFlags:
     warm_start: bool = True             # Q18: one network refit at every date (weights + Adam persist)
     restore_best_at_end: bool = False   # Keras-2: restore best weights only on early stop
     numpy_binomial: bool = False        # Q20: numpy MT19937 reseeded 1234+t (CPU oracle only)
-    local_residual_pnl: bool = True     # Q24: "P&L at T" is the one-step residual
+    local_residual_pnl: bool = False    # Q24: report the one-step residual as "the P&L at T" (reference);
+                                        # False = the self-financing hedge P&L (driver k_hedge_pnl scan)
     complement_head: bool = False       # Q13: European psi = 1 - phi head
     eo_discount_artifact: bool = False  # Q14: report V0*e^{-rT} as "discounted E[V(T)]"
     raw_features: bool = False          # reference nets see raw (unstandardised) state features

@@ -23,8 +23,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from .engine import (DateData, FitConfig, TrainConfig, fit_seed, fit_summary, geometric_lr_schedule,
-                     keras_lr_schedule, reduce_stats)
+from .engine import (MAXIN, DateData, FitConfig, PnlData, TrainConfig, fit_seed, fit_summary,
+                     geometric_lr_schedule, keras_lr_schedule, reduce_stats)
 from .models.hedge_mlp import NetSpec
 from .ops import layout as L
 from .ops.paths import Paths
@@ -49,7 +49,6 @@ class InductionConfig:
     warm_start: bool = True              # Q18
     restore_best_at_end: bool = False
     keep_paths: bool = True              # values / holdings / residual arrays
-    snapshot_weights: bool = True        # per-date weights for the saved-model format
     poll_every: int = 0                  # host early-stop polling (0 = async)
     seed: int = 1234
     # input standardisation (fused into the kernels' feature loads):
@@ -105,7 +104,9 @@ class InductionResult:
     weights_snapshots: torch.Tensor | None = None  # [n_coarse-1, 2, NETW]
     v0: float = float("nan")
     holdings0: np.ndarray | None = None
-    terminal: DateResult | None = None
+    terminal: DateResult | None = None             # one-step residual of the last date (Q24 "P&L")
+    pnl: DateResult | None = None                  # self-financing P&L: stats in the eval layout (ES_RES = P&L)
+    pnl_paths: torch.Tensor | None = None          # [n_local] per-path self-financing P&L (keep_paths)
 
 
 class BackwardInduction:
@@ -140,8 +141,9 @@ class BackwardInduction:
         self.opt_init = backend.new_opt()
         self.fits = [[backend.new_fit(), backend.new_fit()] for _ in range(self.n_dates)]
         self.stats = [[backend.new_stats(), backend.new_stats()] for _ in range(self.n_dates)]
-        self.snap = torch.zeros(self.n_dates, 2, L.NETW_FLOATS, dtype=torch.float32, device=dev) \
-            if icfg.snapshot_weights else None
+        # per-date weights (written by the final eval of each date): saved-model
+        # format and the self-financing P&L scan
+        self.snap = torch.zeros(self.n_dates, 2, L.NETW_FLOATS, dtype=torch.float32, device=dev)
         if icfg.lr_schedule_first:
             self.lr_first = tuple(keras_lr_schedule(icfg.epochs_first))
         else:
@@ -150,6 +152,25 @@ class BackwardInduction:
         self.lr_rest = geometric_lr_schedule(icfg.lr_rest or icfg.lr, icfg.epochs_rest, icfg.lr_decay) \
             if (icfg.lr_rest > 0 or icfg.lr_decay != 1.0) else None
         self.norms = feature_norms(paths, icfg.feature_norm, world)
+        # self-financing P&L scan inputs (device tables built once, outside any capture)
+        nd, nin = self.n_dates, spec.nin
+        fmu = np.zeros((nd, MAXIN), np.float32)
+        fisd = np.ones((nd, MAXIN), np.float32)
+        for t, (mu, isd) in enumerate(self.norms):
+            fmu[t, :nin], fisd[t, :nin] = mu, isd
+        self.pnl_data = PnlData(n_dates=nd, features=paths.features, prices=paths.prices,
+                                bond=torch.tensor(np.asarray(paths.bond, np.float64), device=dev),
+                                fmu=torch.from_numpy(fmu).to(dev), fisd=torch.from_numpy(fisd).to(dev),
+                                w0=self.values[0], payoff=self.values[nc - 1])
+        self.pnl_stats = backend.new_pnl_stats()
+        self.pnl_paths = torch.empty(n, dtype=torch.float32, device=dev) if keep else None
+        self.pnl_done = False
+
+    @property
+    def hold_c(self) -> float:
+        """Reported holdings hA + hold_c (hB - hA) (get_phi_psi_VaR, RP:114-115; Q2 sign)."""
+        c = self.cfg
+        return -c.cost_of_capital if c.holdings_blend_sign_rp else c.cost_of_capital
 
     def _fcfg(self, first: bool, loss: int) -> FitConfig:
         c = self.cfg
@@ -209,15 +230,17 @@ class BackwardInduction:
                 else:
                     be.fit(self.w_q, self.opt_q, f_q, data, self._fcfg(first, L.LOSS_PINBALL),
                            seed=fit_seed(c.seed, t, 1), poll_every=c.poll_every)
-                hc = -c.cost_of_capital if c.holdings_blend_sign_rp else c.cost_of_capital
                 be.eval(self.w_mse, data, s_q, wts_b=self.w_q, g_base=self.gbuf, blend_c=c.cost_of_capital,
-                        hold_c=hc, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out)
+                        hold_c=self.hold_c, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out,
+                        snap_a=self.snap[t, 0], snap_b=self.snap[t, 1])
             else:
-                be.eval(self.w_mse, data, s_q, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out)
-            if self.snap is not None:
-                self.snap[t, 0].copy_(self.w_mse)
-                if c.q99:
-                    self.snap[t, 1].copy_(self.w_q)
+                be.eval(self.w_mse, data, s_q, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out,
+                        snap_a=self.snap[t, 0])
+        # self-financing P&L of the reported holdings (needs every date's network)
+        self.pnl_done = start == nc - 2
+        if self.pnl_done:
+            be.pnl(self.snap, self.pnl_data, self.pnl_stats, has_b=c.q99, hold_c=self.hold_c,
+                   pnl_out=self.pnl_paths)
 
     def collect(self) -> InductionResult:
         c = self.cfg
@@ -237,6 +260,10 @@ class BackwardInduction:
         res.terminal = res.dates[0]
         res.v0 = d0.mean_value
         res.holdings0 = d0.mean_holdings(self.spec.nhold)
+        if self.pnl_done:
+            res.pnl = DateResult(index=-1, time=float(self.paths.grid.times()[-1]),
+                                 stats=reduce_stats(self.pnl_stats, self.world))
+            res.pnl_paths = self.pnl_paths
         return res
 
 

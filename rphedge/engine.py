@@ -138,6 +138,24 @@ class DateData:
     fisd: tuple = ()
 
 
+@dataclass
+class PnlData:
+    """Inputs of the self-financing P&L scan (k_hedge_pnl / TorchBackend.pnl)."""
+
+    n_dates: int
+    features: object               # t -> list of [n_local] state-feature tensors at date t (raw)
+    prices: object                 # t -> list of [n_local] traded-asset tensors at date t (bond excluded)
+    bond: torch.Tensor             # [n_dates + 1] float64 bank account B_t (device)
+    fmu: torch.Tensor              # [n_dates, MAXIN] float32 per-date standardisation (device)
+    fisd: torch.Tensor             # [n_dates, MAXIN]
+    w0: torch.Tensor               # [n_local] initial wealth (the fitted V_0)
+    payoff: torch.Tensor           # [n_local] terminal liability
+
+
+PNL_PPT = 4  # paths per thread of k_hedge_pnl (csrc/hedge_mlp.hip PNL_PPT)
+MAXIN = 8
+
+
 def _set_norm(d, data: DateData):
     for i, (m, s) in enumerate(zip(data.fmu, data.fisd)):
         d.fmu[i], d.fisd[i] = float(m), float(s)
@@ -465,10 +483,41 @@ class HipBackend:
             raise RuntimeError("persistent fit kernel: workgroups not co-resident (wait timed out); "
                                "use TrainConfig.step_mode='lag' or 'ticket'")
 
+    def pnl_wgs(self) -> int:
+        return (self.n_local + 256 * PNL_PPT - 1) // (256 * PNL_PPT)
+
+    def new_pnl_stats(self):
+        return torch.zeros(self.pnl_wgs(), L.EVAL_NSTAT, dtype=torch.float64, device=self.device)
+
+    def pnl(self, snap, data: PnlData, stats, has_b: bool = False, hold_c: float = 0.0, pnl_out=None):
+        """Enqueue the self-financing P&L scan (one k_hedge_pnl launch)."""
+        n = self.native
+        d = n.PnlDesc()
+        f1 = data.features(1) if data.n_dates >= 1 else data.features(0)
+        for i, f in enumerate(data.features(0)):
+            d.feat[i] = f.data_ptr()
+            d.feat_ts[i] = (f1[i].data_ptr() - f.data_ptr()) // 4
+        p0, p1 = data.prices(0), data.prices(1)
+        for k, p in enumerate(p0):
+            d.price[k] = p.data_ptr()
+            d.price_ts[k] = (p1[k].data_ptr() - p.data_ptr()) // 4
+        d.snap = snap.data_ptr()
+        d.fmu, d.fisd, d.bond = data.fmu.data_ptr(), data.fisd.data_ptr(), data.bond.data_ptr()
+        d.w0, d.payoff = data.w0.data_ptr(), data.payoff.data_ptr()
+        d.pnl_out = pnl_out.data_ptr() if pnl_out is not None else None
+        d.stats = stats.data_ptr()
+        d.alpha, d.hold_c, d.wealth0, d.has_b = float(self.spec.alpha), float(hold_c), 0.0, 1 if has_b else 0
+        d.n_local, d.n_dates, d.num_wgs = self.n_local, int(data.n_dates), self.pnl_wgs()
+        d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
+        assert stats.shape[0] == d.num_wgs and snap.shape[0] >= data.n_dates
+        n.pnl(d, self.stream)
+
     def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
-             v_out=None, hold_out=None, resid_out=None, pred1_out=None):
+             v_out=None, hold_out=None, resid_out=None, pred1_out=None, snap_a=None, snap_b=None):
         n = self.native
         d = n.EvalDesc()
+        d.snap_a = snap_a.data_ptr() if snap_a is not None else None
+        d.snap_b = snap_b.data_ptr() if snap_b is not None else None
         for i, f in enumerate(data.feats):
             d.feat[i] = f.data_ptr()
         for i, p in enumerate(data.prices_now):
@@ -642,10 +691,51 @@ class TorchBackend:
         fit[L.F_HIST:L.F_HIST + k] = torch.tensor(hist[:k], dtype=torch.float32)
         _ = stopped
 
-    def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
-             v_out=None, hold_out=None, resid_out=None, pred1_out=None):
+    def pnl_wgs(self) -> int:
+        return 1
+
+    def new_pnl_stats(self):
+        return torch.zeros(1, L.EVAL_NSTAT, dtype=torch.float64, device=self.device)
+
+    def pnl(self, snap, data: PnlData, stats, has_b: bool = False, hold_c: float = 0.0, pnl_out=None):
+        """Self-financing P&L scan (reference semantics of k_hedge_pnl)."""
         spec, dt = self.spec, torch.float32
         P = spec.nparams
+        bond = data.bond.detach().cpu().double().numpy()
+        fmu, fisd = data.fmu.detach().cpu(), data.fisd.detach().cpu()
+        wealth = data.w0.to(dt).clone()
+        with torch.no_grad():
+            for t in range(data.n_dates):
+                X = torch.stack([f.to(dt) for f in data.features(t)], dim=1)
+                X = (X - fmu[t, : spec.nin].to(dt)) * fisd[t, : spec.nin].to(dt)
+                hold = torch_forward(spec, snap[t, 0, :P].to(dt), X)
+                if has_b:
+                    hb = torch_forward(spec, snap[t, 1, :P].to(dt), X)
+                    hold = hold + hold_c * (hb - hold)
+                grow = float(bond[t + 1] / bond[t])
+                w = wealth * grow
+                for a, (s0, s1) in enumerate(zip(data.prices(t), data.prices(t + 1))):
+                    w = w + hold[:, a] * (s1.to(dt) - s0.to(dt) * grow)
+                wealth = w
+            pnl = wealth - data.payoff.to(dt)
+            if pnl_out is not None:
+                pnl_out.copy_(pnl)
+            st = torch.zeros(L.EVAL_NSTAT, dtype=torch.float64)
+            wd, pd = wealth.double(), pnl.double()
+            st[L.ES_V], st[L.ES_V2] = wd.sum(), (wd * wd).sum()
+            st[L.ES_RES], st[L.ES_RES2], st[L.ES_ABSRES] = pd.sum(), (pd * pd).sum(), pd.abs().sum()
+            st[L.ES_COUNT] = pd.numel()
+            st[L.ES_RESMIN], st[L.ES_RESMAX] = pd.min(), pd.max()
+            stats[0].copy_(st)
+
+    def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
+             v_out=None, hold_out=None, resid_out=None, pred1_out=None, snap_a=None, snap_b=None):
+        spec, dt = self.spec, torch.float32
+        P = spec.nparams
+        if snap_a is not None:
+            snap_a.copy_(wts)
+        if snap_b is not None:
+            snap_b.copy_(wts_b if wts_b is not None else wts)
         X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
 
         def cw(t):

@@ -60,12 +60,24 @@ class EvalDesc(C.Structure):
         ("hold_c", C.c_float),
         ("n_local", C.c_int), ("num_wgs", C.c_int), ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int),
         ("head", C.c_int), ("fmu", C.c_float * MAXIN), ("fisd", C.c_float * MAXIN),
+        ("snap_a", VP), ("snap_b", VP),
     ]
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
         for f in range(MAXIN):
             self.fisd[f] = 1.0
+
+
+class PnlDesc(C.Structure):
+    _fields_ = [
+        ("feat", VP * MAXIN), ("feat_ts", C.c_longlong * MAXIN), ("price", VP * MAXHOLD),
+        ("price_ts", C.c_longlong * MAXHOLD), ("snap", VP), ("fmu", VP), ("fisd", VP), ("bond", VP),
+        ("w0", VP), ("payoff", VP), ("pnl_out", VP), ("stats", VP),
+        ("alpha", C.c_float), ("hold_c", C.c_float), ("wealth0", C.c_float), ("has_b", C.c_int),
+        ("n_local", C.c_int), ("n_dates", C.c_int), ("num_wgs", C.c_int),
+        ("nin", C.c_int), ("h", C.c_int), ("nout", C.c_int), ("head", C.c_int),
+    ]
 
 
 class SimDesc(C.Structure):
@@ -100,6 +112,10 @@ def _expected_layout() -> list[int]:
         C.sizeof(E), E.price_t.offset, E.price_t1.offset, E.target.offset, E.wa.offset, E.g_base.offset,
         E.v_out.offset, E.hold_out.offset, E.resid_out.offset, E.pred1_out.offset, E.stats.offset,
         E.bond_t.offset, E.hold_c.offset, E.n_local.offset, E.head.offset, E.fmu.offset, E.fisd.offset,
+        E.snap_a.offset, E.snap_b.offset,
+        C.sizeof(PnlDesc), PnlDesc.feat_ts.offset, PnlDesc.price.offset, PnlDesc.price_ts.offset,
+        PnlDesc.snap.offset, PnlDesc.bond.offset, PnlDesc.pnl_out.offset, PnlDesc.stats.offset,
+        PnlDesc.alpha.offset, PnlDesc.has_b.offset, PnlDesc.n_dates.offset, PnlDesc.head.offset,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
         S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset, S.sv_tscale.offset, S.scheme.offset,
@@ -134,6 +150,7 @@ def _bind(lib):
         "rph_train_lag_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_train_ticket_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
+        "rph_pnl": (C.c_int, [C.POINTER(PnlDesc), VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
         "rph_payoff": (C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP, C.c_float, VP, VP, VP]),
@@ -271,6 +288,12 @@ def train_update(desc: TrainDesc, step: int, epoch: int, stream=None):
 
 def eval_(desc: EvalDesc, stream=None):
     _check(_lib.rph_eval(C.byref(desc), stream_handle(stream)), "rph_eval")
+
+
+def pnl(desc: PnlDesc, stream=None):
+    """Self-financing hedge P&L scan over the rebalancing dates (k_hedge_pnl)."""
+    load(required=True)
+    _check(_lib.rph_pnl(C.byref(desc), stream_handle(stream)), "rph_pnl")
 
 
 def payoff(kind: int, s: torch.Tensor, out: torch.Tensor, strike: float, nfrac=None, wts=None, na: int = 1,

@@ -547,3 +547,23 @@ def test_k10_first_step_matches_torch_optim_adam(dev, mode):
     loss.backward()
     opt.step()
     np.testing.assert_allclose(wg, p.detach().numpy(), rtol=1e-4, atol=2e-6)
+
+
+@pytest.mark.parametrize("case", ["euro", "pension_q99"])
+def test_pnl_scan_kernel_vs_numpy(dev, case):
+    """k_hedge_pnl (self-financing P&L over the per-date networks written by
+    the eval kernels' snapshots) against the numpy recursion."""
+    from test_pnl import check_against_oracle
+
+    from rphedge.api import european_option, run_params
+    from rphedge.experiments import mts_parameters
+
+    if case == "euro":
+        res = european_option(N_paths=1 << 14, dt=1 / 52, rebalancing_frequency=1 / 13, epochs_first=40,
+                              epochs_rest=8, batch_size=4096, verbose=False, device=dev)
+        check_against_oracle(res)
+    else:
+        res = run_params(mts_parameters(n_paths=13, dt=0.1, rebalancing=1.0, epochs_first=30, epochs_rest=6,
+                                        verbose=False, device=dev, batch_size=2048))
+        check_against_oracle(res, hold_c=0.1)
+    assert res.induction.pnl_paths.is_cuda
