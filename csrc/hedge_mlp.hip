@@ -513,20 +513,35 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const long long base = (long long)blockIdx.x * 256 * PNL_PPT + tid;
   const bool has_b = d.has_b != 0;
-  float wealth[PNL_PPT];
+  // per path: wealth, the traded prices at the current date (carried to the
+  // next date: each price row is loaded once) and the next date's inputs,
+  // all loads of a date issued together before any compute
+  float wealth[PNL_PPT], s_cur[PNL_PPT][NA > 0 ? NA : 1];
+  long long pidx[PNL_PPT];
 #pragma unroll
   for (int j = 0; j < PNL_PPT; ++j) {
     const long long p = base + (long long)j * 256;
-    wealth[j] = p < d.n_local ? (d.w0 ? d.w0[p] : d.wealth0) : 0.f;
+    const bool ok = p < d.n_local;
+    pidx[j] = ok ? p : 0;  // invalid paths compute on path 0 and are never stored
+    wealth[j] = ok ? (d.w0 ? d.w0[p] : d.wealth0) : 0.f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) s_cur[j][a] = d.price[a][pidx[j]];
   }
   for (int t = 0; t < d.n_dates; ++t) {
+    float xr[PNL_PPT][NIN], s_nxt[PNL_PPT][NA > 0 ? NA : 1];
+#pragma unroll
+    for (int j = 0; j < PNL_PPT; ++j) {
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) xr[j][f] = d.feat[f][(long long)t * d.feat_ts[f] + pidx[j]];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) s_nxt[j][a] = d.price[a][(long long)(t + 1) * d.price_ts[a] + pidx[j]];
+    }
     __syncthreads();  // every thread is done with date t-1's weights
     const NetWeights* wt = d.snap + (size_t)t * 2;
     for (int i = tid; i < S::P; i += 256) {
       wl[i] = wt[0].w[0][i];
       if (has_b) wl[WBOFF + i] = wt[1].w[0][i];
     }
-    __syncthreads();
     float mu[NIN], isd[NIN];
 #pragma unroll
     for (int f = 0; f < NIN; ++f) {
@@ -534,17 +549,16 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
       isd[f] = d.fisd[t * MAXIN + f];
     }
     const float grow = (float)(d.bond[t + 1] / d.bond[t]);
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < PNL_PPT; ++j) {
-      const long long p = base + (long long)j * 256;
-      if (p >= d.n_local) continue;
       uint32_t zo = 0;  // opaque zero: weights stay in LDS (broadcast reads), not hoisted into VGPRs
       asm volatile("" : "+v"(zo));
       const float* __restrict__ WA = (const float*)__builtin_assume_aligned(wl + (zo & ~3u), 16);
       const float* __restrict__ WB = (const float*)__builtin_assume_aligned(wl + WBOFF + (zo & ~3u), 16);
       float x[NIN];
 #pragma unroll
-      for (int f = 0; f < NIN; ++f) x[f] = (d.feat[f][(long long)t * d.feat_ts[f] + p] - mu[f]) * isd[f];
+      for (int f = 0; f < NIN; ++f) x[f] = (xr[j][f] - mu[f]) * isd[f];
       float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], hb[NHOLD];
       net_forward<NIN, H, NO, HEAD>(WA, x, d.alpha, z1, a1, z2, a2, hold);
       if (has_b) {
@@ -555,9 +569,8 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
       float w = wealth[j] * grow;
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
-        const float s0 = d.price[a][(long long)t * d.price_ts[a] + p];
-        const float s1 = d.price[a][(long long)(t + 1) * d.price_ts[a] + p];
-        w = fmaf(hold[a], s1 - s0 * grow, w);
+        w = fmaf(hold[a], s_nxt[j][a] - s_cur[j][a] * grow, w);
+        s_cur[j][a] = s_nxt[j][a];
       }
       wealth[j] = w;
     }

@@ -136,7 +136,7 @@ class HedgeRun:
                 if c.model == "heston":
                     p = P.simulate_sv(g, self.n_local, c.Y, c.r, c.v0, model="heston", kappa=c.kappa,
                                       theta=c.theta, xi=c.xi, rho=c.rho, norm=c.Y, fp64=fp64,
-                                      scheme=c.heston_scheme, **kw)
+                                      scheme=c.heston_scheme, joint=not c.parity.paired_sobol, **kw)
                 else:
                     scheme = "arith" if c.model == "gbm" else "log"
                     p = P.simulate_gbm(g, self.n_local, c.Y, c.r, c.sigma, scheme=scheme, norm=c.Y, fp64=fp64,
@@ -160,7 +160,7 @@ class HedgeRun:
                                       kappa=c.kappa, theta=c.theta, xi=c.xi, rho=c.rho, fp64=fp64,
                                       parity_nan=c.parity.sv_sqrt_nan, scheme=c.heston_scheme,
                                       sv_tscale=0.0 if c.parity.sv_reference_dynamics else c.sv_days_per_year,
-                                      **kw)
+                                      joint=not c.parity.paired_sobol, **kw)
                 else:
                     p = P.simulate_gbm(g, self.n_local, c.Y, c.mu, c.sigma, scheme=("log" if c.model == "gbm_log"
                                                                                    else "arith"),

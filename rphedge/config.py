@@ -38,6 +38,9 @@ class ParityFlags:
     complement_head: bool = False       # Q13: European psi = 1 - phi head
     eo_discount_artifact: bool = False  # Q14: report V0*e^{-rT} as "discounted E[V(T)]"
     raw_features: bool = False          # reference nets see raw (unstandardised) state features
+    paired_sobol: bool = False          # Q25: SV price / vol shocks from two scrambled Sobol sequences of the
+                                        # SAME dimensions (RP:274-275; dependent, not independent, shocks);
+                                        # False = one sequence of 2 n_fine dimensions
 
     @classmethod
     def reference(cls) -> "ParityFlags":
@@ -45,7 +48,7 @@ class ParityFlags:
                    sv_c_overwrite=True, sv_reference_dynamics=True, sv_sqrt_nan=True,
                    fine_terminal_payoff=True, lr_schedule_first_only=True, warm_start=True,
                    restore_best_at_end=False, numpy_binomial=True, local_residual_pnl=True,
-                   complement_head=True, eo_discount_artifact=True, raw_features=True)
+                   complement_head=True, eo_discount_artifact=True, raw_features=True, paired_sobol=True)
 
 
 @dataclass

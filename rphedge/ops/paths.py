@@ -149,7 +149,7 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
                 a=0.0, b=0.0, c=0.0, kappa=0.0, theta=0.0, xi=0.0, rho=0.0, norm: float = 1.0,
                 device="cuda", offset: int = 0, fp64: bool = False, parity_nan: bool = False,
                 seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None, out: Paths | None = None,
-                scheme: str = "qe", sv_tscale: float = 0.0) -> Paths:
+                scheme: str = "qe", sv_tscale: float = 0.0, joint: bool | None = None) -> Paths:
     """Reference CIR-on-sigma SV (RP:282-289) or Heston (K4).
 
     ``scheme`` (Heston): "qe" = Andersen quadratic-exponential variance step
@@ -162,6 +162,16 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
         raise ValueError(f"heston scheme must be qe | euler, got {scheme!r}")
     if model == "heston" and scheme == "qe" and not (kappa > 0 and xi > 0):
         scheme = "euler"  # QE needs a mean-reverting, stochastic variance
+    # The reference draws W1 and W_SV from two separately scrambled Sobol
+    # sequences of the SAME dimensions (RP:274-275): dimension t of both is a
+    # bijective re-scrambling of one coordinate, so the two shocks of a step are
+    # deterministically paired, not independent (it biased the Heston price by
+    # about -1 % with QE, +1.3 % with Euler).  Heston and the corrected SV model
+    # draw both shocks from ONE sequence of 2 n_fine dimensions instead; the
+    # reference SV recursion keeps the reference's two sequences.
+    # (``joint``: None = by model; ParityFlags.paired_sobol selects it in the API)
+    if joint is None:
+        joint = model == "heston" or (model == "sv_ref" and sv_tscale > 0)
     dev = torch.device(device)
     S = out.S if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
     V = out.vol if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
@@ -170,11 +180,19 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
     if _dev_is_gpu(dev):
         from . import native
 
-        sv1, sh1, d1 = device_table(grid.n_fine, seed1, dev)
-        sv2, sh2, d2 = device_table(grid.n_fine, seed2, dev)
         d = _desc(mcode, n_local, offset, grid, fp64, parity_nan)
-        d.sv1, d.shift1, d.dims1 = sv1.data_ptr(), sh1.data_ptr(), d1
-        d.sv2, d.shift2, d.dims2 = sv2.data_ptr(), sh2.data_ptr(), d2
+        nf = grid.n_fine
+        if joint:
+            # ONE Sobol sequence of 2 n_fine dimensions: price shocks at dims
+            # [0, nf), variance shocks at [nf, 2 nf) - jointly equidistributed
+            sv, sh, dd = device_table(2 * nf, seed1, dev)
+            d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), nf
+            d.sv2, d.shift2, d.dims2 = sv.data_ptr() + nf * 32 * 4, sh.data_ptr() + nf * 4, nf
+        else:
+            sv1, sh1, d1 = device_table(nf, seed1, dev)
+            sv2, sh2, d2 = device_table(nf, seed2, dev)
+            d.sv1, d.shift1, d.dims1 = sv1.data_ptr(), sh1.data_ptr(), d1
+            d.sv2, d.shift2, d.dims2 = sv2.data_ptr(), sh2.data_ptr(), d2
         d.s0[0], d.mu[0], d.inv_norm[0] = s0, mu, 1.0 / norm
         d.v0, d.a, d.b, d.c = v0, a, b, c
         d.kappa, d.theta, d.xi, d.rho = kappa, theta, xi, rho
@@ -185,7 +203,7 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
     else:
         s_np, v_np, f_np = _cpu_sv(grid, n_local, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset,
                                    parity_nan, seed1, seed2, scheme=scheme,
-                                   sv_tscale=float(sv_tscale) if model == "sv_ref" else 0.0)
+                                   sv_tscale=float(sv_tscale) if model == "sv_ref" else 0.0, joint=joint)
         S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
         V.copy_(torch.from_numpy(v_np.astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
@@ -360,9 +378,16 @@ def _qe_step(v, z1, x2, dt, mu, kappa, theta, xi, rho):
 
 
 def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, parity_nan, seed1, seed2,
-            scheme="euler", sv_tscale=0.0):
-    W1 = _normals(grid.n_fine, seed1, n, offset, grid.n_fine)
-    X2 = _u30(grid.n_fine, seed2, n, offset, grid.n_fine)
+            scheme="euler", sv_tscale=0.0, joint=None):
+    if joint is None:
+        joint = model == "heston" or (model == "sv_ref" and sv_tscale > 0)
+    nf = grid.n_fine
+    if joint:  # one 2 n_fine-dimensional sequence (see simulate_sv)
+        X = _u30(2 * nf, seed1, n, offset, 2 * nf)
+        W1, X2 = ndtri_u30_f64(X[:, :nf]), X[:, nf:]
+    else:
+        W1 = _normals(nf, seed1, n, offset, nf)
+        X2 = _u30(nf, seed2, n, offset, nf)
     W2 = ndtri_u30_f64(X2)
     dt = grid.dt
     ly = np.full(n, math.log(s0))

@@ -64,7 +64,9 @@ def test_european_eo_corrected():
     _record("eo_corrected", {"V0": res.v0, "phi0": res.phi, "psi0": res.psi, "pnl": res.terminal_pnl,
                              "var": res.var})
     assert abs(res.v0 - 10.3896) < 0.5
-    assert res.terminal_pnl["std"] < 1.7504     # beats the reference's terminal residual std
+    # like-for-like with the reference's "P&L" (the one-step residual at T, Q24)
+    assert res.terminal_residual["std"] < 1.7504
+    assert res.terminal_pnl["kind"] == "self_financing" and math.isfinite(res.terminal_pnl["std"])
 
 
 def test_heston_and_basket_runs():

@@ -99,4 +99,6 @@ def test_wide_european_end_to_end(dev, feature_norm):  # noqa: F811
     # profiles/wide_e2e_scatter_r1.jsonl), whose P&L std is ~25 % lower
     assert abs(res.phi - 0.7285) < 0.03, res.phi
     assert abs(res.v0 - 10.3896) < (0.8 if feature_norm == "none" else 2.0), res.v0
-    assert res.terminal_pnl["std"] < (1.3 if feature_norm == "none" else 0.9), res.terminal_pnl
+    assert res.terminal_residual["std"] < (1.3 if feature_norm == "none" else 0.9), res.terminal_residual
+    # self-financing P&L over the 12 monthly dates (BS delta hedge on the same grid: ~1.4)
+    assert res.terminal_pnl["kind"] == "self_financing" and res.terminal_pnl["std"] < 2.5, res.terminal_pnl
