@@ -400,6 +400,10 @@ __global__ __launch_bounds__(256) void k_hedge_lag_finalize(const TrainDesc d, c
   __syncthreads();
   for (int i = threadIdx.x; i < 3 * LAG_SLOTS * R; i += 256) st_agent(d.acc + i, 0.f);
   if (!run || bad) return;
+  // diagnostics (TrainConfig.expose_packet): the summed - and, data parallel,
+  // exchanged - packet of the last step, as every rank applies it
+  if (d.grad_out != nullptr)
+    for (int i = threadIdx.x; i < R; i += 256) d.grad_out[i] = red[i];
   const int S = d.steps_per_epoch;
   const int kp = K - 1, ep = kp / S;
   int ep_done = ep;

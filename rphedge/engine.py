@@ -105,6 +105,8 @@ class TrainConfig:
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
     mfma_fp32: bool = False        # 32-unit nets: exact fp32 MFMA instead of bf16 operands
+    expose_packet: bool = False    # lagged fits: the finalize kernel writes the last step's summed (and
+                                   # data-parallel exchanged) gradient packet to HipBackend.grad (tests)
     # optimizer-step schedule on the GPU:
     #   "lag"        one kernel per step, the Adam update of step k applied by every
     #                workgroup in the prologue of kernel k+1 (no in-kernel sync)
@@ -384,6 +386,8 @@ class HipBackend:
         d = self._train_desc(wts, opt, fit, data, fcfg, seed, lr_t)
         n, S = self.native, self.steps_per_epoch
         mode = self.step_mode(poll_every)
+        if mode == "lag" and not self.tcfg.expose_packet:
+            d.grad_out = None  # (the finalize kernel writes the packet only when asked)
         if mode == "lag" and fcfg.epochs > 0:
             # kernel 0 reads the fit-state template and publishes it as `fit`;
             # the previous lag fit's finalize left the accumulators zeroed

@@ -208,6 +208,13 @@ def test_train_step_matches_torch(dev, shape, mode):
                                                                    step_mode=mode)
     np.testing.assert_allclose(wg, wc, rtol=2e-3, atol=2e-4)
     assert og[L.O_T] == oc[L.O_T] == 16
+    # Adam moments: m, v are linear / quadratic in the gradient, so (unlike the
+    # weights) they expose a mis-scaled gradient packet
+    P = spec.nparams
+    for off in (L.O_M, L.O_V):
+        ref = oc[off:off + P]
+        np.testing.assert_allclose(og[off:off + P], ref, rtol=0, atol=5e-3 * np.abs(ref).max())
+        assert abs(np.linalg.norm(og[off:off + P]) / np.linalg.norm(ref) - 1.0) < 5e-3
     np.testing.assert_allclose(fg[L.F_HIST:L.F_HIST + 2], fc[L.F_HIST:L.F_HIST + 2], rtol=1e-3)
     np.testing.assert_allclose(vg, vc, rtol=1e-3, atol=1e-4)
     np.testing.assert_allclose(rg, rc, rtol=1e-3, atol=1e-4)
