@@ -61,6 +61,7 @@ def autograd_packet(spec, w0, feats, prices, target, idx, loss, q=0.99, bond=1.0
     lv = torch.maximum(q * -e, (q - 1) * -e) if loss == L.LOSS_PINBALL else e * e
     B = world_batch or len(idx)
     (lv.sum() / B).backward()
+    lv, e = lv.detach(), e.detach()
     stats = [float(lv.sum()), float(e.abs().sum()), float((e.abs() / y.abs().clamp_min(1e-7)).sum()), float(len(idx))]
     return w.grad.numpy(), np.asarray(stats)
 
@@ -105,7 +106,8 @@ def test_split_update_packet_matches_fp64_autograd(shape, loss):
     pkt = be.grad.cpu().numpy()
     g_ref, s_ref = autograd_packet(spec, w0, feats, prices, target, torch.arange(batch, 2 * batch), loss)
     # fp32 VALU / fp32 MFMA: 1e-5 relative; bf16 MFMA operands: 1e-2 (cosine-level agreement)
-    _check(pkt, spec.nparams, g_ref, s_ref, gtol=2e-2 if (h == 32 and not fp32_mfma) else 2e-5)
+    bf16 = h == 32 and not fp32_mfma
+    _check(pkt, spec.nparams, g_ref, s_ref, gtol=2e-2 if bf16 else 2e-5, stol=2e-3 if bf16 else 1e-5)
 
 
 @pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (5, 8, 6, 0), (1, 32, 2, 0), (2, 32, 2, 0)])
