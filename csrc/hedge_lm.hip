@@ -1,0 +1,494 @@
+// rphedge — Levenberg-Marquardt (damped Gauss-Newton) fits of the reference's
+// 8-unit hedge nets on gfx950: the MSE objective of one backward-induction
+// date, mean over paths of (h(state_t) . prices_{t+1} - V_{t+1})^2
+// (Replicating_Portfolio.py:211, the fit that Keras-Adam runs for 500 / 100
+// epochs), solved by full-batch damped Gauss-Newton steps instead.
+//
+// One PASS evaluates one trial point theta:
+//   k_lm_pass    every local path: loss, |e|, ape and the exact gradient
+//                g = (2/n) sum_p e_p J_p on the VALU (NarrowBody, the same fused
+//                fwd/bwd body as the Adam step kernels, full batch, no shuffle);
+//                the Gram matrix of a 64-path tile per gram workgroup,
+//                G += J^T J over the tile, on the matrix cores
+//                (v_mfma_f32_32x32x2_f32, J staged through LDS, upper-
+//                triangular 32x32 blocks spread over the 4 waves);
+//                per-workgroup results go to slabs (no float atomics)
+//   k_lm_reduce  fixed-order sums of the slabs -> one reduced block
+//                [G | g | stats] (bitwise reproducible run to run)
+//   (data parallel: one all-reduce of the reduced block between the two)
+//   k_lm_solve   one workgroup: accept the trial if its loss beats the best
+//                point (damping down) or reject it (damping up), then the
+//                Marquardt step (2G + lam diag(2G) + ridge) d = -g by an fp64
+//                Cholesky factorisation in LDS and the next trial
+//                theta_best + d; the last pass writes theta_best to the
+//                canonical NetWeights and the FitState bookkeeping.
+// The start point is pass 0; `passes` trial points follow.  Everything stays
+// on the device and graph-captures with the rest of the induction.
+#include "hedge_core.h"
+#include "hedge_narrow.h"
+
+namespace rph {
+
+typedef float lm_f32x16 __attribute__((ext_vector_type(16)));
+
+template <int P>
+struct LmShape {
+  static constexpr int NP = ((P + 31) / 32) * 32;  // padded to MFMA blocks
+  static constexpr int NB = NP / 32;
+  static constexpr int NBLK = NB * (NB + 1) / 2;    // upper-triangular 32x32 blocks
+  static constexpr int JP = NP + 33;                // LDS pitch of the J tile (odd*32+1: conflict-free)
+  static_assert(NP <= LM_NPMAX && NBLK * 1024 <= LM_GBLK_MAX, "network too large for the LM solver");
+};
+
+// upper-triangular block b -> (mb, nb), mb <= nb, row-major
+RPH_INLINE void lm_blk(int b, int NB, int& mb, int& nb) {
+  int m = 0;
+  while (b >= NB - m) {
+    b -= NB - m;
+    ++m;
+  }
+  mb = m;
+  nb = m + b;
+}
+
+// unit (row) of 32x32 accumulator register q in lane half h
+RPH_INLINE constexpr int lm_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
+
+// ---------------------------------------------------------------------------
+// Pass kernel.  B = NarrowBody<...> (full batch: batch = n_local, no shuffle).
+// ---------------------------------------------------------------------------
+template <class B>
+__global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainDesc d, const LmDesc lm, const int pass) {
+  constexpr int P = B::P;
+  constexpr int R = B::R;
+  constexpr int NR = B::NR;
+  using S = typename B::S;
+  using LS = LmShape<P>;
+  constexpr int NP = LS::NP, NB = LS::NB, NBLK = LS::NBLK, JP = LS::JP;
+  constexpr int NIN = B::NIN_, H = B::H_, NO = B::NO_, HEAD = B::HEAD_, NHOLD = B::NHOLD;
+  const uint32_t kat = prefetch_kernarg_begin<sizeof(TrainDesc) + sizeof(LmDesc) + sizeof(int)>();
+  __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
+  __shared__ __attribute__((aligned(16))) float wl[P + 4];
+  __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  prefetch_kernarg_end(kat);
+  double* st = lm.state;
+  // trial point: pass 0 = the start point (canonical weights, published as
+  // slot 0); later passes = the slot k_lm_solve wrote
+  const int trial = pass == 0 ? 0 : 1 - (int)st[LMS_BEST];
+  const Perm perm = make_perm(1u, 0u, 0u, false);
+  typename B::Pre pre;
+  B::load(d, 0, perm, B::first(wid), lane, pre);
+  for (int i = tid; i < P; i += 256) {
+    const float w = pass == 0 ? d.wts->w[0][i] : (float)st[LMS_W + trial * LM_NPMAX + i];
+    wl[i] = w;
+    if (pass == 0 && blockIdx.x == 0) st[LMS_W + i] = (double)w;
+  }
+  if (pass == 0 && blockIdx.x == 0 && tid == 0) {
+    st[LMS_BEST] = 1.0;
+    st[LMS_LAM] = lm.lam0;
+    st[LMS_NACC] = 0.0;
+    st[LMS_FAIL] = 0.0;
+  }
+  __syncthreads();
+  // ---- loss + exact gradient over every local path (VALU) -------------------
+  typename B::Frags fr;
+  B::make_frags(wl + S::OW2, fr);
+  float val[NR];
+  B::partial(d, 0, perm, wl, fr, scratch, pre, val);
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+    if (tid + 256 * j < R) lm.slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
+  if ((int)blockIdx.x >= lm.gram_wgs) return;
+  // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
+  if (wid == 0) {
+    const long long p = (long long)blockIdx.x * LM_TILE + lane;
+    const bool ok = p < d.n_local;
+    const long long q = ok ? p : 0;
+    float x[NIN], pr[NHOLD];
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) x[f] = (d.feat[f][q] - d.fmu[f]) * d.fisd[f];
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = d.price[k][q];
+    pr[NHOLD - 1] = d.bond;
+    float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
+    net_forward<NIN, H, NO, HEAD>(wl, x, d.alpha, z1, a1, z2, a2, hold);
+    // J_p = dV_p / dtheta  (dV = 1)
+    float dout[NO];
+    if (HEAD == HEAD_COMPLEMENT) {
+      dout[0] = pr[0] - pr[1];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NO; ++k) dout[k] = pr[k];
+    }
+    float* row = jt + lane * JP;
+    const float m = ok ? 1.f : 0.f;  // paths beyond the shard contribute nothing
+#pragma unroll
+    for (int k = 0; k < NO; ++k) row[S::OB3 + k] = m * dout[k];
+    float dz2[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      float da = 0.f;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        row[S::OW3 + j * NO + k] = m * a2[j] * dout[k];
+        da = fmaf(wl[S::OW3 + j * NO + k], dout[k], da);
+      }
+      dz2[j] = m * da * lrelu_d(a2[j], d.alpha);
+      row[S::OB2 + j] = dz2[j];
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      float da = 0.f;
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        row[S::OW2 + i * H + j] = a1[i] * dz2[j];
+        da = fmaf(wl[S::OW2 + i * H + j], dz2[j], da);
+      }
+      const float dz1 = da * lrelu_d(a1[i], d.alpha);
+      row[S::OB1 + i] = dz1;
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) row[S::OW1 + f * H + i] = x[f] * dz1;
+    }
+#pragma unroll
+    for (int i = P; i < NP; ++i) row[i] = 0.f;
+  }
+  __syncthreads();
+  const int h = lane >> 5, r = lane & 31;
+  for (int b = wid; b < NBLK; b += 4) {
+    int mb, nb;
+    lm_blk(b, NB, mb, nb);
+    lm_f32x16 acc = {};
+#pragma unroll 8
+    for (int s = 0; s < LM_TILE / 2; ++s) {
+      const float* row = jt + (2 * s + h) * JP;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(row[mb * 32 + r], row[nb * 32 + r], acc, 0, 0, 0);
+    }
+    float* out = lm.slab_g + ((size_t)blockIdx.x * NBLK + b) * 1024;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[q * 64 + lane] = acc[q];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Reduce kernel: red[e] = fixed-order sums of the slabs.
+// ---------------------------------------------------------------------------
+template <int P, int R>
+__global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __restrict__ red) {
+  using LS = LmShape<P>;
+  constexpr int NG = LS::NBLK * 1024;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < NG) {
+    double s = 0.0;
+    const float* col = lm.slab_g + e;
+#pragma unroll 4
+    for (int w = 0; w < lm.gram_wgs; ++w) s += (double)col[(size_t)w * NG];
+    red[e] = s * (double)lm.inv_ns;
+    return;
+  }
+  // gradient packet (the last workgroup): GROUPS row groups per entry,
+  // combined in LDS in a fixed order
+  constexpr int GROUPS = 256 / R;
+  __shared__ double part[256];
+  const int i = threadIdx.x % R, grp = threadIdx.x / R;
+  double s = 0.0;
+#pragma unroll 4
+  for (int w = grp; w < lm.num_wgs; w += GROUPS) s += (double)lm.slab_b[(size_t)w * R + i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < R) {
+    double v = 0.0;
+    for (int q = 0; q < GROUPS; ++q) v += part[q * R + threadIdx.x];
+    if (threadIdx.x < P) red[LM_GBLK_MAX + threadIdx.x] = v;
+    else if (threadIdx.x < P + 4) red[LM_GBLK_MAX + LM_NPMAX + threadIdx.x - P] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Solve kernel (one workgroup): accept / reject, damping, Cholesky, next trial.
+// red_new: the reduced block of the trial just evaluated (all-reduced when
+// data parallel); the state keeps the best point's block.
+// ---------------------------------------------------------------------------
+RPH_INLINE int lm_tri(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower triangle, j <= i
+
+template <int P, int R>
+__global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDesc lm, const double* __restrict__ red_new,
+                                                  const int pass) {
+  using LS = LmShape<P>;
+  constexpr int NB = LS::NB, NBLK = LS::NBLK;
+  constexpr int NG = NBLK * 1024;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* A = lds;                          // packed lower triangle [P(P+1)/2]
+  double* vec = lds + P * (P + 1) / 2;      // [P] rhs / solution
+  __shared__ int s_fail;
+  __shared__ double s_diag;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double* st = lm.state;
+  double* best_red = st + LMS_RED;  // the best point's reduced block
+  const int best_old = pass == 0 ? 1 : (int)st[LMS_BEST];
+  const int trial = 1 - best_old;
+  auto pkt = [&](int i) -> double {  // packet entries of the trial: [g (P) | loss, |e|, ape, count]
+    return i < P ? red_new[LM_GBLK_MAX + i] : red_new[LM_GBLK_MAX + LM_NPMAX + i - P];
+  };
+  const double cnt = pkt(P + 3);
+  const double Lt = pkt(P + 0) / fmax(cnt, 1.0);
+  const double Lb = pass == 0 ? INFINITY : st[LMS_RED + LM_GBLK_MAX + LM_NPMAX + 4];
+  const bool accept = pass == 0 || (Lt == Lt && Lt < Lb);
+  double lam = st[LMS_LAM];
+  int best = best_old;
+  if (accept) {
+    best = trial;
+    if (pass > 0) lam = fmax(lam * lm.lam_down, (double)lm.lam_min);
+    // the best point's block := the trial's (G, g, stats)
+    for (int e = tid; e < NG; e += 256) best_red[e] = red_new[e];
+    for (int i = tid; i < P + 4; i += 256) {
+      const double v = pkt(i);
+      if (i < P) best_red[LM_GBLK_MAX + i] = v;
+      else best_red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
+    }
+    if (tid == 0) {
+      best_red[LM_GBLK_MAX + LM_NPMAX + 4] = Lt;
+      st[LMS_NACC] += pass > 0 ? 1.0 : 0.0;
+    }
+  } else {
+    lam = fmin(lam * lm.lam_up, (double)lm.lam_max);
+  }
+  if (tid == 0 && pass < MAXHIST) d.fit->hist[pass] = (float)Lt;
+  __syncthreads();
+  const double* g = best_red + LM_GBLK_MAX;
+  if (pass == lm.passes) {  // final pass: publish the best point
+    for (int i = tid; i < P; i += 256) {
+      const float w = (float)st[LMS_W + best * LM_NPMAX + i];
+      d.wts->w[0][i] = w;
+      d.fit->w_best[i] = w;
+    }
+    if (tid == 0) {
+      const double* sb = best_red + LM_GBLK_MAX + LM_NPMAX;
+      const double c = fmax(sb[3], 1.0);
+      FitState* f = d.fit;
+      f->best_loss = (float)sb[4];
+      f->last_loss = (float)sb[4];
+      f->last_mae = (float)(sb[1] / c);
+      f->last_mape = (float)(100.0 * sb[2] / c);
+      f->epoch = (float)(pass + 1);
+      f->stopped = 1.f;
+      f->has_best = 1.f;
+      f->wait = 0.f;
+      f->loss_sum = f->abs_sum = f->ape_sum = f->loss_cnt = 0.f;
+      st[LMS_BEST] = (double)best;
+      st[LMS_LAM] = lam;
+    }
+    return;
+  }
+  // ---- A = 2 G + lam diag(2 G) + ridge * mean diag, packed lower triangle -----
+  const int h = lane >> 5, r = lane & 31;
+  for (int b = wid; b < NBLK; b += 4) {
+    int mb, nb;
+    lm_blk(b, NB, mb, nb);
+    const double* blk = best_red + (size_t)b * 1024;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = mb * 32 + lm_row(q, h), j = nb * 32 + r;  // i <= j when mb < nb
+      if (i < P && j < P && (mb < nb || i >= j)) {
+        const int hi = i > j ? i : j, lo = i > j ? j : i;
+        A[lm_tri(hi, lo)] = 2.0 * blk[q * 64 + lane];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+    for (int i = 0; i < P; ++i) s += A[lm_tri(i, i)];
+    s_diag = s / P;
+    s_fail = 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < P; i += 256) {
+    double& a = A[lm_tri(i, i)];
+    a = a * (1.0 + lam) + (double)lm.ridge * s_diag;
+    vec[i] = -g[i];
+  }
+  // ---- right-looking Cholesky, one barrier per column ---------------------------
+  for (int k = 0; k < P; ++k) {
+    __syncthreads();
+    const double akk = A[lm_tri(k, k)];
+    if (!(akk > 0.0)) {
+      if (tid == 0) s_fail = 1;
+      break;
+    }
+    const double rk = 1.0 / akk;
+    const int m = P - 1 - k;
+    const int cnt_t = m * (m + 1) / 2;
+    for (int t = tid; t < cnt_t; t += 256) {
+      int ii = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+      while ((ii + 1) * (ii + 2) / 2 <= t) ++ii;
+      while (ii * (ii + 1) / 2 > t) --ii;
+      const int jj = t - ii * (ii + 1) / 2;
+      const int i = k + 1 + ii, j = k + 1 + jj;
+      A[lm_tri(i, j)] -= A[lm_tri(i, k)] * A[lm_tri(j, k)] * rk;
+    }
+  }
+  __syncthreads();
+  if (s_fail) {
+    // not positive definite at this damping: re-evaluate the best point with
+    // more damping (trial := best)
+    for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
+    if (tid == 0) {
+      st[LMS_BEST] = (double)best;
+      st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
+      st[LMS_FAIL] += 1.0;
+    }
+    return;
+  }
+  // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k)
+  {
+    const int tot = P * (P + 1) / 2;
+    for (int t = tid; t < tot; t += 256) {
+      int i = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+      while ((i + 1) * (i + 2) / 2 <= t) ++i;
+      while (i * (i + 1) / 2 > t) --i;
+      const int k = t - i * (i + 1) / 2;
+      A[t] = (i == k) ? sqrt(A[t]) : A[t] / sqrt(A[lm_tri(k, k)]);
+    }
+  }
+  __syncthreads();
+  // ---- triangular solves in one wave (no barriers): L y = rhs, L^T d = y --------
+  if (wid == 0) {
+    for (int i = 0; i < P; ++i) {
+      double s = 0.0;
+      for (int m = lane; m < i; m += 64) s += A[lm_tri(i, m)] * vec[m];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) vec[i] = (vec[i] - s) / A[lm_tri(i, i)];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    for (int i = P - 1; i >= 0; --i) {
+      double s = 0.0;
+      for (int m = i + 1 + lane; m < P; m += 64) s += A[lm_tri(m, i)] * vec[m];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) vec[i] = (vec[i] - s) / A[lm_tri(i, i)];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i] + vec[i];
+  if (tid == 0) {
+    st[LMS_BEST] = (double)best;
+    st[LMS_LAM] = lam;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <int NIN, int H, int NO, int HEAD>
+struct LmKernels {
+  // the 1-3 input nets run two workgroups per CU (variant 5 body), the others one
+  static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
+  using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
+  using S = NetShape<NIN, H, NO, HEAD>;
+  static int smem() { return (int)((S::P * (S::P + 1) / 2 + S::P) * sizeof(double)); }
+};
+
+static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {
+  if (int rc = validate_train(d, 3 /* no schedule buffers */, "rph_lm")) return rc;
+  if (!lm->state || !lm->slab_b || !lm->slab_g) return rph_report("rph_lm", "null LM buffer");
+  if (d->batch != d->n_local || d->steps_per_epoch != 1) return rph_report("rph_lm", "LM fits are full batch");
+  if (lm->num_wgs < 1 || lm->num_wgs > 65535 || lm->passes < 0 || lm->passes >= MAXHIST)
+    return rph_report("rph_lm", "bad num_wgs / passes");
+  if (lm->gram_wgs < 1 || lm->gram_wgs > lm->num_wgs || (long long)lm->gram_wgs * LM_TILE > d->n_local)
+    return rph_report("rph_lm", "gram_wgs must cover 64-path tiles inside the shard");
+  if (lm->red_wgs != nblk * 1024 / 256 + 1) return rph_report("rph_lm", "bad red_wgs");
+  if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
+  (void)P;
+  return 0;
+}
+
+template <int A, int B, int C, int E>
+static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, hipStream_t s) {
+  using K = LmKernels<A, B, C, E>;
+  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs), dim3(256), 0, s, *d, *lm, pass);
+  return (int)hipGetLastError();
+}
+
+}  // namespace rph
+
+using namespace rph;
+
+#define RPH_LM_SHAPES(X)         \
+  X(1, 8, 1, HEAD_COMPLEMENT)    \
+  X(1, 8, 2, HEAD_FREE)          \
+  X(2, 8, 2, HEAD_FREE)          \
+  X(3, 8, 2, HEAD_FREE)          \
+  X(4, 8, 2, HEAD_FREE)          \
+  X(5, 8, 6, HEAD_FREE)          \
+  X(6, 8, 7, HEAD_FREE)
+
+// Geometry of the LM kernels for a shape: returns 0 and fills (P, R, NBLK,
+// two workgroups per CU) or -1 for shapes without an LM solver.
+extern "C" int rph_lm_shape(int nin, int h, int nout, int head, int* p, int* r, int* nblk, int* two_per_cu) {
+#define X(A, B, C, E)                                                    \
+  if (shape_is(nin, h, nout, head, A, B, C, E)) {                        \
+    using K = LmKernels<A, B, C, E>;                                     \
+    *p = K::S::P;                                                        \
+    *r = K::S::R;                                                        \
+    *nblk = LmShape<K::S::P>::NBLK;                                      \
+    *two_per_cu = K::TWO ? 1 : 0;                                        \
+    return 0;                                                            \
+  }
+  RPH_LM_SHAPES(X)
+#undef X
+  return -1;
+}
+
+// One pass = pass kernel + reduce kernel (into red_new); the caller all-reduces
+// red_new when data parallel, then launches rph_lm_solve.
+extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new, int pass, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                           \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                  \
+    using K = LmKernels<A, B, C, E>;                                                            \
+    if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK)) return rc;      \
+    if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, s)) return rc;                         \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs), dim3(256), 0, s, *lm, red_new); \
+    return (int)hipGetLastError();                                                              \
+  }
+  RPH_LM_SHAPES(X)
+#undef X
+  return rph_report("rph_lm_eval", "no LM solver for this network shape (8-unit nets only)");
+}
+
+extern "C" int rph_lm_solve(const TrainDesc* d, const LmDesc* lm, const double* red_new, int pass, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define X(A, B, C, E)                                                                                  \
+  if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                         \
+    using K = LmKernels<A, B, C, E>;                                                                   \
+    const int bytes = K::smem();                                                                       \
+    static bool attr = false;                                                                          \
+    if (!attr) {                                                                                       \
+      hipError_t e = hipFuncSetAttribute((const void*)k_lm_solve<K::S::P, K::S::R>,                   \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);           \
+      if (e != hipSuccess) return (int)e;                                                              \
+      attr = true;                                                                                     \
+    }                                                                                                  \
+    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(1), dim3(256), bytes, s, *d, *lm, red_new, pass); \
+    return (int)hipGetLastError();                                                                     \
+  }
+  RPH_LM_SHAPES(X)
+#undef X
+  return rph_report("rph_lm_solve", "no LM solver for this network shape");
+}
+
+// Whole single-rank fit: passes + 1 evaluations, each followed by a solve.
+extern "C" int rph_lm_fit(const TrainDesc* d, const LmDesc* lm, double* red_new, void* stream) {
+  for (int k = 0; k <= lm->passes; ++k) {
+    if (int rc = rph_lm_eval(d, lm, red_new, k, stream)) return rc;
+    if (int rc = rph_lm_solve(d, lm, red_new, k, stream)) return rc;
+  }
+  return 0;
+}

@@ -26,166 +26,9 @@
 #include "hedge_core.h"
 #include "hedge_fit.h"
 #include "hedge_lag.h"
+#include "hedge_narrow.h"
 
 namespace rph {
-
-// ---------------------------------------------------------------------------
-// Per-workgroup gradient packet of one minibatch step, thread-per-path VALU
-// (the reference's 8-unit nets).  Used by the per-step kernel below and by the
-// persistent per-fit kernel (hedge_fit.h).
-// ---------------------------------------------------------------------------
-template <int NIN, int H, int NO, int HEAD, int WPE = 1, int PFD = 1, bool LDSW = (WPE > 1), bool HYB = false>
-struct NarrowBody {
-  static constexpr int WAVES_PER_SIMD = WPE;
-  // LDSW: weights are re-read from LDS every path iteration instead of being
-  // hoisted into registers (needed at 2 waves/SIMD; at 1 wave/SIMD it keeps
-  // the wide-packet nets - basket 5-8-6, R = 256 - out of scratch spills)
-  static constexpr bool LDS_WEIGHTS = LDSW;
-  // path-data prefetch distance in loop iterations (1: the next path is loaded
-  // while the current one computes; >1 keeps PFD loads in flight, so a thread's
-  // later paths never wait on a fresh L2/MALL round trip)
-  static constexpr int PF = PFD;
-  using S = NetShape<NIN, H, NO, HEAD>;
-  static constexpr int P = S::P;
-  static constexpr int R = S::R;
-  static constexpr int NR = (R + 255) / 256;  // packet entries per thread (1)
-  static constexpr int NREP = NARROW_NREP;    // lagged schedule: float-atomic replicas
-  static constexpr bool ACC_PLAIN = true;      // lagged prologue: cached (L2-shared) accumulator loads
-  static constexpr int NHOLD = S::NHOLD;
-  static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
-  struct Frags {};  // (weights are read from LDS)
-  struct Pre {      // first path of the step, loaded ahead by the caller
-    float x[NIN], pr[NHOLD], y;
-    bool valid;
-  };
-
-  RPH_INLINE static void make_frags(const float*, Frags&) {}
-
-  RPH_INLINE static long long first(int wid) { return (long long)(blockIdx.x * 4 + wid) * 64; }
-
-  RPH_INLINE static void load(const TrainDesc& d, int step, const Perm& perm, long long j0, int lane, Pre& p) {
-    const long long jl = j0 + lane;
-    const long long j = (long long)step * d.batch + jl;
-    p.valid = (jl < d.batch) && (j < d.n_local);
-    const uint32_t q = p.valid ? perm_path(perm, (uint32_t)j, d.chunk_log2, d.n_local) : 0u;
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) p.x[f] = d.feat[f][q];  // raw, unselected (q = 0 when invalid; invalid paths carry dV = 0):
-                                                   // no v_cndmask forcing an early vmcnt wait
-#pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = d.price[k][q];
-    p.pr[NHOLD - 1] = d.bond;
-    p.y = d.target[q];
-  }
-
-  // W: weights in LDS; lds: SCRATCH_FLOATS of LDS; pre: the first path (loaded).
-  // Returns in val[0] (threads < R) the workgroup sum of packet entry tid.
-  RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
-                                 const Frags&, float* lds, Pre& pre, float (&val)[NR]) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const long long stride = (long long)gridDim.x * 4 * 64;
-    float g[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) g[i] = 0.f;
-    const float alpha = d.alpha;
-    // ring of prefetched paths: q[0] = current (loaded by the caller), q[i] the
-    // path i iterations ahead
-    Pre q[PF];
-    q[0] = pre;
-#pragma unroll
-    for (int i = 1; i < PF; ++i) {
-      q[i].valid = false;
-      if (first(wid) + i * stride < d.batch) load(d, step, perm, first(wid) + i * stride, lane, q[i]);
-    }
-    for (long long j0 = first(wid); j0 < d.batch; j0 += stride) {
-      // WPE 1: the loop-invariant LDS weights are hoisted into registers (AGPR
-      // overflow); WPE 2: an opaque zero offset makes every iteration re-read
-      // them as LDS broadcasts, so the kernel fits 256 registers = 2 waves/SIMD
-      // HYB: only the W2 block (the most-used weights, forward and backward)
-      // is hoisted into registers, the rest is re-read from LDS, so the
-      // hoisted weights fit in VGPRs instead of overflowing to AGPRs (each
-      // AGPR-resident weight costs a v_accvgpr_read per use)
-      const float* __restrict__ Wi = W;
-      if constexpr (LDSW || HYB) {
-        // opaque 16-byte-aligned base: every use is a ds_read_b128 broadcast
-        // off ONE address register with an immediate offset
-        uint32_t z = 0;
-        asm volatile("" : "+v"(z));
-        Wi = (const float*)__builtin_assume_aligned(W + (z & ~3u), 16);
-      }
-      const float* __restrict__ W2s = HYB ? W : Wi;
-      float x[NIN], pr[NHOLD];
-#pragma unroll
-      for (int f = 0; f < NIN; ++f) x[f] = (q[0].x[f] - d.fmu[f]) * d.fisd[f];
-#pragma unroll
-      for (int k = 0; k < NHOLD; ++k) pr[k] = q[0].pr[k];
-      const float y = q[0].y;
-      const bool valid = q[0].valid;
-#pragma unroll
-      for (int i = 0; i + 1 < PF; ++i) q[i] = q[i + 1];
-      if (j0 + PF * stride < d.batch) load(d, step, perm, j0 + PF * stride, lane, q[PF - 1]);  // software pipelining
-
-      float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
-      net_forward<NIN, H, NO, HEAD>(Wi, x, alpha, z1, a1, z2, a2, hold, W2s);
-      float V = 0.f;
-#pragma unroll
-      for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
-      float l, dV;
-      path_loss(d.loss, d.quantile, V, y, l, dV);  // dL/dV (mean over the global batch below)
-      dV = valid ? dV * d.inv_batch : 0.f;
-      const float ae = fabsf(V - y);
-      g[P + 0] += valid ? l : 0.f;
-      g[P + 1] += valid ? ae : 0.f;
-      g[P + 2] += valid ? ae * __frcp_rn(fmaxf(fabsf(y), 1e-7f)) : 0.f;
-      g[P + 3] += valid ? 1.f : 0.f;
-
-      // backward
-      float dout[NO];
-      if (HEAD == HEAD_COMPLEMENT) {
-        dout[0] = dV * (pr[0] - pr[1]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
-      }
-#pragma unroll
-      for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k];
-      float dz2[H];
-#pragma unroll
-      for (int j = 0; j < H; ++j) {
-        float da = 0.f;
-#pragma unroll
-        for (int k = 0; k < NO; ++k) {
-          g[S::OW3 + j * NO + k] = fmaf(a2[j], dout[k], g[S::OW3 + j * NO + k]);
-          da = fmaf(Wi[S::OW3 + j * NO + k], dout[k], da);
-        }
-        dz2[j] = da * lrelu_d(a2[j], alpha);  // (a > 0 <=> z > 0 for 0 <= alpha: z1/z2 need not stay live)
-        g[S::OB2 + j] += dz2[j];
-      }
-#pragma unroll
-      for (int i = 0; i < H; ++i) {
-        float da = 0.f;
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          g[S::OW2 + i * H + j] = fmaf(a1[i], dz2[j], g[S::OW2 + i * H + j]);
-          da = fmaf(W2s[S::OW2 + i * H + j], dz2[j], da);
-        }
-        const float dz1 = da * lrelu_d(a1[i], alpha);
-        g[S::OB1 + i] += dz1;
-#pragma unroll
-        for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
-      }
-    }
-    RPH_STAMP(5);  // path loop done
-    // ---- in-wave reduce-scatter, cross-wave LDS sum ------------------------
-    wave_reduce_scatter<R>(g, lane);
-    constexpr int PER = R / 64;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
-    __syncthreads();
-    const int t = threadIdx.x;
-    val[0] = (t < R) ? (lds[t] + lds[R + t]) + (lds[2 * R + t] + lds[3 * R + t]) : 0.f;
-    __syncthreads();
-  }
-};
 
 // ---------------------------------------------------------------------------
 // K9: one optimizer step.  Grid = num_wgs workgroups of 256 threads.

@@ -169,6 +169,44 @@ struct PnlDesc {
   int nin, h, nout, head;
 };
 
+// Levenberg-Marquardt fit (hedge_lm.hip): full-batch MSE fits of the 8-unit
+// nets by damped Gauss-Newton steps.  One PASS = k_lm_pass (loss + gradient
+// over every local path, VALU; Gram matrix J^T J of a path subsample on the
+// matrix cores) -> k_lm_reduce (fixed-order sums of the per-workgroup slabs) ->
+// [data parallel: all-reduce of the reduced block] -> k_lm_solve (one
+// workgroup: accept / reject the trial point, damping, fp64 Cholesky solve of
+// (G + lam diag G) d = -g, next trial point).  Deterministic: no float atomics.
+constexpr int LM_NPMAX = 192;        // padded parameter count (6 x 32)
+constexpr int LM_TILE = 64;          // Gram subsample paths per gram workgroup (one MFMA K tile)
+// reduced block (doubles) of one trial point: [G blocks | g | stats]
+//   G: NB(NB+1)/2 upper-triangular 32x32 blocks in MFMA register order
+//   g: gradient of mean((V - y)^2) [LM_NPMAX]; stats: loss sum, |e| sum, ape sum, count
+constexpr int LM_GBLK_MAX = 21 * 1024;
+constexpr int LM_RED = LM_GBLK_MAX + LM_NPMAX + 8;
+// solver state (doubles)
+enum LmState : int {
+  LMS_W = 0,                         // [2][LM_NPMAX] weights of the two slots (trial / best)
+  LMS_RED = 2 * LM_NPMAX,            // [2][LM_RED] reduced blocks of the two slots
+  LMS_BEST = LMS_RED + 2 * LM_RED,   // index of the best slot
+  LMS_LAM,                           // damping
+  LMS_NACC,                          // accepted steps
+  LMS_FAIL,                          // Cholesky failures (non-positive pivot)
+  LMS_FLOATS = LMS_FAIL + 8
+};
+
+struct LmDesc {
+  double* state;                 // [LMS_FLOATS]
+  float* slab_b;                 // [num_wgs][R] per-workgroup gradient packets
+  float* slab_g;                 // [gram_wgs][NBLK * 1024] per-workgroup Gram blocks
+  int num_wgs;                   // pass-kernel grid
+  int gram_wgs;                  // workgroups [0, gram_wgs) add the Gram tile of local paths [64 wg, 64 wg + 64)
+  int red_wgs;                   // reduce-kernel grid
+  int passes;                    // trial points evaluated after the start point
+  float inv_ns;                  // 1 / (global Gram subsample size)
+  float inv_n;                   // 1 / (global path count)
+  float lam0, lam_up, lam_down, lam_min, lam_max, ridge;
+};
+
 // Eval stats slab columns
 enum EvalStat : int {
   ES_V = 0, ES_V2 = 1, ES_RES = 2, ES_RES2 = 3, ES_ABSRES = 4, ES_APE = 5, ES_PRED1 = 6,

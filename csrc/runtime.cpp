@@ -66,6 +66,10 @@ extern "C" int rph_layout(long long* out, int cap) {
       (long long)sizeof(PnlDesc), OFF(PnlDesc, feat_ts), OFF(PnlDesc, price), OFF(PnlDesc, price_ts),
       OFF(PnlDesc, snap), OFF(PnlDesc, bond), OFF(PnlDesc, pnl_out), OFF(PnlDesc, stats), OFF(PnlDesc, alpha),
       OFF(PnlDesc, has_b), OFF(PnlDesc, n_dates), OFF(PnlDesc, head),
+      // LmDesc + LM state layout
+      (long long)sizeof(LmDesc), OFF(LmDesc, slab_b), OFF(LmDesc, slab_g), OFF(LmDesc, num_wgs),
+      OFF(LmDesc, passes), OFF(LmDesc, inv_ns), OFF(LmDesc, lam0), OFF(LmDesc, ridge),
+      (long long)LM_NPMAX, (long long)LM_RED, (long long)LMS_BEST, (long long)LMS_FLOATS,
       // SimDesc
       (long long)sizeof(SimDesc), OFF(SimDesc, path_offset), OFF(SimDesc, sv1), OFF(SimDesc, dims1),
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),

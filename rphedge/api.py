@@ -231,7 +231,8 @@ class HedgeRun:
         tr = c.train
         tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
                            lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs,
-                           mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode)
+                           mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode,
+                           lm_gram_paths=int(tr.lm_gram_paths))
         if int(tr.variant) >= 0:
             tcfg.variant = int(tr.variant)
         kw = {}
@@ -254,7 +255,9 @@ class HedgeRun:
                                holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start,
                                restore_best_at_end=pf.restore_best_at_end, keep_paths=c.keep_paths,
                                poll_every=tr.poll_every, seed=tr.seed,
-                               feature_norm="none" if pf.raw_features else tr.feature_norm)
+                               feature_norm="none" if pf.raw_features else tr.feature_norm,
+                               optimizer=str(tr.optimizer).lower(), lm_passes_first=int(tr.lm_passes_first),
+                               lm_passes_rest=int(tr.lm_passes_rest))
         backend_q = None
         if (self.backend_kind == "hip" and self.di.world == 1 and icfg.q99 and not icfg.shared_q99_model
                 and not icfg.poll_every and tr.concurrent_q99):

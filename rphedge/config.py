@@ -81,6 +81,11 @@ class TrainingParams:
     step_mode: str = "auto"          # GPU step schedule: auto | lag | ticket | persistent (engine.TrainConfig)
     variant: int = -1                # narrow lag-kernel variant (-1: engine default; see engine.TrainConfig)
     concurrent_q99: bool = True      # two networks: run the pinball fit concurrently with the MSE fit (GPU)
+    optimizer: str = "adam"          # MSE fits: "adam" (Keras-Adam minibatches, the reference) | "lm" (full-batch
+                                     # Levenberg-Marquardt on the GPU: csrc/hedge_lm.hip; pinball fits stay Adam)
+    lm_passes_first: int = 80        # LM trial points on the first date (from the random init)
+    lm_passes_rest: int = 3          # LM trial points on later dates (warm start, Q18)
+    lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
     feature_norm: str = "date"       # input standardisation: none | global | date (driver.feature_norms);
                                      # ParityFlags.raw_features forces none (reference)
 

@@ -55,6 +55,9 @@ class InductionConfig:
     # "none" = raw features (reference), "global" = one mean/std per feature
     # pooled over all fitted dates, "date" = per-date mean/std
     feature_norm: str = "none"
+    optimizer: str = "adam"              # MSE fits: adam | lm (engine.FitConfig.optimizer)
+    lm_passes_first: int = 80
+    lm_passes_rest: int = 3
 
 
 @dataclass
@@ -174,6 +177,9 @@ class BackwardInduction:
 
     def _fcfg(self, first: bool, loss: int) -> FitConfig:
         c = self.cfg
+        if c.optimizer == "lm" and loss == L.LOSS_MSE:
+            return FitConfig(epochs=c.lm_passes_first if first else c.lm_passes_rest, loss=loss,
+                             optimizer="lm", early_stopping=False)
         return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
                          patience=c.patience_first if first else c.patience_rest,
                          loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else self.lr_rest,

@@ -82,6 +82,10 @@ class FitConfig:
     restore_best: bool = True
     restore_at_end: bool = False          # Keras-3 behaviour; Keras-2 restores only on early stop
     early_stopping: bool = True
+    # "adam" (the reference's Keras-Adam minibatch fit) or "lm": full-batch
+    # Levenberg-Marquardt passes (MSE fits of the 8-unit nets; ``epochs`` = the
+    # number of trial points after the start point; csrc/hedge_lm.hip)
+    optimizer: str = "adam"
 
     def key(self):
         return (self.epochs, self.patience if self.early_stopping else 1 << 30, self.restore_best,
@@ -105,6 +109,17 @@ class TrainConfig:
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
     mfma_fp32: bool = False        # 32-unit nets: exact fp32 MFMA instead of bf16 operands
+    # Levenberg-Marquardt fits (FitConfig.optimizer == "lm"): Gram matrix from a
+    # subsample of lm_gram_paths paths (global; 64-path tiles on the matrix
+    # cores), Marquardt damping lam0, x lam_up on a rejected trial, x lam_down
+    # on an accepted one, clamped to [lam_min, lam_max]; ridge x mean diagonal
+    lm_gram_paths: int = 4096
+    lm_lam0: float = 1e-3
+    lm_lam_up: float = 4.0
+    lm_lam_down: float = 1.0 / 3.0
+    lm_lam_min: float = 1e-9
+    lm_lam_max: float = 1e10
+    lm_ridge: float = 1e-10
     expose_packet: bool = False    # lagged fits: the finalize kernel writes the last step's summed (and
                                    # data-parallel exchanged) gradient packet to HipBackend.grad (tests)
     # optimizer-step schedule on the GPU:
@@ -382,6 +397,8 @@ class HipBackend:
         enqueueing; otherwise everything is asynchronous (graph-capturable) and
         surplus steps after an early stop are device-side no-ops."""
         assert len(data.feats) == self.spec.nin and len(data.prices_next) == self.spec.nhold - 1
+        if fcfg.optimizer == "lm":
+            return self._lm_fit(wts, opt, fit, data, fcfg)
         lr_t = self._lr(fcfg)
         d = self._train_desc(wts, opt, fit, data, fcfg, seed, lr_t)
         n, S = self.native, self.steps_per_epoch
@@ -434,6 +451,76 @@ class HipBackend:
             if poll_every and (e + 1) % poll_every == 0 and e + 1 < fcfg.epochs:
                 if float(fit[L.F_STOPPED].item()) != 0.0:
                     break
+
+    # -- Levenberg-Marquardt ----------------------------------------------------
+    def lm_supported(self) -> bool:
+        return self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head) is not None
+
+    def _lm_buffers(self):
+        def make():
+            shp = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+            if shp is None:
+                raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets only)")
+            P, R, nblk, two = shp
+            t = self.tcfg
+            nw = int(max(1, min(512 if two else 256, self.n_local // 256)))
+            ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // max(self.world, 1), self.n_local))
+            gw = int(max(1, min(ns_local // L.LM_TILE, nw)))
+            dev = self.device
+            lm = self.native.LmDesc()
+            bufs = dict(state=torch.zeros(L.LMS_FLOATS, dtype=torch.float64, device=dev),
+                        red=torch.zeros(L.LM_RED, dtype=torch.float64, device=dev),
+                        slab_b=torch.zeros(nw, R, dtype=torch.float32, device=dev),
+                        slab_g=torch.zeros(gw, nblk * 1024, dtype=torch.float32, device=dev))
+            lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
+            lm.num_wgs, lm.gram_wgs, lm.red_wgs = nw, gw, nblk * 1024 // 256 + 1
+            lm.inv_ns = 1.0 / float(gw * L.LM_TILE * max(self.world, 1))
+            lm.inv_n = 1.0 / float(self.n_local * max(self.world, 1))
+            lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
+            lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
+            bufs["desc"] = lm
+            return bufs
+        return self._cache.get(("lm",), make)
+
+    def _lm_fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
+        """Enqueue a full-batch Levenberg-Marquardt fit (MSE): ``fcfg.epochs``
+        trial points after the start point, 3 launches each (pass, reduce,
+        solve), graph-capturable; data parallel: the reduced [G | g | stats]
+        block is all-reduced between reduce and solve (one collective)."""
+        if fcfg.loss != L.LOSS_MSE:
+            raise ValueError("Levenberg-Marquardt fits minimise the MSE loss only")
+        b = self._lm_buffers()
+        lm = b["desc"]
+        lm.passes = int(fcfg.epochs)
+        d = self._train_desc(wts, opt, fit, data, fcfg, 0, None)
+        d.batch, d.steps_per_epoch, d.shuffle = self.n_local, 1, 0
+        d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
+        d.loss = L.LOSS_MSE
+        n = self.native
+        if self.world <= 1:
+            n.lm_fit(d, lm, b["red"], self.stream)
+            return
+        comm = self._lm_comm()
+        for k in range(lm.passes + 1):
+            n.lm_eval(d, lm, b["red"], k, self.stream)
+            comm.allreduce_(b["red"], self.stream)
+            n.lm_solve(d, lm, b["red"], k, self.stream)
+
+    def _lm_comm(self):
+        """Communicator for the LM reduced block: the backend's RCCL comm, or
+        one created on first use (collective: every rank runs the same fits)."""
+        if self.comm is not None:
+            return self.comm
+        if getattr(self, "_lm_nccl", None) is None:
+            from .parallel.dist import _store
+
+            self._lm_nccl = self.native.NcclComm(self.rank, self.world, _store(), tag="rph_lm")
+        return self._lm_nccl
+
+    def lm_state(self) -> dict:
+        """Host view of the last LM fit (accepted steps, Cholesky failures, damping)."""
+        st = self._lm_buffers()["state"].cpu().numpy()
+        return {"accepted": int(st[L.LMS_NACC]), "chol_failures": int(st[L.LMS_FAIL]), "lam": float(st[L.LMS_LAM])}
 
     def step_mode(self, poll_every: int = 0) -> str:
         """Resolve TrainConfig.step_mode for this backend (see TrainConfig)."""
@@ -594,9 +681,98 @@ class TorchBackend:
             dist.all_reduce(t)
         return t
 
+    def _lm_fit(self, wts, fit, data: DateData, fcfg: FitConfig):
+        """Reference semantics of the HIP Levenberg-Marquardt fit (hedge_lm.hip):
+        same trial sequence, damping rule, Gram subsample (the first
+        lm_gram_paths / world local paths) and bookkeeping, in float64."""
+        from torch.func import jacrev, vmap
+
+        spec, t = self.spec, self.tcfg
+        P = spec.nparams
+        dt = torch.float64
+        X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
+        pr = torch.stack([p.to(dt) for p in data.prices_next] +
+                         [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
+        y = data.target.to(dt)
+        W = max(self.world, 1)
+        n_glob = float(self.n_local * W)
+        nw = max(1, min(512, self.n_local // 256))
+        ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // W, self.n_local))
+        gw = max(1, min(ns_local // L.LM_TILE, nw))
+        ns = gw * L.LM_TILE
+        inv_ns = 1.0 / float(ns * W)
+
+        def v_one(w, x, p):
+            return (torch_forward(spec, w, x[None])[0] * p).sum()
+
+        def evaluate(w):
+            wg = w.detach().clone().requires_grad_(True)
+            e = (torch_forward(spec, wg, X) * pr).sum(1) - y
+            lsum = (e * e).sum()
+            (lsum / n_glob).backward()
+            J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X[:ns], pr[:ns])
+            red = torch.cat([(J.T @ J).reshape(-1) * inv_ns, wg.grad.detach(),
+                             torch.stack([lsum.detach(), e.detach().abs().sum(),
+                                          (e.detach().abs() / y.abs().clamp_min(1e-7)).sum(),
+                                          torch.tensor(float(len(y)), dtype=dt)])])
+            if self.world > 1:
+                self._allreduce(red)
+            G = red[: P * P].reshape(P, P)
+            g = red[P * P: P * P + P]
+            st = red[P * P + P:]
+            return G, g, st
+
+        cur = int(wts[L.W_CUR].item())
+        w_best = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
+        lam = float(t.lm_lam0)
+        hist = []
+        G, g, stb = evaluate(w_best)
+        Lb = float(stb[0] / stb[3].clamp_min(1.0))
+        hist.append(Lb)
+        trial = None
+        for k in range(1, int(fcfg.epochs) + 1):
+            A = 2.0 * G
+            dg = torch.diagonal(A).clone()
+            A = A + torch.diag(dg * lam + float(t.lm_ridge) * float(dg.mean()))
+            Lc, info = torch.linalg.cholesky_ex(A)
+            if int(info) != 0:
+                trial = w_best.clone()
+                lam = min(lam * t.lm_lam_up * t.lm_lam_up, t.lm_lam_max)
+            else:
+                trial = w_best + torch.cholesky_solve(-g[:, None], Lc)[:, 0]
+            Gt, gt, stt = evaluate(trial)
+            Lt = float(stt[0] / stt[3].clamp_min(1.0))
+            hist.append(Lt)
+            if Lt == Lt and Lt < Lb:
+                w_best, G, g, stb, Lb = trial, Gt, gt, stt, Lt
+                lam = max(lam * t.lm_lam_down, t.lm_lam_min)
+            else:
+                lam = min(lam * t.lm_lam_up, t.lm_lam_max)
+        w32 = w_best.to(torch.float32)
+        wts[:P] = w32
+        wts[L.PMAX:L.PMAX + P] = w32
+        wts[L.W_CUR] = 0.0
+        fit.zero_()
+        fit[L.F_WBEST:L.F_WBEST + P] = w32
+        c = max(float(stb[3]), 1.0)
+        fit[L.F_BEST] = Lb
+        fit[L.F_LAST_LOSS] = Lb
+        fit[L.F_LAST_MAE] = float(stb[1]) / c
+        fit[L.F_LAST_MAPE] = 100.0 * float(stb[2]) / c
+        fit[L.F_EPOCH] = len(hist)
+        fit[L.F_STOPPED] = 1.0
+        fit[L.F_HASBEST] = 1.0
+        k = min(len(hist), L.MAXHIST)
+        fit[L.F_HIST:L.F_HIST + k] = torch.tensor(hist[:k], dtype=torch.float32)
+        self.lm_last = {"lam": lam, "hist": hist}
+
     def fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig, seed: int, poll_every: int = 0):
         spec, dt = self.spec, self.dtype
         P = spec.nparams
+        if fcfg.optimizer == "lm":
+            if fcfg.loss != L.LOSS_MSE:
+                raise ValueError("Levenberg-Marquardt fits minimise the MSE loss only")
+            return self._lm_fit(wts, fit, data, fcfg)
         fit.copy_(fit_template(fcfg, self.device))
         X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
         pr = torch.stack([p.to(dt) for p in data.prices_next] +

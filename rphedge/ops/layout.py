@@ -58,3 +58,16 @@ LOSS_MSE, LOSS_PINBALL = 0, 1
 
 SIM_GBM_ARITH, SIM_GBM_LOG, SIM_SV_REF, SIM_HESTON, SIM_BASKET, SIM_MORTALITY = range(6)
 HESTON_EULER, HESTON_QE = 0, 1   # SimDesc.scheme (csrc/rph_types.h HestonScheme)
+
+# Levenberg-Marquardt solver (csrc/rph_types.h LmState)
+LM_NPMAX = 192
+LM_TILE = 64
+LM_GBLK_MAX = 21 * 1024
+LM_RED = LM_GBLK_MAX + LM_NPMAX + 8
+LMS_W = 0
+LMS_RED = 2 * LM_NPMAX
+LMS_BEST = LMS_RED + 2 * LM_RED
+LMS_LAM = LMS_BEST + 1
+LMS_NACC = LMS_BEST + 2
+LMS_FAIL = LMS_BEST + 3
+LMS_FLOATS = LMS_FAIL + 8

@@ -80,6 +80,16 @@ class PnlDesc(C.Structure):
     ]
 
 
+class LmDesc(C.Structure):
+    _fields_ = [
+        ("state", VP), ("slab_b", VP), ("slab_g", VP),
+        ("num_wgs", C.c_int), ("gram_wgs", C.c_int), ("red_wgs", C.c_int), ("passes", C.c_int),
+        ("inv_ns", C.c_float), ("inv_n", C.c_float),
+        ("lam0", C.c_float), ("lam_up", C.c_float), ("lam_down", C.c_float), ("lam_min", C.c_float),
+        ("lam_max", C.c_float), ("ridge", C.c_float),
+    ]
+
+
 class SimDesc(C.Structure):
     _fields_ = [
         ("model", C.c_int), ("n_local", C.c_int), ("path_offset", C.c_longlong),
@@ -116,6 +126,9 @@ def _expected_layout() -> list[int]:
         C.sizeof(PnlDesc), PnlDesc.feat_ts.offset, PnlDesc.price.offset, PnlDesc.price_ts.offset,
         PnlDesc.snap.offset, PnlDesc.bond.offset, PnlDesc.pnl_out.offset, PnlDesc.stats.offset,
         PnlDesc.alpha.offset, PnlDesc.has_b.offset, PnlDesc.n_dates.offset, PnlDesc.head.offset,
+        C.sizeof(LmDesc), LmDesc.slab_b.offset, LmDesc.slab_g.offset, LmDesc.num_wgs.offset,
+        LmDesc.passes.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset, LmDesc.ridge.offset,
+        L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
         S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset, S.sv_tscale.offset, S.scheme.offset,
@@ -151,6 +164,10 @@ def _bind(lib):
         "rph_train_ticket_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_pnl": (C.c_int, [C.POINTER(PnlDesc), VP]),
+        "rph_lm_shape": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4),
+        "rph_lm_eval": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
+        "rph_lm_solve": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
+        "rph_lm_fit": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
         "rph_payoff": (C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP, C.c_float, VP, VP, VP]),
@@ -184,7 +201,7 @@ def load(required: bool | None = None):
             _build.build(debug=v == "debug", asan=v == "asan")
         lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
         _bind(lib)
-        cap = 128
+        cap = 256
         buf = (C.c_longlong * cap)()
         n = lib.rph_layout(buf, cap)
         got = list(buf[:n])
@@ -288,6 +305,31 @@ def train_update(desc: TrainDesc, step: int, epoch: int, stream=None):
 
 def eval_(desc: EvalDesc, stream=None):
     _check(_lib.rph_eval(C.byref(desc), stream_handle(stream)), "rph_eval")
+
+
+def lm_shape(nin: int, h: int, nout: int, head: int):
+    """(P, R, Gram blocks, two workgroups per CU) of the LM kernels, or None."""
+    lib = load(required=True)
+    v = [C.c_int() for _ in range(4)]
+    if lib.rph_lm_shape(nin, h, nout, head, *[C.byref(x) for x in v]) != 0:
+        return None
+    return tuple(int(x.value) for x in v)
+
+
+def lm_eval(desc: TrainDesc, lm: LmDesc, red_new: torch.Tensor, pass_: int, stream=None):
+    _check(_lib.rph_lm_eval(C.byref(desc), C.byref(lm), ptr(red_new), int(pass_), stream_handle(stream)),
+           "rph_lm_eval")
+
+
+def lm_solve(desc: TrainDesc, lm: LmDesc, red_new: torch.Tensor, pass_: int, stream=None):
+    _check(_lib.rph_lm_solve(C.byref(desc), C.byref(lm), ptr(red_new), int(pass_), stream_handle(stream)),
+           "rph_lm_solve")
+
+
+def lm_fit(desc: TrainDesc, lm: LmDesc, red_new: torch.Tensor, stream=None):
+    """Whole single-rank Levenberg-Marquardt fit (csrc/hedge_lm.hip), launched from C++."""
+    load(required=True)
+    _check(_lib.rph_lm_fit(C.byref(desc), C.byref(lm), ptr(red_new), stream_handle(stream)), "rph_lm_fit")
 
 
 def pnl(desc: PnlDesc, stream=None):

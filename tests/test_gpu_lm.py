@@ -1,0 +1,138 @@
+"""Levenberg-Marquardt kernels (csrc/hedge_lm.hip) vs fp64 torch: one pass's
+reduced block [G | g | stats] (the Gram matrix on the matrix cores), whole
+fits vs the torch reference, run-to-run determinism, and the 30-date
+induction quality."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from test_lm_cpu import _teacher_problem
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (5, 8, 6, 0), (6, 8, 7, 0)]
+
+
+def _lm_row(q, h):
+    return (q & 3) + 8 * (q >> 2) + 4 * h
+
+
+def decode_gram(red, P):
+    """Dense G from the upper-triangular 32x32 blocks in MFMA register order."""
+    NP = (P + 31) // 32 * 32
+    NB = NP // 32
+    G = np.zeros((NP, NP))
+    b = 0
+    for mb in range(NB):
+        for nb in range(mb, NB):
+            blk = red[b * 1024:(b + 1) * 1024]
+            for q in range(16):
+                for lane in range(64):
+                    i = mb * 32 + _lm_row(q, lane >> 5)
+                    j = nb * 32 + (lane & 31)
+                    G[i, j] = G[j, i] = blk[q * 64 + lane]
+            b += 1
+    return G[:P, :P]
+
+
+def _setup(shape, n, dev, seed=0):
+    from rphedge.engine import DateData, HipBackend, TrainConfig
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(*shape)
+    feats, pr, y = _teacher_problem(spec, n, seed)
+    y = y + 0.05 * torch.sin(7 * feats[0])  # not exactly representable
+    data = DateData(feats=[f.to(dev) for f in feats], prices_next=[p.to(dev) for p in pr], bond_next=1.01,
+                    target=y.to(dev), prices_now=[p.to(dev) for p in pr], fmu=tuple([0.1] * spec.nin),
+                    fisd=tuple([1.5] * spec.nin))
+    w0 = init_weights(spec, [0.5] * spec.nout, seed=1)
+    return spec, feats, pr, y, data, w0
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_lm_pass_block_matches_fp64(shape):
+    from rphedge.engine import FitConfig, HipBackend, TrainConfig
+    from rphedge.models.hedge_mlp import torch_forward
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 15
+    spec, feats, pr, y, data, w0 = _setup(shape, n, dev)
+    be = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=4096), device=dev)
+    b = be._lm_buffers()
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    d = be._train_desc(w, o, f, data, FitConfig(), 0, None)
+    d.batch, d.steps_per_epoch, d.shuffle, d.inv_batch = n, 1, 0, 1.0 / n
+    lm = b["desc"]
+    lm.passes = 1
+    be.native.lm_eval(d, lm, b["red"], 0, None)
+    torch.cuda.synchronize()
+    red = b["red"].cpu().numpy()
+    P = spec.nparams
+    ns = lm.gram_wgs * 64
+    assert ns == 4096
+    # fp64 reference
+    X = (torch.stack(feats, 1).double() - 0.1) * 1.5
+    Pm = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
+    wt = torch.tensor(np.asarray(w0, np.float64), requires_grad=True)
+    e = (torch_forward(spec, wt, X) * Pm).sum(1) - y.double()
+    ((e * e).sum() / n).backward()
+    from torch.func import jacrev, vmap
+
+    J = vmap(jacrev(lambda ww, x, p: (torch_forward(spec, ww, x[None])[0] * p).sum()), in_dims=(None, 0, 0))(
+        wt.detach(), X[:ns], Pm[:ns])
+    G_ref = (J.T @ J).numpy() / ns
+    G = decode_gram(red, P)
+    assert np.linalg.norm(G - G_ref) / np.linalg.norm(G_ref) < 2e-5
+    g = red[L.LM_GBLK_MAX:L.LM_GBLK_MAX + P]
+    g_ref = wt.grad.numpy()
+    assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 2e-5
+    st = red[L.LM_GBLK_MAX + L.LM_NPMAX:L.LM_GBLK_MAX + L.LM_NPMAX + 4]
+    assert st[0] == pytest.approx(float((e * e).sum()), rel=1e-5) and st[3] == n
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (5, 8, 6, 0)])
+def test_lm_fit_matches_torch_and_is_deterministic(shape):
+    from rphedge.engine import FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 14
+    spec, feats, pr, y, data, w0 = _setup(shape, n, dev, seed=3)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=2048)
+    fc = FitConfig(epochs=12, optimizer="lm", early_stopping=False)
+    outs = []
+    for _ in range(2):
+        be = HipBackend(spec, n, tc, device=dev)
+        w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, fc, seed=0)
+        torch.cuda.synchronize()
+        outs.append((current_weights(spec, w), f.cpu().numpy(), be.lm_state()))
+    assert np.array_equal(outs[0][0], outs[1][0])           # bitwise reproducible (no float atomics)
+    assert outs[0][2]["chol_failures"] == 0
+    from rphedge.engine import DateData
+
+    cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
+    tb = TorchBackend(spec, n, tc)
+    wc, oc, fcs = tb.new_weights(w0), tb.new_opt(), tb.new_fit()
+    tb.fit(wc, oc, fcs, cd, fc, seed=0)
+    hist_g = outs[0][1][2048 + 16:2048 + 16 + 13]
+    hist_c = np.asarray(tb.lm_last["hist"])
+    # the trial losses follow the fp64 reference (same accept/reject decisions)
+    np.testing.assert_allclose(hist_g[:6], hist_c[:6], rtol=2e-3)
+    assert min(hist_g) == pytest.approx(min(hist_c), rel=2e-2)
+
+
+def test_lm_induction_quality_on_gpu():
+    """30-date European call, 2^18 paths, LM 80 / 3 passes: V0 at Black-
+    Scholes, the last date's residual at the BS-delta floor (0.304) and a
+    self-financing P&L near the BS delta hedge's (0.875)."""
+    from rphedge.api import european_option
+
+    r = european_option(N_paths=1 << 18, dt=1 / 30, rebalancing_frequency=1 / 30, batch_size=1 << 16,
+                        verbose=False, device="cuda", early_stopping=False, q99=False, chunk_log2=6,
+                        optimizer="lm", lm_passes_first=80, lm_passes_rest=3, keep_paths=False)
+    assert abs(r.v0 - 10.3896) < 0.1, r.v0
+    assert r.terminal_residual["std"] < 0.33, r.terminal_residual
+    assert r.terminal_pnl["kind"] == "self_financing" and r.terminal_pnl["std"] < 1.0, r.terminal_pnl
