@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   if ((int)blockIdx.x >= lm.gram_wgs) return;
   // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
   if (wid == 0) {
-    const long long p = (long long)blockIdx.x * LM_TILE + lane;
+    const long long slot = (long long)blockIdx.x * LM_TILE + lane;
+    const long long p = (slot / lm.gram_blk) * lm.gram_blk_stride + slot % lm.gram_blk;
     const bool ok = p < d.n_local;
     const long long q = ok ? p : 0;
     float x[NIN], pr[NHOLD];
@@ -186,21 +187,26 @@ __global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __re
     red[e] = s * (double)lm.inv_ns;
     return;
   }
-  // gradient packet (the last workgroup): GROUPS row groups per entry,
-  // combined in LDS in a fixed order
-  constexpr int GROUPS = 256 / R;
+  // gradient packet: workgroup pw handles entries [16 pw, 16 pw + 16), each
+  // over 16 row groups (rows g, g + 16, ...) combined in LDS in a fixed order
   __shared__ double part[256];
-  const int i = threadIdx.x % R, grp = threadIdx.x / R;
-  double s = 0.0;
-#pragma unroll 4
-  for (int w = grp; w < lm.num_wgs; w += GROUPS) s += (double)lm.slab_b[(size_t)w * R + i];
-  part[threadIdx.x] = s;
+  const int pw = blockIdx.x - NG / 256;
+  const int i = pw * 16 + (threadIdx.x & 15), grp = threadIdx.x >> 4;
+  double s0 = 0.0, s1 = 0.0;
+  int w = grp;
+  for (; w + 16 < lm.num_wgs; w += 32) {
+    s0 += (double)lm.slab_b[(size_t)w * R + i];
+    s1 += (double)lm.slab_b[(size_t)(w + 16) * R + i];
+  }
+  if (w < lm.num_wgs) s0 += (double)lm.slab_b[(size_t)w * R + i];
+  part[threadIdx.x] = s0 + s1;
   __syncthreads();
-  if (threadIdx.x < R) {
+  if (threadIdx.x < 16) {
     double v = 0.0;
-    for (int q = 0; q < GROUPS; ++q) v += part[q * R + threadIdx.x];
-    if (threadIdx.x < P) red[LM_GBLK_MAX + threadIdx.x] = v;
-    else if (threadIdx.x < P + 4) red[LM_GBLK_MAX + LM_NPMAX + threadIdx.x - P] = v;
+    for (int q = 0; q < 16; ++q) v += part[q * 16 + threadIdx.x];
+    const int e2 = pw * 16 + threadIdx.x;
+    if (e2 < P) red[LM_GBLK_MAX + e2] = v;
+    else if (e2 < P + 4) red[LM_GBLK_MAX + LM_NPMAX + e2 - P] = v;
   }
 }
 
@@ -211,15 +217,27 @@ __global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __re
 // ---------------------------------------------------------------------------
 RPH_INLINE int lm_tri(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower triangle, j <= i
 
+// LDS storage of the fp64 system matrix (lower triangle used): dense with an
+// odd pitch up to 128 parameters (no index arithmetic in the inner loops),
+// packed lower-triangular above (the 160 KB LDS holds 191 x 192 / 2 doubles)
+template <int P>
+struct LmSys {
+  static constexpr bool DENSE = P <= 128;
+  static constexpr int LD = P + 1;
+  static constexpr int ELEMS = DENSE ? P * LD : P * (P + 1) / 2;
+  RPH_INLINE static int idx(int i, int j) { return DENSE ? i * LD + j : lm_tri(i, j); }
+};
+
 template <int P, int R>
 __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDesc lm, const double* __restrict__ red_new,
                                                   const int pass) {
   using LS = LmShape<P>;
   constexpr int NB = LS::NB, NBLK = LS::NBLK;
   constexpr int NG = NBLK * 1024;
+  using SY = LmSys<P>;
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* A = lds;                          // packed lower triangle [P(P+1)/2]
-  double* vec = lds + P * (P + 1) / 2;      // [P] rhs / solution
+  double* A = lds;                          // system matrix, lower triangle (LmSys layout)
+  double* vec = lds + SY::ELEMS;            // [P] rhs / solution, then [P] pivots
   __shared__ int s_fail;
   __shared__ double s_diag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -291,41 +309,42 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       const int i = mb * 32 + lm_row(q, h), j = nb * 32 + r;  // i <= j when mb < nb
       if (i < P && j < P && (mb < nb || i >= j)) {
         const int hi = i > j ? i : j, lo = i > j ? j : i;
-        A[lm_tri(hi, lo)] = 2.0 * blk[q * 64 + lane];
+        A[SY::idx(hi, lo)] = 2.0 * blk[q * 64 + lane];
       }
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (wid == 0) {
     double s = 0.0;
-    for (int i = 0; i < P; ++i) s += A[lm_tri(i, i)];
-    s_diag = s / P;
-    s_fail = 0;
+    for (int i = lane; i < P; i += 64) s += A[SY::idx(i, i)];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) {
+      s_diag = s / P;
+      s_fail = 0;
+    }
   }
   __syncthreads();
   for (int i = tid; i < P; i += 256) {
-    double& a = A[lm_tri(i, i)];
+    double& a = A[SY::idx(i, i)];
     a = a * (1.0 + lam) + (double)lm.ridge * s_diag;
     vec[i] = -g[i];
   }
-  // ---- right-looking Cholesky, one barrier per column ---------------------------
+  // ---- right-looking Cholesky, one barrier per column; 16 x 16 thread tile ----
+  // over the trailing triangle (thread (ty, tx): rows k+1+ty (+16), columns
+  // k+1+tx (+16) up to the row); the L scaling is deferred to one pass below
+  const int ty = tid >> 4, tx = tid & 15;
   for (int k = 0; k < P; ++k) {
     __syncthreads();
-    const double akk = A[lm_tri(k, k)];
+    const double akk = A[SY::idx(k, k)];
     if (!(akk > 0.0)) {
       if (tid == 0) s_fail = 1;
       break;
     }
     const double rk = 1.0 / akk;
-    const int m = P - 1 - k;
-    const int cnt_t = m * (m + 1) / 2;
-    for (int t = tid; t < cnt_t; t += 256) {
-      int ii = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
-      while ((ii + 1) * (ii + 2) / 2 <= t) ++ii;
-      while (ii * (ii + 1) / 2 > t) --ii;
-      const int jj = t - ii * (ii + 1) / 2;
-      const int i = k + 1 + ii, j = k + 1 + jj;
-      A[lm_tri(i, j)] -= A[lm_tri(i, k)] * A[lm_tri(j, k)] * rk;
+    for (int i = k + 1 + ty; i < P; i += 16) {
+      const double aik = A[SY::idx(i, k)] * rk;
+      for (int j = k + 1 + tx; j <= i; j += 16) A[SY::idx(i, j)] -= aik * A[SY::idx(j, k)];
     }
   }
   __syncthreads();
@@ -340,40 +359,63 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
     return;
   }
-  // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k)
-  {
-    const int tot = P * (P + 1) / 2;
-    for (int t = tid; t < tot; t += 256) {
-      int i = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
-      while ((i + 1) * (i + 2) / 2 <= t) ++i;
-      while (i * (i + 1) / 2 > t) --i;
-      const int k = t - i * (i + 1) / 2;
-      A[t] = (i == k) ? sqrt(A[t]) : A[t] / sqrt(A[lm_tri(k, k)]);
-    }
-  }
+  // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k);
+  // the pivots are read into their own array first (the diagonal is rewritten)
+  double* dgs = vec + P;
+  for (int k = tid; k < P; k += 256) dgs[k] = sqrt(A[SY::idx(k, k)]);
   __syncthreads();
-  // ---- triangular solves in one wave (no barriers): L y = rhs, L^T d = y --------
+  for (int i = ty; i < P; i += 16)
+    for (int k = tx; k <= i; k += 16) {
+      double& a = A[SY::idx(i, k)];
+      a = (i == k) ? dgs[i] : a / dgs[k];
+    }
+  __syncthreads();
+  // ---- triangular solves in one wave, column-oriented: each lane keeps the
+  // right-hand side of rows lane, lane + 64, lane + 128 in registers; the
+  // solved entry of step m is broadcast with v_readlane (no LDS round trip on
+  // the dependency chain), the column / row of L comes from LDS
+  static_assert(P <= 192, "three rows per lane");
   if (wid == 0) {
-    for (int i = 0; i < P; ++i) {
-      double s = 0.0;
-      for (int m = lane; m < i; m += 64) s += A[lm_tri(i, m)] * vec[m];
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-      if (lane == 0) vec[i] = (vec[i] - s) / A[lm_tri(i, i)];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double b0 = lane < P ? vec[lane] : 0.0;
+    double b1 = lane + 64 < P ? vec[lane + 64] : 0.0;
+    double b2 = lane + 128 < P ? vec[lane + 128] : 0.0;
+    auto bcast = [](double v, int l) -> double {
+      const unsigned long long u = __double_as_longlong(v);
+      const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+      const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+      return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+    };
+    // forward: L y = b
+    for (int m = 0; m < P; ++m) {
+      const int src = m & 63;
+      const double bm = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
+      const double ym = bm / dgs[m];
+      if (lane == src) {
+        if (m < 64) b0 = ym;
+        else if (m < 128) b1 = ym;
+        else b2 = ym;
+      }
+      if (lane > m && lane < P) b0 -= A[SY::idx(lane, m)] * ym;
+      if (lane + 64 > m && lane + 64 < P) b1 -= A[SY::idx(lane + 64, m)] * ym;
+      if (lane + 128 > m && lane + 128 < P) b2 -= A[SY::idx(lane + 128, m)] * ym;
     }
-    for (int i = P - 1; i >= 0; --i) {
-      double s = 0.0;
-      for (int m = i + 1 + lane; m < P; m += 64) s += A[lm_tri(m, i)] * vec[m];
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-      if (lane == 0) vec[i] = (vec[i] - s) / A[lm_tri(i, i)];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // backward: L^T d = y
+    for (int m = P - 1; m >= 0; --m) {
+      const int src = m & 63;
+      const double ym = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
+      const double dm = ym / dgs[m];
+      if (lane == src) {
+        if (m < 64) b0 = dm;
+        else if (m < 128) b1 = dm;
+        else b2 = dm;
+      }
+      if (lane < m) b0 -= A[SY::idx(m, lane)] * dm;
+      if (lane + 64 < m) b1 -= A[SY::idx(m, lane + 64)] * dm;
+      if (lane + 128 < m) b2 -= A[SY::idx(m, lane + 128)] * dm;
     }
+    if (lane < P) vec[lane] = b0;
+    if (lane + 64 < P) vec[lane + 64] = b1;
+    if (lane + 128 < P) vec[lane + 128] = b2;
   }
   __syncthreads();
   for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i] + vec[i];
@@ -392,7 +434,7 @@ struct LmKernels {
   static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
   using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
   using S = NetShape<NIN, H, NO, HEAD>;
-  static int smem() { return (int)((S::P * (S::P + 1) / 2 + S::P) * sizeof(double)); }
+  static int smem() { return (int)((LmSys<S::P>::ELEMS + 2 * S::P) * sizeof(double)); }
 };
 
 static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {
@@ -401,9 +443,14 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (d->batch != d->n_local || d->steps_per_epoch != 1) return rph_report("rph_lm", "LM fits are full batch");
   if (lm->num_wgs < 1 || lm->num_wgs > 65535 || lm->passes < 0 || lm->passes >= MAXHIST)
     return rph_report("rph_lm", "bad num_wgs / passes");
-  if (lm->gram_wgs < 1 || lm->gram_wgs > lm->num_wgs || (long long)lm->gram_wgs * LM_TILE > d->n_local)
-    return rph_report("rph_lm", "gram_wgs must cover 64-path tiles inside the shard");
-  if (lm->red_wgs != nblk * 1024 / 256 + 1) return rph_report("rph_lm", "bad red_wgs");
+  if (lm->gram_wgs < 1 || lm->gram_wgs > lm->num_wgs || lm->gram_blk < 1 || lm->gram_blk > lm->gram_blk_stride)
+    return rph_report("rph_lm", "bad Gram subsample geometry");
+  {
+    const long long ns = (long long)lm->gram_wgs * LM_TILE;  // the last slot must stay inside the shard
+    const long long last = ((ns - 1) / lm->gram_blk) * lm->gram_blk_stride + (ns - 1) % lm->gram_blk;
+    if (last >= d->n_local) return rph_report("rph_lm", "Gram subsample leaves the shard");
+  }
+  if (lm->red_wgs != nblk * 1024 / 256 + R / 16) return rph_report("rph_lm", "bad red_wgs");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   (void)P;
   return 0;

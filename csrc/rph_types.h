@@ -199,9 +199,15 @@ struct LmDesc {
   float* slab_b;                 // [num_wgs][R] per-workgroup gradient packets
   float* slab_g;                 // [gram_wgs][NBLK * 1024] per-workgroup Gram blocks
   int num_wgs;                   // pass-kernel grid
-  int gram_wgs;                  // workgroups [0, gram_wgs) add the Gram tile of local paths [64 wg, 64 wg + 64)
+  int gram_wgs;                  // workgroups [0, gram_wgs) add the Gram tile of subsample slots [64 wg, 64 wg + 64)
   int red_wgs;                   // reduce-kernel grid
   int passes;                    // trial points evaluated after the start point
+  // Gram subsample: the global path range is cut into 8 aligned blocks and
+  // the first gram_blk paths of each block are used (aligned prefixes of a
+  // Sobol sequence are nets; the same global subsample at world size 1, 2,
+  // 4, 8): slot j of this rank = local path (j / gram_blk) * gram_blk_stride + j % gram_blk
+  int gram_blk;
+  int gram_blk_stride;
   float inv_ns;                  // 1 / (global Gram subsample size)
   float inv_n;                   // 1 / (global path count)
   float lam0, lam_up, lam_down, lam_min, lam_max, ridge;

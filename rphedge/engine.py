@@ -170,6 +170,19 @@ class PnlData:
 
 
 PNL_PPT = 4  # paths per thread of k_hedge_pnl (csrc/hedge_mlp.hip PNL_PPT)
+GRAM_BLOCKS = 8  # global blocks of the LM Gram subsample (the largest single-node world size)
+
+
+def lm_gram_geometry(n_local: int, ns_local: int, world: int) -> tuple[int, int]:
+    """(gram_blk, gram_blk_stride) of the LM Gram subsample (LmDesc): the
+    global path range is cut into GRAM_BLOCKS aligned blocks and the first
+    paths of each block are used, so the subsample is the same set of global
+    paths at world size 1, 2, 4, 8 (aligned prefixes of a Sobol sequence are
+    nets; a strided subset is not: every 2^k-th point shares k digits)."""
+    bpr = max(1, GRAM_BLOCKS // max(int(world), 1))   # blocks per rank
+    while bpr > 1 and (ns_local % bpr or n_local % bpr):
+        bpr //= 2
+    return max(1, ns_local // bpr), max(1, n_local // bpr)
 MAXIN = 8
 
 
@@ -473,7 +486,8 @@ class HipBackend:
                         slab_b=torch.zeros(nw, R, dtype=torch.float32, device=dev),
                         slab_g=torch.zeros(gw, nblk * 1024, dtype=torch.float32, device=dev))
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
-            lm.num_wgs, lm.gram_wgs, lm.red_wgs = nw, gw, nblk * 1024 // 256 + 1
+            lm.num_wgs, lm.gram_wgs, lm.red_wgs = nw, gw, nblk * 1024 // 256 + R // 16
+            lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, gw * L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(gw * L.LM_TILE * max(self.world, 1))
             lm.inv_n = 1.0 / float(self.n_local * max(self.world, 1))
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
@@ -701,6 +715,8 @@ class TorchBackend:
         gw = max(1, min(ns_local // L.LM_TILE, nw))
         ns = gw * L.LM_TILE
         inv_ns = 1.0 / float(ns * W)
+        blk, bstride = lm_gram_geometry(self.n_local, ns, self.world)
+        sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
 
         def v_one(w, x, p):
             return (torch_forward(spec, w, x[None])[0] * p).sum()
@@ -710,7 +726,7 @@ class TorchBackend:
             e = (torch_forward(spec, wg, X) * pr).sum(1) - y
             lsum = (e * e).sum()
             (lsum / n_glob).backward()
-            J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X[:ns], pr[:ns])
+            J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X[sub], pr[sub])
             red = torch.cat([(J.T @ J).reshape(-1) * inv_ns, wg.grad.detach(),
                              torch.stack([lsum.detach(), e.detach().abs().sum(),
                                           (e.detach().abs() / y.abs().clamp_min(1e-7)).sum(),

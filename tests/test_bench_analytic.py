@@ -56,7 +56,8 @@ def test_bench_cpu_preset_contract():
     assert KEYS <= set(r)
     assert r["n_gpus"] == 1 and r["steps"] == 1 and r["higher_is_better"] is True and r["scaling"] == "weak"
     assert r["config"]["preset"] == "euro1_cpu" and r["config"]["parallelism"] == "dp1"
-    assert r["value"] > 0 and r["vs_baseline"] == pytest.approx(r["value"] / (512 / 0.006))
+    assert r["value"] > 0 and r["vs_baseline"] == pytest.approx(r["value"] / (4096.0 / ((500 + 29 * 904 / 51) * 0.048)))
+    assert r["path_samples_per_s"] == pytest.approx(r["value"] * r["full_passes_per_run"])
     assert r["quality"]["anchor"]["analytic"] == "black_scholes"
 
 

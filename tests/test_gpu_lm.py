@@ -81,8 +81,10 @@ def test_lm_pass_block_matches_fp64(shape):
     ((e * e).sum() / n).backward()
     from torch.func import jacrev, vmap
 
+    sub = torch.tensor([(j // lm.gram_blk) * lm.gram_blk_stride + j % lm.gram_blk for j in range(ns)])
+    assert lm.gram_blk == ns // 8 and lm.gram_blk_stride == n // 8
     J = vmap(jacrev(lambda ww, x, p: (torch_forward(spec, ww, x[None])[0] * p).sum()), in_dims=(None, 0, 0))(
-        wt.detach(), X[:ns], Pm[:ns])
+        wt.detach(), X[sub], Pm[sub])
     G_ref = (J.T @ J).numpy() / ns
     G = decode_gram(red, P)
     assert np.linalg.norm(G - G_ref) / np.linalg.norm(G_ref) < 2e-5
