@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   // already final are skipped by wave-uniform branches.  Above 128 parameters
   // the elements stay in (packed) LDS.
   const int ty = tid >> 4, tx = tid & 15;
+  __syncthreads();  // the damped diagonal is in place
   if constexpr (SY::DENSE) {
     __shared__ double colb[2][128];
     double Rg[8][8];
@@ -365,21 +366,28 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
         if (tid == 0) s_fail = 1;
         break;
       }
-      const double rk = 1.0 / akk;
+      double rk = __builtin_amdgcn_rcp(akk);  // + one Newton step: ~0.5 ulp
+      rk = rk * (2.0 - akk * rk);
       double ri[8], cj[8];
 #pragma unroll
       for (int a = 0; a < 8; ++a) ri[a] = ck[ty + 16 * a] * rk;
 #pragma unroll
       for (int b = 0; b < 8; ++b) cj[b] = ck[tx + 16 * b];
+      // only columns j > k change: blocks b < k/16 are final (skipped,
+      // uniform), blocks above k/16 update unconditionally, the block holding
+      // column k selects per lane; rows that are final / above the diagonal
+      // / beyond P only collect harmless values in unused upper-triangle slots
+      // (the published columns are zero beyond P)
+      const int bk = k >> 4;
+      const bool lane_act = tx > k - 16 * bk;
 #pragma unroll
       for (int a = 0; a < 8; ++a) {
         if (16 * a + (wid * 4) + 3 <= k) continue;          // the wave's rows of block a are final
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          if (16 * b + 15 <= k || b > a) continue;          // final columns / above the diagonal block
-          const int i = ty + 16 * a, j = tx + 16 * b;
+        for (int b = 0; b <= a; ++b) {
+          if (b < bk) continue;
           const double v = Rg[a][b] - ri[a] * cj[b];
-          Rg[a][b] = (j > k && j <= i && i < P) ? v : Rg[a][b];
+          Rg[a][b] = (b > bk || lane_act) ? v : Rg[a][b];
         }
       }
       // publish column k+1 (final now) into the other buffer

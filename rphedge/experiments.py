@@ -32,6 +32,37 @@ def mts_parameters(**over) -> dict:
     return p
 
 
+def mts_notebook_parameters(**over) -> dict:
+    """The paths behind the "Multi Time Step.ipynb" HEADLINE numbers (Q15):
+    cell 9 ("SV - Version", exec 94) overwrote ``Y_paths`` after the GBM cell -
+    log-Euler fund paths with vol s0 = sigma_0 = 0.15965 held CONSTANT (Q6:
+    ``vt[:,t]`` is read before it is written, so it is the fill value) and
+    mu = 0.09464, dt = 1/365 (3651 fine steps), Sobol seed 1235 ("Multi Time
+    Step.ipynb":218-248); mortality and the quarterly induction as in the
+    notebook's training cells (shared Q99 model, c = 0.1, Keras LR schedule,
+    ``parity=True``).  Published: V0 = 981,038.213, phi0 / psi0 = 643,687 /
+    350,888, overall residual VaR 98.5 / 99 / 99.5 % = -121.96 / 54.38 /
+    1,160.76 EUR (":1039", ":987-988", ":954-956")."""
+    p = mts_parameters(dt=1 / 365, model="gbm_log", mu=0.09464, sigma=0.15965, parity=True)
+    p.update(over)
+    return p
+
+
+MTS_NOTEBOOK_PUBLISHED = {"V0": 981_038.213, "phi0": 643_687.0, "psi0": 350_888.0,
+                          "VaR": (-121.96, 54.38, 1_160.76)}
+
+
+def mts_notebook(**over) -> dict:
+    """Run :func:`mts_notebook_parameters` and report the notebook's headline
+    quantities next to the published ones."""
+    res = run_params(mts_notebook_parameters(**over))
+    out = {"V0": res.v0, "phi0": res.phi, "psi0": res.psi, "published": MTS_NOTEBOOK_PUBLISHED,
+           "epochs_mse": res.summary.get("epochs_mse"), "result": res}
+    if res.var:
+        out["VaR"] = [res.var[k] for k in ("VaR(98.5%)", "VaR(99.0%)", "VaR(99.5%)") if k in res.var]
+    return out
+
+
 def sv_parameters(**over) -> dict:
     """``sv_parameters`` of "Multi Time Step.ipynb":2612-2639 (duplicate 'c' key: later value wins, Q4)."""
     p = dict(Y=1, K=1, T=10, mu=0.09464, r=0.03, s0=0.15965, a=0.0033566, b=0.15431, c=0.075,

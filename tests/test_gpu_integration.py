@@ -129,3 +129,20 @@ def test_concurrent_q99_fit_matches_sequential():
     assert rc.phi == pytest.approx(rs.phi, rel=1e-5)
     assert rc.psi == pytest.approx(rs.psi, rel=1e-5)
     assert rc.v0 == pytest.approx(rs.v0, rel=1e-5)
+
+
+def test_mts_notebook_headline():
+    """The "Multi Time Step.ipynb" headline run (Q15 paths: log-Euler fund,
+    constant vol 0.15965, dt = 1/365, 4096 Sobol paths, quarterly; shared Q99
+    model, Keras schedule; parity).  Published: V0 981,038.213, phi0 / psi0
+    643,687 / 350,888.  Bands: V0 +-1.5 % (the liability value is pinned by the
+    paths), holdings +-12 % (the reference's own seed / TF scatter: its RP-module
+    run of the same liability printed 634,349 / 350,176)."""
+    from rphedge.experiments import MTS_NOTEBOOK_PUBLISHED as PUB
+    from rphedge.experiments import mts_notebook
+
+    out = mts_notebook(verbose=False, poll_every=10)
+    _record("mts_notebook", {k: v for k, v in out.items() if k != "result"})
+    assert abs(out["V0"] / PUB["V0"] - 1) < 0.015, out["V0"]
+    assert abs(out["phi0"] / PUB["phi0"] - 1) < 0.12, out["phi0"]
+    assert abs(out["psi0"] / PUB["psi0"] - 1) < 0.12, out["psi0"]
