@@ -228,6 +228,211 @@ struct LmSys {
   RPH_INLINE static int idx(int i, int j) { return DENSE ? i * LD + j : lm_tri(i, j); }
 };
 
+// fp64 reciprocal / reciprocal square root from the hardware approximations
+// (v_rcp_f64 / v_rsq_f64) + two Newton steps (~1 ulp): the IEEE division and
+// sqrt sequences cost ~100 ns each on the dependency chains of the solver
+RPH_INLINE double lm_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+}
+RPH_INLINE double lm_rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
+  return y * __builtin_fma(-0.5 * x * y, y, 1.5);
+}
+
+// Blocked (8-column panels) fp64 Cholesky + triangular solves of the LM
+// system for up to 128 parameters, one workgroup.  Thread (ty, tx) keeps the
+// elements (ty + 16 a, tx + 16 b) of the trailing matrix in REGISTERS; per
+// panel of 8 columns: the panel columns are broadcast through LDS, the 8 x 8
+// diagonal block is factorised redundantly by the row threads, every row's
+// L21 entries are solved once (phase 1), then every thread applies the rank-8
+// update to its register tile (phase 2) and the owners publish the next panel.
+// P/8 panels -> 2 barriers each instead of one barrier + a rank-1 update per
+// column.  The matrix is padded to a multiple of 8 with identity rows.  L is
+// written over A (lower triangle, SY layout); the solution replaces vec.
+template <int P, class SY>
+RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsigned long long* stamps) {
+#define RPH_STAMPB(k) do { if (stamps != nullptr && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  constexpr int PB = (P + 7) / 8 * 8;
+  constexpr int NK = PB / 8;
+  static_assert(PB <= 128, "blocked solver: up to 128 parameters");
+  __shared__ double colb[2][8][128];
+  __shared__ double uL[128][9];
+  __shared__ double Li[NK][8][8];  // inverses of the diagonal blocks (for the solves)
+  __shared__ double ytmp[8];
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15, wid = tid >> 6;
+  double Rg[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int i = ty + 16 * a, j = tx + 16 * b;
+      Rg[a][b] = (i < P && j <= i) ? A[SY::idx(i, j)] : ((i == j && i < PB) ? 1.0 : 0.0);
+    }
+  for (int t = tid; t < 128 * 9; t += 256) (&uL[0][0])[t] = 0.0;
+  if (tx < 8) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a) colb[0][tx][ty + 16 * a] = Rg[a][0];
+  }
+  for (int K = 0; K < NK; ++K) {
+    const int k0 = 8 * K;
+    __syncthreads();
+    if (K == 6) RPH_STAMPB(8);
+    const double(*cb)[128] = colb[K & 1];
+    // ---- phase 1: row threads t in [k0, PB): diagonal block + L21 row ----------
+    if (tid >= k0 && tid < PB) {
+      double L[8][8], rl[8];
+      bool ok = true;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        double sc = cb[c][k0 + c];
+#pragma unroll
+        for (int p = 0; p < c; ++p) sc -= L[c][p] * L[c][p];
+        ok = ok && sc > 0.0;
+        rl[c] = lm_rsq(sc);  // 1 / L_cc
+        L[c][c] = sc * rl[c];
+#pragma unroll
+        for (int r = c + 1; r < 8; ++r) {
+          double v = cb[c][k0 + r];
+#pragma unroll
+          for (int p = 0; p < c; ++p) v -= L[r][p] * L[c][p];
+          L[r][c] = v * rl[c];
+        }
+      }
+      if (!ok && tid == k0) *s_fail = 1;
+      const int i = tid;
+      if (i >= k0 + 8) {
+        double u[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          double v = cb[c][i];
+#pragma unroll
+          for (int p = 0; p < c; ++p) v -= u[p] * L[c][p];
+          u[c] = v * rl[c];
+          uL[i][c] = u[c];
+          if (i < P && k0 + c < P) A[SY::idx(i, k0 + c)] = u[c];
+        }
+      } else if (i < P) {
+        const int rr = i - k0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (r == rr) {
+#pragma unroll
+            for (int c = 0; c <= r; ++c)
+              if (k0 + c < P) A[SY::idx(i, k0 + c)] = L[r][c];
+          }
+      }
+    }
+    __syncthreads();
+    if (K == 6) RPH_STAMPB(9);
+    if (*s_fail) return;
+    // ---- phase 2: rank-8 update of the trailing register tile + next panel ----
+    const int kn = k0 + 8;
+    if (kn >= PB) break;
+    const int bk = kn >> 4, off = kn & 15;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (16 * a + wid * 4 + 3 < kn) continue;  // the wave's rows of block a are final
+      double ua[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ua[q] = uL[ty + 16 * a][q];
+#pragma unroll
+      for (int b = 0; b <= a; ++b) {
+        if (b < bk) continue;
+        double sv = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sv = __builtin_fma(ua[q], uL[tx + 16 * b][q], sv);
+        const bool act = b > bk || tx >= off;
+        Rg[a][b] = act ? Rg[a][b] - sv : Rg[a][b];
+      }
+    }
+    if (tx >= off && tx < off + 8) {
+      double(*cn)[128] = colb[(K + 1) & 1];
+#define RPH_PUBK(BB)                                                               \
+  case BB:                                                                         \
+    _Pragma("unroll") for (int a = 0; a < 8; ++a) cn[tx - off][ty + 16 * a] = Rg[a][BB]; \
+    break;
+      switch (bk) { RPH_PUBK(0) RPH_PUBK(1) RPH_PUBK(2) RPH_PUBK(3) RPH_PUBK(4) RPH_PUBK(5) RPH_PUBK(6) RPH_PUBK(7) }
+#undef RPH_PUBK
+    }
+    if (K == 6) RPH_STAMPB(10);
+  }
+  __syncthreads();
+  RPH_STAMPB(6);
+  // inverses of the diagonal blocks, one block per thread (off the panel loop's
+  // critical path): Linv[r][c] = -Linv[r][r] sum_{q=c}^{r-1} L[r][q] Linv[q][c]
+  if (tid < NK) {
+    const int k0 = 8 * tid;
+    double Lv[8][8], Lb[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c <= r; ++c) Lb[r][c] = k0 + r < P ? A[SY::idx(k0 + r, k0 + c)] : (r == c ? 1.0 : 0.0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      Lv[c][c] = lm_rcp(Lb[c][c]);
+#pragma unroll
+      for (int r = c + 1; r < 8; ++r) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = c; q < r; ++q) v = __builtin_fma(Lb[r][q], Lv[q][c], v);
+        Lv[r][c] = -lm_rcp(Lb[r][r]) * v;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) Li[tid][r][c] = c <= r ? Lv[r][c] : 0.0;
+  }
+  __syncthreads();
+  RPH_STAMPB(7);
+  // ---- blocked triangular solves: L y = b, then L^T d = y (in vec) --------------
+  // per block: the 8 diagonal entries by a matvec with the stored block
+  // inverse (8 threads), then the row updates (all threads): two short phases
+  for (int K = 0; K < NK; ++K) {
+    const int k0 = 8 * K;
+    if (tid < 8) {
+      double v = 0.0;
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (p <= tid && k0 + p < P) v = __builtin_fma(Li[K][tid][p], vec[k0 + p], v);
+      ytmp[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 8 && k0 + tid < P) vec[k0 + tid] = ytmp[tid];
+    for (int i = k0 + 8 + tid; i < P; i += 256) {
+      double v = vec[i];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (k0 + c < P) v -= A[SY::idx(i, k0 + c)] * ytmp[c];
+      vec[i] = v;
+    }
+    __syncthreads();
+  }
+  for (int K = NK - 1; K >= 0; --K) {
+    const int k0 = 8 * K;
+    if (tid < 8) {
+      double v = 0.0;
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (p >= tid && k0 + p < P) v = __builtin_fma(Li[K][p][tid], vec[k0 + p], v);
+      ytmp[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 8 && k0 + tid < P) vec[k0 + tid] = ytmp[tid];
+    for (int i = tid; i < k0; i += 256) {
+      double v = vec[i];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (k0 + c < P) v -= A[SY::idx(k0 + c, i)] * ytmp[c];
+      vec[i] = v;
+    }
+    __syncthreads();
+  }
+}
+
 template <int P, int R>
 __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDesc lm, const double* __restrict__ red_new,
                                                   const int pass) {
@@ -333,88 +538,26 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     vec[i] = -g[i];
   }
   RPH_STAMP(2);
-  // ---- right-looking Cholesky, one barrier per column ----------------------------
-  // thread (ty, tx) owns the elements (ty + 16 a, tx + 16 b); up to 128
-  // parameters they live in REGISTERS for the whole factorisation (8 x 8
-  // doubles): per step k the owners of column k+1 publish it to a double-
-  // buffered LDS column, everybody reads the two broadcast vectors and
-  // updates its trailing elements in place; whole row / column blocks that are
-  // already final are skipped by wave-uniform branches.  Above 128 parameters
-  // the elements stay in (packed) LDS.
-  const int ty = tid >> 4, tx = tid & 15;
   __syncthreads();  // the damped diagonal is in place
   if constexpr (SY::DENSE) {
-    __shared__ double colb[2][128];
-    double Rg[8][8];
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int i = ty + 16 * a, j = tx + 16 * b;
-        Rg[a][b] = (i < P && j <= i) ? A[SY::idx(i, j)] : 0.0;
-      }
-    // column 0
-    if (tx == 0) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a) colb[0][ty + 16 * a] = Rg[a][0];
-    }
-    for (int k = 0; k < P; ++k) {
-      __syncthreads();
-      const double* ck = colb[k & 1];
-      const double akk = ck[k];
-      if (!(akk > 0.0)) {
-        if (tid == 0) s_fail = 1;
-        break;
-      }
-      double rk = __builtin_amdgcn_rcp(akk);  // + one Newton step: ~0.5 ulp
-      rk = rk * (2.0 - akk * rk);
-      double ri[8], cj[8];
-#pragma unroll
-      for (int a = 0; a < 8; ++a) ri[a] = ck[ty + 16 * a] * rk;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) cj[b] = ck[tx + 16 * b];
-      // only columns j > k change: blocks b < k/16 are final (skipped,
-      // uniform), blocks above k/16 update unconditionally, the block holding
-      // column k selects per lane; rows that are final / above the diagonal
-      // / beyond P only collect harmless values in unused upper-triangle slots
-      // (the published columns are zero beyond P)
-      const int bk = k >> 4;
-      const bool lane_act = tx > k - 16 * bk;
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        if (16 * a + (wid * 4) + 3 <= k) continue;          // the wave's rows of block a are final
-#pragma unroll
-        for (int b = 0; b <= a; ++b) {
-          if (b < bk) continue;
-          const double v = Rg[a][b] - ri[a] * cj[b];
-          Rg[a][b] = (b > bk || lane_act) ? v : Rg[a][b];
-        }
-      }
-      // publish column k+1 (final now) into the other buffer
-      const int kn = k + 1;
-      if (kn < P) {
-        const int bn = kn >> 4;
-        double* cn = colb[kn & 1];
-        if (tx == (kn & 15)) {
-#define RPH_PUB(BB)                                                     \
-  case BB:                                                              \
-    _Pragma("unroll") for (int a = 0; a < 8; ++a) cn[ty + 16 * a] = Rg[a][BB]; \
-    break;
-          switch (bn) { RPH_PUB(0) RPH_PUB(1) RPH_PUB(2) RPH_PUB(3) RPH_PUB(4) RPH_PUB(5) RPH_PUB(6) RPH_PUB(7) }
-#undef RPH_PUB
-        }
-      }
-    }
+    lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, d.stamps);
     __syncthreads();
-    // elements back to LDS for the scaling and the triangular solves
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int i = ty + 16 * a, j = tx + 16 * b;
-        if (i < P && j <= i) A[SY::idx(i, j)] = Rg[a][b];
+    if (s_fail) {
+      // not positive definite at this damping: re-evaluate the best point with
+      // more damping (trial := best)
+      for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
+      if (tid == 0) {
+        st[LMS_BEST] = (double)best;
+        st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
+        st[LMS_FAIL] += 1.0;
       }
+      return;
+    }
+    RPH_STAMP(4);
   } else {
+    // packed LDS storage (more than 128 parameters): column-by-column
+    // right-looking Cholesky, one barrier per column
+    const int ty = tid >> 4, tx = tid & 15;
     for (int k = 0; k < P; ++k) {
       __syncthreads();
       const double akk = A[SY::idx(k, k)];
@@ -428,83 +571,83 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
         for (int j = k + 1 + tx; j <= i; j += 16) A[SY::idx(i, j)] -= aik * A[SY::idx(j, k)];
       }
     }
-  }
-  __syncthreads();
-  if (s_fail) {
-    // not positive definite at this damping: re-evaluate the best point with
-    // more damping (trial := best)
-    for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
-    if (tid == 0) {
-      st[LMS_BEST] = (double)best;
-      st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
-      st[LMS_FAIL] += 1.0;
+    __syncthreads();
+    if (s_fail) {
+      // not positive definite at this damping: re-evaluate the best point with
+      // more damping (trial := best)
+      for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
+      if (tid == 0) {
+        st[LMS_BEST] = (double)best;
+        st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
+        st[LMS_FAIL] += 1.0;
+      }
+      return;
     }
-    return;
-  }
-  // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k);
-  // the pivots are read into their own array first (the diagonal is rewritten)
-  RPH_STAMP(3);
-  double* dgs = vec + P;
-  for (int k = tid; k < P; k += 256) dgs[k] = sqrt(A[SY::idx(k, k)]);
-  __syncthreads();
-  double* rdg = vec + 2 * P;  // reciprocal pivots for the solves
-  for (int k = tid; k < P; k += 256) rdg[k] = 1.0 / dgs[k];
-  __syncthreads();
-  for (int i = ty; i < P; i += 16)
+    // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k);
+    // the pivots are read into their own array first (the diagonal is rewritten)
+    RPH_STAMP(3);
+    double* dgs = vec + P;
+    for (int k = tid; k < P; k += 256) dgs[k] = sqrt(A[SY::idx(k, k)]);
+    __syncthreads();
+    double* rdg = vec + 2 * P;  // reciprocal pivots for the solves
+    for (int k = tid; k < P; k += 256) rdg[k] = 1.0 / dgs[k];
+    __syncthreads();
+    for (int i = ty; i < P; i += 16)
     for (int k = tx; k <= i; k += 16) {
       double& a = A[SY::idx(i, k)];
       a = (i == k) ? dgs[i] : a / dgs[k];
     }
-  __syncthreads();
-  // ---- triangular solves in one wave, column-oriented: each lane keeps the
-  // right-hand side of rows lane, lane + 64, lane + 128 in registers; the
-  // solved entry of step m is broadcast with v_readlane (no LDS round trip on
-  // the dependency chain), the column / row of L comes from LDS
-  RPH_STAMP(4);
-  static_assert(P <= 192, "three rows per lane");
-  if (wid == 0) {
-    double b0 = lane < P ? vec[lane] : 0.0;
-    double b1 = lane + 64 < P ? vec[lane + 64] : 0.0;
-    double b2 = lane + 128 < P ? vec[lane + 128] : 0.0;
-    auto bcast = [](double v, int l) -> double {
-      const unsigned long long u = __double_as_longlong(v);
-      const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
-      const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-      return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-    };
-    // forward: L y = b
-    for (int m = 0; m < P; ++m) {
-      const int src = m & 63;
-      const double bm = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
-      const double ym = bm * rdg[m];
-      if (lane == src) {
-        if (m < 64) b0 = ym;
-        else if (m < 128) b1 = ym;
-        else b2 = ym;
+    __syncthreads();
+    // ---- triangular solves in one wave, column-oriented: each lane keeps the
+    // right-hand side of rows lane, lane + 64, lane + 128 in registers; the
+    // solved entry of step m is broadcast with v_readlane (no LDS round trip on
+    // the dependency chain), the column / row of L comes from LDS
+    RPH_STAMP(4);
+    static_assert(P <= 192, "three rows per lane");
+    if (wid == 0) {
+      double b0 = lane < P ? vec[lane] : 0.0;
+      double b1 = lane + 64 < P ? vec[lane + 64] : 0.0;
+      double b2 = lane + 128 < P ? vec[lane + 128] : 0.0;
+      auto bcast = [](double v, int l) -> double {
+        const unsigned long long u = __double_as_longlong(v);
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+        return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+      };
+      // forward: L y = b
+      for (int m = 0; m < P; ++m) {
+        const int src = m & 63;
+        const double bm = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
+        const double ym = bm * rdg[m];
+        if (lane == src) {
+          if (m < 64) b0 = ym;
+          else if (m < 128) b1 = ym;
+          else b2 = ym;
+        }
+        if (lane > m && lane < P) b0 -= A[SY::idx(lane, m)] * ym;
+        if (lane + 64 > m && lane + 64 < P) b1 -= A[SY::idx(lane + 64, m)] * ym;
+        if (lane + 128 > m && lane + 128 < P) b2 -= A[SY::idx(lane + 128, m)] * ym;
       }
-      if (lane > m && lane < P) b0 -= A[SY::idx(lane, m)] * ym;
-      if (lane + 64 > m && lane + 64 < P) b1 -= A[SY::idx(lane + 64, m)] * ym;
-      if (lane + 128 > m && lane + 128 < P) b2 -= A[SY::idx(lane + 128, m)] * ym;
-    }
-    // backward: L^T d = y
-    for (int m = P - 1; m >= 0; --m) {
-      const int src = m & 63;
-      const double ym = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
-      const double dm = ym * rdg[m];
-      if (lane == src) {
-        if (m < 64) b0 = dm;
-        else if (m < 128) b1 = dm;
-        else b2 = dm;
+      // backward: L^T d = y
+      for (int m = P - 1; m >= 0; --m) {
+        const int src = m & 63;
+        const double ym = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
+        const double dm = ym * rdg[m];
+        if (lane == src) {
+          if (m < 64) b0 = dm;
+          else if (m < 128) b1 = dm;
+          else b2 = dm;
+        }
+        if (lane < m) b0 -= A[SY::idx(m, lane)] * dm;
+        if (lane + 64 < m) b1 -= A[SY::idx(m, lane + 64)] * dm;
+        if (lane + 128 < m) b2 -= A[SY::idx(m, lane + 128)] * dm;
       }
-      if (lane < m) b0 -= A[SY::idx(m, lane)] * dm;
-      if (lane + 64 < m) b1 -= A[SY::idx(m, lane + 64)] * dm;
-      if (lane + 128 < m) b2 -= A[SY::idx(m, lane + 128)] * dm;
+      if (lane < P) vec[lane] = b0;
+      if (lane + 64 < P) vec[lane + 64] = b1;
+      if (lane + 128 < P) vec[lane + 128] = b2;
     }
-    if (lane < P) vec[lane] = b0;
-    if (lane + 64 < P) vec[lane + 64] = b1;
-    if (lane + 128 < P) vec[lane + 128] = b2;
+    __syncthreads();
   }
-  __syncthreads();
   RPH_STAMP(5);
   for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i] + vec[i];
   if (tid == 0) {

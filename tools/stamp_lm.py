@@ -38,7 +38,12 @@ def run(n_log2=20, nin=1, passes=40):
     e1.record()
     torch.cuda.synchronize()
     st = be.stamps[0].cpu().tolist()
-    ph = {f"solve_phase_{k}_{k + 1}_us": (st[k + 1] - st[k]) / 100.0 for k in range(5) if st[k + 1] and st[k]}
+    order = [k for k in (0, 1, 2, 6, 7, 3, 4, 5) if st[k]]
+    ph = {f"solve_phase_{a}_{b}_us": (st[b] - st[a]) / 100.0 for a, b in zip(order, order[1:])}
+    s1 = be.stamps[1].cpu().tolist()
+    if s1[0] and s1[1] and s1[2]:
+        ph["panel6_phase1_us"] = (s1[1] - s1[0]) / 100.0
+        ph["panel6_phase2_us"] = (s1[2] - s1[1]) / 100.0
     return {"n_log2": n_log2, "nin": nin, "passes": passes, "us_per_pass": 1000.0 * e0.elapsed_time(e1) / (passes + 1),
             **ph, "lm": be.lm_state()}
 

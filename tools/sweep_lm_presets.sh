@@ -1,0 +1,12 @@
+#!/bin/bash
+# LM vs Adam on every BASELINE preset (quality vs time), one JSON line per run.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+for p in heston30 euro252; do
+  for opt in adam lm; do
+    timeout -k 10 200 python bench.py --preset $p --optimizer $opt --steps 2 --warmup 1 \
+      | grep '^{' >> gpurun_out/sweep_presets_lm.jsonl || exit 1
+  done
+done
+timeout -k 10 300 python bench.py --preset basket5 --optimizer lm --lm-passes-rest 2 --steps 1 --warmup 1 \
+  | grep '^{' >> gpurun_out/sweep_presets_lm.jsonl || exit 1
