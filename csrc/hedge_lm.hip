@@ -483,7 +483,18 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const double* g = best_red + LM_GBLK_MAX;
   if (pass == lm.passes) {  // final pass: publish the best point
     for (int i = tid; i < P; i += 256) {
-      const float w = (float)st[LMS_W + best * LM_NPMAX + i];
+      double wd = st[LMS_W + best * LM_NPMAX + i];
+      if (i == lm.bias_index) {
+        // exact Newton step on this bias alone (the loss is quadratic in it):
+        // d = -g_i / (2 G_ii), G_ii from the diagonal 32x32 Gram block
+        const int kb = i >> 5, ri = i & 31;
+        int b = 0;
+        for (int m = 0; m < kb; ++m) b += LS::NB - m;
+        const int q = (ri >> 3) * 4 + (ri & 3), hh = (ri >> 2) & 1;
+        const double gii = best_red[(size_t)b * 1024 + q * 64 + hh * 32 + ri];
+        if (gii > 0.0) wd -= g[i] / (2.0 * gii);
+      }
+      const float w = (float)wd;
       d.wts->w[0][i] = w;
       d.fit->w_best[i] = w;
     }

@@ -211,6 +211,11 @@ struct LmDesc {
   float inv_ns;                  // 1 / (global Gram subsample size)
   float inv_n;                   // 1 / (global path count)
   float lam0, lam_up, lam_down, lam_min, lam_max, ridge;
+  // after the last pass, the parameter bias_index (the bond holding's output
+  // bias) takes an exact 1-D Newton step: the value fit's residual mean over
+  // all paths becomes zero, so no drift accumulates over the dates; -1: off
+  int bias_index;
+  int pad1;
 };
 
 // Eval stats slab columns

@@ -120,6 +120,10 @@ class TrainConfig:
     lm_lam_min: float = 1e-9
     lm_lam_max: float = 1e10
     lm_ridge: float = 1e-10
+    # after the last pass: exact Newton step on the bond holding's output bias
+    # (free heads), so the fitted values' mean over all paths equals the
+    # target's and no mean error drifts down the backward induction
+    lm_bias_fix: bool = True
     expose_packet: bool = False    # lagged fits: the finalize kernel writes the last step's summed (and
                                    # data-parallel exchanged) gradient packet to HipBackend.grad (tests)
     # optimizer-step schedule on the GPU:
@@ -171,6 +175,12 @@ class PnlData:
 
 PNL_PPT = 4  # paths per thread of k_hedge_pnl (csrc/hedge_mlp.hip PNL_PPT)
 GRAM_BLOCKS = 8  # global blocks of the LM Gram subsample (the largest single-node world size)
+
+
+def _lm_bias_index(spec, t) -> int:
+    """LmDesc.bias_index: the bond holding's output bias (the last parameter of
+    a free-head net), -1 for the complement head or with lm_bias_fix off."""
+    return spec.nparams - 1 if (t.lm_bias_fix and spec.head == L.HEAD_FREE) else -1
 
 
 def lm_gram_geometry(n_local: int, ns_local: int, world: int) -> tuple[int, int]:
@@ -492,6 +502,7 @@ class HipBackend:
             lm.inv_n = 1.0 / float(self.n_local * max(self.world, 1))
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
+            lm.bias_index = _lm_bias_index(self.spec, t)
             bufs["desc"] = lm
             return bufs
         return self._cache.get(("lm",), make)
@@ -764,6 +775,10 @@ class TorchBackend:
                 lam = max(lam * t.lm_lam_down, t.lm_lam_min)
             else:
                 lam = min(lam * t.lm_lam_up, t.lm_lam_max)
+        bi = _lm_bias_index(spec, t)
+        if bi >= 0 and float(G[bi, bi]) > 0.0:
+            w_best = w_best.clone()
+            w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
         w32 = w_best.to(torch.float32)
         wts[:P] = w32
         wts[L.PMAX:L.PMAX + P] = w32
