@@ -41,6 +41,8 @@ class ParityFlags:
     paired_sobol: bool = False          # Q25: SV price / vol shocks from two scrambled Sobol sequences of the
                                         # SAME dimensions (RP:274-275; dependent, not independent, shocks);
                                         # False = one sequence of 2 n_fine dimensions
+    keras_fit_only: bool = False        # the Keras fit's weights are used as they are (no exact bias refit
+                                        # after the Adam MSE fits, TrainingParams.mean_refit)
 
     @classmethod
     def reference(cls) -> "ParityFlags":
@@ -48,7 +50,8 @@ class ParityFlags:
                    sv_c_overwrite=True, sv_reference_dynamics=True, sv_sqrt_nan=True,
                    fine_terminal_payoff=True, lr_schedule_first_only=True, warm_start=True,
                    restore_best_at_end=False, numpy_binomial=True, local_residual_pnl=True,
-                   complement_head=True, eo_discount_artifact=True, raw_features=True, paired_sobol=True)
+                   complement_head=True, eo_discount_artifact=True, raw_features=True, paired_sobol=True,
+                   keras_fit_only=True)
 
 
 @dataclass
@@ -86,6 +89,8 @@ class TrainingParams:
     lm_passes_first: int = 80        # LM trial points on the first date (from the random init)
     lm_passes_rest: int = 3          # LM trial points on later dates (warm start, Q18)
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
+    mean_refit: bool = True          # after each Adam MSE fit: exact refit of the bond holding's bias (the
+                                     # residual mean over all paths -> 0; no mean error drifts into V0)
     feature_norm: str = "date"       # input standardisation: none | global | date (driver.feature_norms);
                                      # ParityFlags.raw_features forces none (reference)
 

@@ -58,6 +58,9 @@ class InductionConfig:
     optimizer: str = "adam"              # MSE fits: adam | lm (engine.FitConfig.optimizer)
     lm_passes_first: int = 80
     lm_passes_rest: int = 3
+    # after each Adam MSE fit: exact refit of the bond holding's output bias
+    # (engine bias_refit; LM fits do it in their last solve)
+    mean_refit: bool = False
 
 
 @dataclass
@@ -227,6 +230,8 @@ class BackwardInduction:
                     join.record(self._side)
             be.fit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE),
                    seed=fit_seed(c.seed, t, 0), poll_every=c.poll_every)
+            if c.mean_refit and c.optimizer != "lm":
+                be.bias_refit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE))
             hold_out = [self.holdings[t, k] for k in range(self.spec.nhold)] if self.holdings is not None else None
             resid_out = self.residuals[t] if self.residuals is not None else None
             if c.q99:

@@ -531,6 +531,50 @@ class HipBackend:
             comm.allreduce_(b["red"], self.stream)
             n.lm_solve(d, lm, b["red"], k, self.stream)
 
+    def bias_refit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
+        """Exact refit of the bond holding's output bias after an Adam fit (one
+        full-batch loss + gradient pass at the fitted weights, then the 1-D
+        Newton step of the LM solver, FitState untouched): the residual's mean
+        over all paths becomes zero, so no mean error drifts down the induction
+        (V0 then sits on the paths' price instead of scattering with the
+        minibatch noise of the last fits).  No-op for complement heads."""
+        bi = _lm_bias_index(self.spec, self.tcfg)
+        if bi < 0:
+            return
+        if not self.lm_supported():
+            # nets without an LM solver (32-unit MFMA family): the eval kernel's
+            # residual sum (res = target - prediction) gives the same step
+            st = self._cache.get(("refit_stats",), self.new_stats)
+            self.eval(wts, data, st)
+            tot = st[:, [L.ES_RES, L.ES_COUNT]].sum(0)
+            if self.world > 1:
+                self._lm_comm().allreduce_(tot, self.stream)
+            delta = (tot[0] / tot[1].clamp_min(1.0) / float(data.bond_next)).to(torch.float32)
+            wts[bi] += delta
+            fit[L.F_WBEST + bi] = wts[bi]
+            return
+        b = self._lm_buffers()
+
+        def make():
+            src = b["desc"]
+            lm = type(src).from_buffer_copy(src)
+            lm.passes, lm.weights_only, lm.gram_wgs = 0, 1, 1
+            lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
+            lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
+            return lm
+        lm = self._cache.get(("lm_refit",), make)
+        d = self._train_desc(wts, opt, fit, data, fcfg, 0, None)
+        d.batch, d.steps_per_epoch, d.shuffle = self.n_local, 1, 0
+        d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
+        d.loss = L.LOSS_MSE
+        n = self.native
+        if self.world <= 1:
+            n.lm_fit(d, lm, b["red"], self.stream)
+            return
+        n.lm_eval(d, lm, b["red"], 0, self.stream)
+        self._lm_comm().allreduce_(b["red"], self.stream)
+        n.lm_solve(d, lm, b["red"], 0, self.stream)
+
     def _lm_comm(self):
         """Communicator for the LM reduced block: the backend's RCCL comm, or
         one created on first use (collective: every rank runs the same fits)."""
@@ -796,6 +840,26 @@ class TorchBackend:
         k = min(len(hist), L.MAXHIST)
         fit[L.F_HIST:L.F_HIST + k] = torch.tensor(hist[:k], dtype=torch.float32)
         self.lm_last = {"lam": lam, "hist": hist}
+
+    def bias_refit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
+        """Reference semantics of HipBackend.bias_refit: b_psi -= mean(e) / B
+        (e = fitted value - target over all paths, B = the bond price)."""
+        spec = self.spec
+        bi = _lm_bias_index(spec, self.tcfg)
+        if bi < 0:
+            return
+        dt = torch.float64
+        X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
+        pr = torch.stack([p.to(dt) for p in data.prices_next] +
+                         [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
+        cur = int(wts[L.W_CUR].item())
+        w = wts[cur * L.PMAX: cur * L.PMAX + spec.nparams].to(dt)
+        e = (torch_forward(spec, w, X) * pr).sum(1) - data.target.to(dt)
+        es = self._allreduce(torch.stack([e.sum(), torch.tensor(float(e.numel()), dtype=dt)]))
+        wb = float(w[bi] - es[0] / es[1] / float(data.bond_next))
+        for k in range(2):
+            wts[k * L.PMAX + bi] = wb
+        fit[L.F_WBEST + bi] = wb
 
     def fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig, seed: int, poll_every: int = 0):
         spec, dt = self.spec, self.dtype

@@ -86,7 +86,7 @@ class LmDesc(C.Structure):
         ("num_wgs", C.c_int), ("gram_wgs", C.c_int), ("red_wgs", C.c_int), ("passes", C.c_int),
         ("gram_blk", C.c_int), ("gram_blk_stride", C.c_int), ("inv_ns", C.c_float), ("inv_n", C.c_float),
         ("lam0", C.c_float), ("lam_up", C.c_float), ("lam_down", C.c_float), ("lam_min", C.c_float),
-        ("lam_max", C.c_float), ("ridge", C.c_float), ("bias_index", C.c_int), ("pad1", C.c_int),
+        ("lam_max", C.c_float), ("ridge", C.c_float), ("bias_index", C.c_int), ("weights_only", C.c_int),
     ]
 
 
@@ -128,7 +128,7 @@ def _expected_layout() -> list[int]:
         PnlDesc.alpha.offset, PnlDesc.has_b.offset, PnlDesc.n_dates.offset, PnlDesc.head.offset,
         C.sizeof(LmDesc), LmDesc.slab_b.offset, LmDesc.slab_g.offset, LmDesc.num_wgs.offset,
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
-        LmDesc.ridge.offset, LmDesc.bias_index.offset,
+        LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,

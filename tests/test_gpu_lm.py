@@ -140,3 +140,46 @@ def test_lm_induction_quality_on_gpu():
     assert abs(r.v0 - 10.3896) < 0.1, r.v0
     assert r.terminal_residual["std"] < 0.33, r.terminal_residual
     assert r.terminal_pnl["kind"] == "self_financing" and r.terminal_pnl["std"] < 1.0, r.terminal_pnl
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (5, 8, 6, 0)])
+def test_bias_refit_matches_torch(shape):
+    """HipBackend.bias_refit (k_lm_pass + k_lm_reduce + k_lm_solve with passes
+    = 0, weights only) after a few Adam steps equals the torch reference
+    refit (b_psi -= mean(e) / B); the full-batch residual mean is ~0 after it
+    and the FitState record of the Adam fit is untouched."""
+    from rphedge.engine import FitConfig, HipBackend, TorchBackend, TrainConfig
+    from rphedge.models.hedge_mlp import torch_forward
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 14
+    spec, feats, pr, y, data, w0 = _setup(shape, n, dev)
+    be = HipBackend(spec, n, TrainConfig(batch_size=1 << 12), device=dev)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    fc = FitConfig(epochs=2, early_stopping=False)
+    be.fit(w, o, f, data, fc, seed=0)
+    torch.cuda.synchronize()
+    P = spec.nparams
+    w_fit = w[:P].double().cpu()
+    f_before = f.clone()
+    be.bias_refit(w, o, f, data, fc)
+    torch.cuda.synchronize()
+    w_hip = w[:P].double().cpu()
+    # torch reference on the same fitted weights
+    tb = TorchBackend(spec, n, TrainConfig(batch_size=1 << 12))
+    wt = tb.new_weights(w_fit.float().numpy())
+    datac = type(data)(feats=[x.cpu() for x in data.feats], prices_next=[p.cpu() for p in data.prices_next],
+                       bond_next=data.bond_next, target=data.target.cpu(), prices_now=None, fmu=data.fmu,
+                       fisd=data.fisd)
+    tb.bias_refit(wt, tb.new_opt(), tb.new_fit(), datac, fc)
+    assert torch.equal(w_hip[:-1], w_fit[:-1])
+    assert float(w_hip[-1]) == pytest.approx(float(wt[P - 1]), abs=2e-5)
+    X = (torch.stack(feats, 1).double() - 0.1) * 1.5
+    Pm = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
+    e = (torch_forward(spec, w_hip, X) * Pm).sum(1) - y.double()
+    assert abs(float(e.mean())) < 2e-5
+    skip = set(range(L.F_WBEST, L.F_WBEST + P))
+    fb, fa = f_before.cpu().view(torch.int32), f.cpu().view(torch.int32)   # bitwise (NaN-filled history)
+    diff = [i for i in range(f.numel()) if i not in skip and int(fa[i]) != int(fb[i])]
+    assert not diff, diff[:10]

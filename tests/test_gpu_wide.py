@@ -7,6 +7,8 @@ permutation).
 * bf16 (default): v_mfma_f32_32x32x16_bf16 operands -> loss history and fitted
   values match to bf16 rounding of activations/gradients.
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -93,12 +95,15 @@ def test_wide_european_end_to_end(dev, feature_norm):  # noqa: F811
     assert run.spec.hidden == 32
     res = run.run()
     # phi0 is stable; V0 (the net evaluated at the single point S0, i.e. its
-    # bond holding) scatters between runs at this small budget (float-atomic
-    # summation order): +-0.3 with raw inputs, 10.1-10.9 with an outlier at 8.8
-    # in 7 runs with standardised inputs (tools/wide_e2e_scatter.py,
-    # profiles/wide_e2e_scatter_r1.jsonl), whose P&L std is ~25 % lower
+    # bond holding) used to scatter between runs at this small budget (round
+    # 1: 10.1-10.9 with an outlier at 8.8 in 7 runs, an 11.34 in round 2):
+    # every date's bias drifted with the minibatch noise of its last Adam
+    # steps.  The exact bond-bias refit after each fit (mean_refit) puts V0 on
+    # the paths' discounted MC payoff
+    mc = res.summary["E_payoff"] * res.scale * math.exp(-0.08)
     assert abs(res.phi - 0.7285) < 0.03, res.phi
-    assert abs(res.v0 - 10.3896) < (0.8 if feature_norm == "none" else 2.0), res.v0
+    assert abs(res.v0 - mc) < 0.05, (res.v0, mc)
+    assert abs(res.v0 - 10.3896) < 0.3, res.v0
     assert res.terminal_residual["std"] < (1.3 if feature_norm == "none" else 0.9), res.terminal_residual
     # self-financing P&L over the 12 monthly dates (BS delta hedge on the same grid: ~1.4)
     assert res.terminal_pnl["kind"] == "self_financing" and res.terminal_pnl["std"] < 2.5, res.terminal_pnl

@@ -69,3 +69,62 @@ def test_lm_induction_beats_adam_on_cpu():
     assert m.terminal_residual["std"] < 0.5 and m.terminal_residual["std"] < 0.6 * a.terminal_residual["std"]
     assert m.terminal_pnl["std"] < 1.1 and m.terminal_pnl["std"] < 0.6 * a.terminal_pnl["std"]
     assert m.induction.dates[0].fit_mse["epochs"] == 61
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0)])
+def test_bias_refit_zeroes_mean_residual(shape):
+    """engine bias_refit (after an Adam fit): the bond holding's output bias
+    moves by -mean(e) / B, the full-batch residual mean becomes zero and the
+    loss can only drop (exact 1-D least squares); complement heads untouched."""
+    from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig
+    from rphedge.models.hedge_mlp import NetSpec, init_weights, torch_forward
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(*shape)
+    n = 1 << 11
+    feats, pr, y = _teacher_problem(spec, n)
+    y = y + 0.05   # a mean offset the Adam fit below does not remove
+    data = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr)
+    be = TorchBackend(spec, n, TrainConfig(batch_size=256))
+    w, o, f = be.new_weights(init_weights(spec, [0.5] * spec.nout, seed=1)), be.new_opt(), be.new_fit()
+    fc = FitConfig(epochs=3, early_stopping=False)
+    be.fit(w, o, f, data, fc, seed=0)
+
+    def resid(wv):
+        X = torch.stack(feats, 1).double()
+        P = torch.stack(pr + [torch.full((n,), 1.01)], 1).double()
+        return (torch_forward(spec, wv.double(), X) * P).sum(1) - y.double()
+
+    cur = int(w[L.W_CUR].item())
+    e0 = resid(w[cur * L.PMAX: cur * L.PMAX + spec.nparams])
+    be.bias_refit(w, o, f, data, fc)
+    e1 = resid(w[cur * L.PMAX: cur * L.PMAX + spec.nparams])
+    assert abs(float(e0.mean())) > 1e-3
+    assert abs(float(e1.mean())) < 1e-5
+    assert float((e1 ** 2).mean()) <= float((e0 ** 2).mean())
+    assert torch.allclose(e1, e0 - e0.mean(), atol=1e-5)
+
+    eo = NetSpec(1, 8, 1, L.HEAD_COMPLEMENT)
+    be2 = TorchBackend(eo, n, TrainConfig(batch_size=256))
+    w2 = be2.new_weights(init_weights(eo, [0.5], seed=1))
+    before = w2.clone()
+    be2.bias_refit(w2, be2.new_opt(), be2.new_fit(), DateData(feats=feats[:1], prices_next=pr[:1], bond_next=1.01,
+                                                              target=y, prices_now=pr[:1]), fc)
+    assert torch.equal(w2, before)
+
+
+def test_mean_refit_keeps_v0_on_price_cpu():
+    """30-date European call through the API with Adam fits: mean_refit (the
+    corrected default) puts V0 on the paths' discounted MC payoff; the parity
+    flag keras_fit_only switches it off."""
+    from rphedge.api import run_params
+
+    base = dict(Y=100, K=100, T=1.0, mu=0.08, r=0.08, sigma=0.15, N=1, P=1, x=0, l0=0, c=0, ita=0,
+                mortality=False, q99=False, dt=1 / 12, rebalancing=1 / 12, n_paths=12, payoff="call",
+                option_type="CALL", model="gbm_log", batch_size=1 << 10, epochs_first=30, epochs_rest=4,
+                lr=1e-2, lr_schedule_first=False, early_stopping=False, verbose=False, device="cpu")
+    on = run_params(base)
+    off = run_params(dict(base, mean_refit=False))
+    mc = on.summary["E_payoff"] * on.scale * math.exp(-0.08)
+    assert abs(on.v0 / mc - 1) < 2e-3, (on.v0, mc)
+    assert abs(on.v0 - off.v0) > 1e-4   # the refit is active in the default run
