@@ -24,6 +24,8 @@
 //                canonical NetWeights and the FitState bookkeeping.
 // The start point is pass 0; `passes` trial points follow.  Everything stays
 // on the device and graph-captures with the rest of the induction.
+#include <utility>
+
 #include "hedge_core.h"
 #include "hedge_narrow.h"
 
@@ -242,39 +244,217 @@ RPH_INLINE double lm_rsq(double x) {
   return y * __builtin_fma(-0.5 * x * y, y, 1.5);
 }
 
-// Blocked (8-column panels) fp64 Cholesky + triangular solves of the LM
-// system for up to 128 parameters, one workgroup.  Thread (ty, tx) keeps the
-// elements (ty + 16 a, tx + 16 b) of the trailing matrix in REGISTERS; per
-// panel of 8 columns: the panel columns are broadcast through LDS, the 8 x 8
-// diagonal block is factorised redundantly by the row threads, every row's
-// L21 entries are solved once (phase 1), then every thread applies the rank-8
-// update to its register tile (phase 2) and the owners publish the next panel.
-// P/8 panels -> 2 barriers each instead of one barrier + a rank-1 update per
-// column.  The matrix is padded to a multiple of 8 with identity rows.  L is
-// written over A (lower triangle, SY layout); the solution replaces vec.
+// Both triangular solves L y = b, L^T d = y of the LM system in ONE wave (no
+// barriers), blocked by 8 columns: lane l keeps the right-hand side of rows
+// l, l + 64, l + 128 in registers; per block the 8 current entries are
+// gathered to every lane with v_readlane, the 8 x 8 diagonal block is solved
+// redundantly on every lane (its L entries are LDS broadcasts), then every
+// lane applies the block to its own rows (8 independent products, tree sum).
+// rdg = reciprocal pivots.  The solution replaces vec.
 template <int P, class SY>
-RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsigned long long* stamps) {
-#define RPH_STAMPB(k) do { if (stamps != nullptr && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-  constexpr int PB = (P + 7) / 8 * 8;
-  constexpr int NK = PB / 8;
-  static_assert(PB <= 128, "blocked solver: up to 128 parameters");
-  __shared__ double colb[2][8][128];
-  __shared__ double uL[128][9];
-  __shared__ double Li[NK][8][8];  // inverses of the diagonal blocks (for the solves)
-  __shared__ double ytmp[8];
-  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15, wid = tid >> 6;
-  double Rg[8][8];
+RPH_INLINE void lm_tri_solve_wave(const double* A, double* vec, const double* rdg) {
+  static_assert(P <= 192, "three rows per lane");
+  constexpr int NS = (P + 63) / 64, NB = (P + 7) / 8;
+  const int lane = threadIdx.x & 63;
+  double b[NS];
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int s = 0; s < NS; ++s) b[s] = lane + 64 * s < P ? vec[lane + 64 * s] : 0.0;
+  auto bcast = [](double v, int l) -> double {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+  };
+  auto slot = [&](int sK) -> double {  // b[sK] for a wave-uniform sK
+    double v = b[0];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int i = ty + 16 * a, j = tx + 16 * b;
-      Rg[a][b] = (i < P && j <= i) ? A[SY::idx(i, j)] : ((i == j && i < PB) ? 1.0 : 0.0);
+    for (int s = 1; s < NS; ++s) v = sK == s ? b[s] : v;
+    return v;
+  };
+  // ---- forward: L y = b --------------------------------------------------------
+  for (int K = 0; K < NB; ++K) {
+    const int k0 = 8 * K, sK = k0 >> 6, l0 = k0 & 63;
+    double lr[NS][8];  // this lane's rows of the block's columns (independent of the chain)
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int row = lane + 64 * s;
+        lr[s][c] = (row >= k0 + 8 && row < P && k0 + c < P) ? A[SY::idx(row, k0 + c)] : 0.0;
+      }
+    const double bs = slot(sK);
+    double y[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      double v = bcast(bs, l0 + c);
+#pragma unroll
+      for (int q = 0; q < c; ++q) v = __builtin_fma(-A[SY::idx(k0 + c, k0 + q)], y[q], v);
+      y[c] = k0 + c < P ? v * rdg[k0 + c] : 0.0;
     }
-  for (int t = tid; t < 128 * 9; t += 256) (&uL[0][0])[t] = 0.0;
-  if (tx < 8) {
 #pragma unroll
-    for (int a = 0; a < 8; ++a) colb[0][tx][ty + 16 * a] = Rg[a][0];
+    for (int s = 0; s < NS; ++s) {
+      const double t01 = __builtin_fma(lr[s][1], y[1], lr[s][0] * y[0]);
+      const double t23 = __builtin_fma(lr[s][3], y[3], lr[s][2] * y[2]);
+      const double t45 = __builtin_fma(lr[s][5], y[5], lr[s][4] * y[4]);
+      const double t67 = __builtin_fma(lr[s][7], y[7], lr[s][6] * y[6]);
+      b[s] -= (t01 + t23) + (t45 + t67);
+      if (s == sK) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) b[s] = lane == l0 + c ? y[c] : b[s];
+      }
+    }
+  }
+  // ---- backward: L^T d = y -----------------------------------------------------
+  for (int K = NB - 1; K >= 0; --K) {
+    const int k0 = 8 * K, sK = k0 >> 6, l0 = k0 & 63;
+    double lr[NS][8];  // L[k0 + c][row] for this lane's rows below k0
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int row = lane + 64 * s;
+        lr[s][c] = (row < k0 && k0 + c < P) ? A[SY::idx(k0 + c, row)] : 0.0;
+      }
+    const double bs = slot(sK);
+    double dv[8];
+#pragma unroll
+    for (int c = 7; c >= 0; --c) {
+      double v = bcast(bs, l0 + c);
+#pragma unroll
+      for (int q = 7; q > c; --q)
+        if (k0 + q < P) v = __builtin_fma(-A[SY::idx(k0 + q, k0 + c)], dv[q], v);
+      dv[c] = k0 + c < P ? v * rdg[k0 + c] : 0.0;
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double t01 = __builtin_fma(lr[s][1], dv[1], lr[s][0] * dv[0]);
+      const double t23 = __builtin_fma(lr[s][3], dv[3], lr[s][2] * dv[2]);
+      const double t45 = __builtin_fma(lr[s][5], dv[5], lr[s][4] * dv[4]);
+      const double t67 = __builtin_fma(lr[s][7], dv[7], lr[s][6] * dv[6]);
+      b[s] -= (t01 + t23) + (t45 + t67);
+      if (s == sK) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) b[s] = lane == l0 + c ? dv[c] : b[s];
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (lane + 64 * s < P) vec[lane + 64 * s] = b[s];
+}
+
+#define RPH_STAMPB(k)                                                                         \
+  do {                                                                                      \
+    if (stamps != nullptr && threadIdx.x == 0)                                              \
+      stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+  } while (0)
+
+// Tiles of the trailing-matrix register state of lm_chol_solve_blocked: the
+// lower triangle of the padded matrix in 16 x 16 tiles, ordered by column
+// block then row block, dealt round-robin to the 4 waves (the tiles still
+// active at panel K are a suffix of that order, so the waves stay balanced).
+template <int P>
+struct CholTiles {
+  static constexpr int PB = (P + 7) / 8 * 8;
+  static constexpr int NT = (PB + 15) / 16;
+  static constexpr int NTILE = NT * (NT + 1) / 2;
+  static constexpr int TPW = (NTILE + 3) / 4;
+  static constexpr int col(int t) {
+    int b = 0;
+    while (t >= NT - b) t -= NT - b++;
+    return b;
+  }
+  static constexpr int row(int t) {
+    int b = 0;
+    while (t >= NT - b) t -= NT - b++;
+    return b + t;
+  }
+};
+
+typedef double lm_d4 __attribute__((ext_vector_type(4)));
+
+// compile-time unrolled loop: f(std::integral_constant<int, j>) for j in [0, N)
+template <class F, int... J>
+RPH_INLINE void lm_static_for(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, class F>
+RPH_INLINE void lm_static_for(F&& f) {
+  lm_static_for(f, std::make_integer_sequence<int, N>{});
+}
+
+// Trailing-matrix tiles of wave W (tile ownership is a compile-time function
+// of W, so every tile and fragment index is a static register index):
+// load from A, rank-8 update on the fp64 matrix cores, publish of the next
+// panel's columns.  Entries left of / above the active trailing block get
+// updated with stale operands but are dead (L is already in A; phase 1 reads
+// only rows >= k0).
+template <int P, class SY, int W>
+struct CholWave {
+  using CT = CholTiles<P>;
+  static constexpr int TPW = CT::TPW;
+  RPH_INLINE static void load(lm_d4* C, const double* A, int lr, int lq) {
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = W + 4 * j;
+      if constexpr (t < CT::NTILE) {
+        constexpr int ib = CT::row(t), jb = CT::col(t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * ib + lq + 4 * r, jj = 16 * jb + lr;
+          C[j][r] = (i < P && jj <= i) ? A[SY::idx(i, jj)] : ((i == jj && i < CT::PB) ? 1.0 : 0.0);
+        }
+      }
+    });
+  }
+  // C -= U U^T over the active tiles (column block >= bk), U = uL (two
+  // v_mfma_f64_16x16x4_f64 per tile: K = 8), then the owners of column block
+  // bk write the next panel's columns [off, off + 8) to cn
+  RPH_INLINE static void update(lm_d4* C, const double (*fu)[2], int bk, int off, double (*cn)[128], int lr,
+                                int lq) {
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = W + 4 * j;
+      if constexpr (t < CT::NTILE) {
+        constexpr int ib = CT::row(t), jb = CT::col(t);
+        if (jb >= bk) {
+          C[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-fu[ib][0], fu[jb][0], C[j], 0, 0, 0);
+          C[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-fu[ib][1], fu[jb][1], C[j], 0, 0, 0);
+        }
+      }
+    });
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = W + 4 * j;
+      if constexpr (t < CT::NTILE) {
+        constexpr int ib = CT::row(t), jb = CT::col(t);
+        if (jb == bk && lr >= off && lr < off + 8) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cn[lr - off][16 * ib + lq + 4 * r] = C[j][r];
+        }
+      }
+    });
+  }
+};
+
+// Panel loop of the blocked Cholesky.  Per panel of 8 columns:
+//   phase 1: row threads t in [k0, PB) factor the 8 x 8 diagonal block
+//            (redundantly, from the LDS-broadcast panel) and solve their L21
+//            row -> uL (LDS) and A;
+//   phase 2: every wave's rank-8 trailing update on the matrix cores
+//            (CholWave), the next panel's columns published (colb,
+//            double-buffered).
+// Phase 1 is one copy of code for all waves; only the small tile code is
+// per-wave (one kernel body fits the instruction cache).
+template <int P, class SY>
+RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[8][128], double (*uL)[9],
+                               unsigned long long* stamps) {
+  using CT = CholTiles<P>;
+  constexpr int PB = CT::PB, NK = PB / 8, NT = CT::NT, TPW = CT::TPW;
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
+  lm_d4 C[TPW];
+  switch (wid) {
+    case 0: CholWave<P, SY, 0>::load(C, A, lr, lq); break;
+    case 1: CholWave<P, SY, 1>::load(C, A, lr, lq); break;
+    case 2: CholWave<P, SY, 2>::load(C, A, lr, lq); break;
+    default: CholWave<P, SY, 3>::load(C, A, lr, lq); break;
   }
   for (int K = 0; K < NK; ++K) {
     const int k0 = 8 * K;
@@ -328,109 +508,57 @@ RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsig
     __syncthreads();
     if (K == 6) RPH_STAMPB(9);
     if (*s_fail) return;
-    // ---- phase 2: rank-8 update of the trailing register tile + next panel ----
+    // ---- phase 2: rank-8 update of the trailing tiles on the matrix cores -------
     const int kn = k0 + 8;
     if (kn >= PB) break;
     const int bk = kn >> 4, off = kn & 15;
+    double fu[NT][2];  // lane (lr, lq): U[16 X + lr][4 s + lq]
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      if (16 * a + wid * 4 + 3 < kn) continue;  // the wave's rows of block a are final
-      double ua[8];
+    for (int X = 0; X < NT; ++X)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) ua[q] = uL[ty + 16 * a][q];
-#pragma unroll
-      for (int b = 0; b <= a; ++b) {
-        if (b < bk) continue;
-        double sv = 0.0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) sv = __builtin_fma(ua[q], uL[tx + 16 * b][q], sv);
-        const bool act = b > bk || tx >= off;
-        Rg[a][b] = act ? Rg[a][b] - sv : Rg[a][b];
-      }
-    }
-    if (tx >= off && tx < off + 8) {
-      double(*cn)[128] = colb[(K + 1) & 1];
-#define RPH_PUBK(BB)                                                               \
-  case BB:                                                                         \
-    _Pragma("unroll") for (int a = 0; a < 8; ++a) cn[tx - off][ty + 16 * a] = Rg[a][BB]; \
-    break;
-      switch (bk) { RPH_PUBK(0) RPH_PUBK(1) RPH_PUBK(2) RPH_PUBK(3) RPH_PUBK(4) RPH_PUBK(5) RPH_PUBK(6) RPH_PUBK(7) }
-#undef RPH_PUBK
+      for (int s2 = 0; s2 < 2; ++s2) fu[X][s2] = uL[16 * X + lr][4 * s2 + lq];
+    double(*cn)[128] = colb[(K + 1) & 1];
+    switch (wid) {
+      case 0: CholWave<P, SY, 0>::update(C, fu, bk, off, cn, lr, lq); break;
+      case 1: CholWave<P, SY, 1>::update(C, fu, bk, off, cn, lr, lq); break;
+      case 2: CholWave<P, SY, 2>::update(C, fu, bk, off, cn, lr, lq); break;
+      default: CholWave<P, SY, 3>::update(C, fu, bk, off, cn, lr, lq); break;
     }
     if (K == 6) RPH_STAMPB(10);
   }
-  __syncthreads();
-  RPH_STAMPB(6);
-  // inverses of the diagonal blocks, one block per thread (off the panel loop's
-  // critical path): Linv[r][c] = -Linv[r][r] sum_{q=c}^{r-1} L[r][q] Linv[q][c]
-  if (tid < NK) {
-    const int k0 = 8 * tid;
-    double Lv[8][8], Lb[8][8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int c = 0; c <= r; ++c) Lb[r][c] = k0 + r < P ? A[SY::idx(k0 + r, k0 + c)] : (r == c ? 1.0 : 0.0);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      Lv[c][c] = lm_rcp(Lb[c][c]);
-#pragma unroll
-      for (int r = c + 1; r < 8; ++r) {
-        double v = 0.0;
-#pragma unroll
-        for (int q = c; q < r; ++q) v = __builtin_fma(Lb[r][q], Lv[q][c], v);
-        Lv[r][c] = -lm_rcp(Lb[r][r]) * v;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int c = 0; c < 8; ++c) Li[tid][r][c] = c <= r ? Lv[r][c] : 0.0;
+}
+
+// Blocked (8-column panels) fp64 Cholesky + triangular solves of the LM
+// system for up to 128 parameters, one workgroup: the trailing matrix lives
+// in the waves' MFMA accumulator tiles (lm_chol_factor), P/8 panels with two
+// barriers each; then blocked triangular solves with the diagonal blocks'
+// inverses.  The matrix is padded to a multiple of 8 with identity rows.  L is
+// written over A (lower triangle, SY layout); the solution replaces vec.
+template <int P, class SY>
+RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsigned long long* stamps) {
+  constexpr int PB = (P + 7) / 8 * 8;
+  constexpr int NK = PB / 8;
+  static_assert(PB <= 128, "blocked solver: up to 128 parameters");
+  __shared__ double colb[2][8][128];
+  __shared__ double uL[128][9];
+  const int tid = threadIdx.x, wid = tid >> 6;
+  for (int t = tid; t < 128 * 9; t += 256) (&uL[0][0])[t] = 0.0;
+  for (int e = tid; e < 8 * 128; e += 256) {
+    const int c = e >> 7, i = e & 127;
+    colb[0][c][i] = (i < P && c <= i) ? A[SY::idx(i, c)] : ((i == c && i < PB) ? 1.0 : 0.0);
   }
+  lm_chol_factor<P, SY>(A, s_fail, colb, uL, stamps);
+  __syncthreads();
+  if (*s_fail) return;
+  RPH_STAMPB(6);
+  // reciprocal pivots, then both triangular solves in one wave (lm_tri_solve_wave)
+  double* rdg = vec + 2 * P;
+  for (int k = tid; k < P; k += 256) rdg[k] = lm_rcp(A[SY::idx(k, k)]);
   __syncthreads();
   RPH_STAMPB(7);
-  // ---- blocked triangular solves: L y = b, then L^T d = y (in vec) --------------
-  // per block: the 8 diagonal entries by a matvec with the stored block
-  // inverse (8 threads), then the row updates (all threads): two short phases
-  for (int K = 0; K < NK; ++K) {
-    const int k0 = 8 * K;
-    if (tid < 8) {
-      double v = 0.0;
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-        if (p <= tid && k0 + p < P) v = __builtin_fma(Li[K][tid][p], vec[k0 + p], v);
-      ytmp[tid] = v;
-    }
-    __syncthreads();
-    if (tid < 8 && k0 + tid < P) vec[k0 + tid] = ytmp[tid];
-    for (int i = k0 + 8 + tid; i < P; i += 256) {
-      double v = vec[i];
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (k0 + c < P) v -= A[SY::idx(i, k0 + c)] * ytmp[c];
-      vec[i] = v;
-    }
-    __syncthreads();
-  }
-  for (int K = NK - 1; K >= 0; --K) {
-    const int k0 = 8 * K;
-    if (tid < 8) {
-      double v = 0.0;
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-        if (p >= tid && k0 + p < P) v = __builtin_fma(Li[K][p][tid], vec[k0 + p], v);
-      ytmp[tid] = v;
-    }
-    __syncthreads();
-    if (tid < 8 && k0 + tid < P) vec[k0 + tid] = ytmp[tid];
-    for (int i = tid; i < k0; i += 256) {
-      double v = vec[i];
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (k0 + c < P) v -= A[SY::idx(k0 + c, i)] * ytmp[c];
-      vec[i] = v;
-    }
-    __syncthreads();
-  }
+  if (wid == 0) lm_tri_solve_wave<P, SY>(A, vec, rdg);
+  __syncthreads();
+  RPH_STAMPB(12);
 }
 
 template <int P, int R>
@@ -477,7 +605,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   } else {
     lam = fmin(lam * lm.lam_up, (double)lm.lam_max);
   }
-  if (tid == 0 && pass < MAXHIST) d.fit->hist[pass] = (float)Lt;
+  if (tid == 0 && pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
   __syncthreads();
   RPH_STAMP(1);
   const double* g = best_red + LM_GBLK_MAX;
@@ -498,7 +626,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       d.wts->w[0][i] = w;
       d.fit->w_best[i] = w;
     }
-    if (tid == 0) {
+    if (tid == 0 && lm.weights_only) {
+      st[LMS_BEST] = (double)best;
+      st[LMS_LAM] = lam;
+    } else if (tid == 0) {
       const double* sb = best_red + LM_GBLK_MAX + LM_NPMAX;
       const double c = fmax(sb[3], 1.0);
       FitState* f = d.fit;
@@ -614,49 +745,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     // solved entry of step m is broadcast with v_readlane (no LDS round trip on
     // the dependency chain), the column / row of L comes from LDS
     RPH_STAMP(4);
-    static_assert(P <= 192, "three rows per lane");
-    if (wid == 0) {
-      double b0 = lane < P ? vec[lane] : 0.0;
-      double b1 = lane + 64 < P ? vec[lane + 64] : 0.0;
-      double b2 = lane + 128 < P ? vec[lane + 128] : 0.0;
-      auto bcast = [](double v, int l) -> double {
-        const unsigned long long u = __double_as_longlong(v);
-        const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
-        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-        return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-      };
-      // forward: L y = b
-      for (int m = 0; m < P; ++m) {
-        const int src = m & 63;
-        const double bm = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
-        const double ym = bm * rdg[m];
-        if (lane == src) {
-          if (m < 64) b0 = ym;
-          else if (m < 128) b1 = ym;
-          else b2 = ym;
-        }
-        if (lane > m && lane < P) b0 -= A[SY::idx(lane, m)] * ym;
-        if (lane + 64 > m && lane + 64 < P) b1 -= A[SY::idx(lane + 64, m)] * ym;
-        if (lane + 128 > m && lane + 128 < P) b2 -= A[SY::idx(lane + 128, m)] * ym;
-      }
-      // backward: L^T d = y
-      for (int m = P - 1; m >= 0; --m) {
-        const int src = m & 63;
-        const double ym = bcast(m < 64 ? b0 : (m < 128 ? b1 : b2), src);
-        const double dm = ym * rdg[m];
-        if (lane == src) {
-          if (m < 64) b0 = dm;
-          else if (m < 128) b1 = dm;
-          else b2 = dm;
-        }
-        if (lane < m) b0 -= A[SY::idx(m, lane)] * dm;
-        if (lane + 64 < m) b1 -= A[SY::idx(m, lane + 64)] * dm;
-        if (lane + 128 < m) b2 -= A[SY::idx(m, lane + 128)] * dm;
-      }
-      if (lane < P) vec[lane] = b0;
-      if (lane + 64 < P) vec[lane + 64] = b1;
-      if (lane + 128 < P) vec[lane + 128] = b2;
-    }
+    if (wid == 0) lm_tri_solve_wave<P, SY>(A, vec, rdg);
     __syncthreads();
   }
   RPH_STAMP(5);

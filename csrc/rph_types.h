@@ -215,7 +215,8 @@ struct LmDesc {
   // bias) takes an exact 1-D Newton step: the value fit's residual mean over
   // all paths becomes zero, so no drift accumulates over the dates; -1: off
   int bias_index;
-  int pad1;
+  int weights_only;              // 1: publish the weights only (no FitState / loss history: a bias refit
+                                 // after an Adam fit, passes = 0)
 };
 
 // Eval stats slab columns

@@ -44,6 +44,11 @@ def run(n_log2=20, nin=1, passes=40):
     if s1[0] and s1[1] and s1[2]:
         ph["panel6_phase1_us"] = (s1[1] - s1[0]) / 100.0
         ph["panel6_phase2_us"] = (s1[2] - s1[1]) / 100.0
+    if s1[4] and st[7]:
+        ph["tri_solves_us"] = (s1[4] - st[7]) / 100.0
+    if s1[3] and s1[4]:
+        ph["forward_solve_us"] = (s1[3] - st[7]) / 100.0
+        ph["backward_solve_us"] = (s1[4] - s1[3]) / 100.0
     return {"n_log2": n_log2, "nin": nin, "passes": passes, "us_per_pass": 1000.0 * e0.elapsed_time(e1) / (passes + 1),
             **ph, "lm": be.lm_state()}
 
