@@ -60,7 +60,8 @@ RPH_INLINE constexpr int lm_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 
 // Pass kernel.  B = NarrowBody<...> (full batch: batch = n_local, no shuffle).
 // ---------------------------------------------------------------------------
 template <class B>
-__global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainDesc d, const LmDesc lm, const int pass) {
+__global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainDesc d, const LmDesc lm, const int pass,
+                                                                   const double* __restrict__ red_new) {
   constexpr int P = B::P;
   constexpr int R = B::R;
   constexpr int NR = B::NR;
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   using LS = LmShape<P>;
   constexpr int NP = LS::NP, NB = LS::NB, NBLK = LS::NBLK, JP = LS::JP;
   constexpr int NIN = B::NIN_, H = B::H_, NO = B::NO_, HEAD = B::HEAD_, NHOLD = B::NHOLD;
-  const uint32_t kat = prefetch_kernarg_begin<sizeof(TrainDesc) + sizeof(LmDesc) + sizeof(int)>();
+  const uint32_t kat = prefetch_kernarg_begin<sizeof(TrainDesc) + sizeof(LmDesc) + 16>();
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
@@ -85,6 +86,17 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     const float w = pass == 0 ? d.wts->w[0][i] : (float)st[LMS_W + trial * LM_NPMAX + i];
     wl[i] = w;
     if (pass == 0 && blockIdx.x == 0) st[LMS_W + i] = (double)w;
+  }
+  if (pass > 0 && st[LMS_COPY] != 0.0) {
+    // the previous solve accepted its trial: best block := that trial's
+    // reduced block (G, g, stats), spread over the grid; red_new is rewritten
+    // only by this pass's reduce kernel, which runs after this one
+    constexpr int NG = LmShape<P>::NBLK * 1024;
+    double* best_red = st + LMS_RED;
+    for (int e = blockIdx.x * 256 + tid; e < NG + P + 4; e += (int)gridDim.x * 256) {
+      const int o = e < NG ? e : (e < NG + P ? LM_GBLK_MAX + e - NG : LM_GBLK_MAX + LM_NPMAX + e - NG - P);
+      best_red[o] = red_new[o];
+    }
   }
   if (pass == 0 && blockIdx.x == 0 && tid == 0) {
     st[LMS_BEST] = 1.0;
@@ -231,16 +243,15 @@ struct LmSys {
 };
 
 // fp64 reciprocal / reciprocal square root from the hardware approximations
-// (v_rcp_f64 / v_rsq_f64) + two Newton steps (~1 ulp): the IEEE division and
-// sqrt sequences cost ~100 ns each on the dependency chains of the solver
+// (v_rcp_f64 / v_rsq_f64, max rel. error 4.6e-8 / 5.2e-8 on gfx950) + ONE
+// Newton step: 2.2e-15 / 4.0e-15 (tools/micro/rsq_prec.hip); the IEEE division
+// and sqrt sequences cost ~100 ns each on the dependency chains of the solver
 RPH_INLINE double lm_rcp(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+  const double r = __builtin_amdgcn_rcp(x);
   return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
 }
 RPH_INLINE double lm_rsq(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  y = y * __builtin_fma(-0.5 * x * y, y, 1.5);
+  const double y = __builtin_amdgcn_rsq(x);
   return y * __builtin_fma(-0.5 * x * y, y, 1.5);
 }
 
@@ -591,13 +602,8 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   if (accept) {
     best = trial;
     if (pass > 0) lam = fmax(lam * lm.lam_down, (double)lm.lam_min);
-    // the best point's block := the trial's (G, g, stats)
-    for (int e = tid; e < NG; e += 256) best_red[e] = red_new[e];
-    for (int i = tid; i < P + 4; i += 256) {
-      const double v = pkt(i);
-      if (i < P) best_red[LM_GBLK_MAX + i] = v;
-      else best_red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
-    }
+    // the best point's block := the trial's: read from red_new below, copied
+    // by the next pass kernel (LMS_COPY); the best loss is recorded now
     if (tid == 0) {
       best_red[LM_GBLK_MAX + LM_NPMAX + 4] = Lt;
       st[LMS_NACC] += pass > 0 ? 1.0 : 0.0;
@@ -606,9 +612,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     lam = fmin(lam * lm.lam_up, (double)lm.lam_max);
   }
   if (tid == 0 && pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
-  __syncthreads();
+  if (tid == 0) st[LMS_COPY] = accept ? 1.0 : 0.0;
   RPH_STAMP(1);
-  const double* g = best_red + LM_GBLK_MAX;
+  const double* src = accept ? red_new : best_red;  // the best point's block
+  const double* g = src + LM_GBLK_MAX;
   if (pass == lm.passes) {  // final pass: publish the best point
     for (int i = tid; i < P; i += 256) {
       double wd = st[LMS_W + best * LM_NPMAX + i];
@@ -619,7 +626,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
         int b = 0;
         for (int m = 0; m < kb; ++m) b += LS::NB - m;
         const int q = (ri >> 3) * 4 + (ri & 3), hh = (ri >> 2) & 1;
-        const double gii = best_red[(size_t)b * 1024 + q * 64 + hh * 32 + ri];
+        const double gii = src[(size_t)b * 1024 + q * 64 + hh * 32 + ri];
         if (gii > 0.0) wd -= g[i] / (2.0 * gii);
       }
       const float w = (float)wd;
@@ -630,11 +637,12 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       st[LMS_BEST] = (double)best;
       st[LMS_LAM] = lam;
     } else if (tid == 0) {
-      const double* sb = best_red + LM_GBLK_MAX + LM_NPMAX;
+      const double* sb = src + LM_GBLK_MAX + LM_NPMAX;
       const double c = fmax(sb[3], 1.0);
       FitState* f = d.fit;
-      f->best_loss = (float)sb[4];
-      f->last_loss = (float)sb[4];
+      const double lbest = best_red[LM_GBLK_MAX + LM_NPMAX + 4];  // written above by this thread
+      f->best_loss = (float)lbest;
+      f->last_loss = (float)lbest;
       f->last_mae = (float)(sb[1] / c);
       f->last_mape = (float)(100.0 * sb[2] / c);
       f->epoch = (float)(pass + 1);
@@ -652,7 +660,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   for (int b = wid; b < NBLK; b += 4) {
     int mb, nb;
     lm_blk(b, NB, mb, nb);
-    const double* blk = best_red + (size_t)b * 1024;
+    const double* blk = src + (size_t)b * 1024;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int i = mb * 32 + lm_row(q, h), j = nb * 32 + r;  // i <= j when mb < nb
@@ -788,9 +796,9 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
 }
 
 template <int A, int B, int C, int E>
-static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, hipStream_t s) {
+static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const double* red_new, hipStream_t s) {
   using K = LmKernels<A, B, C, E>;
-  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs), dim3(256), 0, s, *d, *lm, pass);
+  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs), dim3(256), 0, s, *d, *lm, pass, red_new);
   return (int)hipGetLastError();
 }
 
@@ -832,7 +840,7 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                  \
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK)) return rc;      \
-    if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, s)) return rc;                         \
+    if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
     hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs), dim3(256), 0, s, *lm, red_new); \
     return (int)hipGetLastError();                                                              \
   }

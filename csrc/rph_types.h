@@ -191,6 +191,8 @@ enum LmState : int {
   LMS_LAM,                           // damping
   LMS_NACC,                          // accepted steps
   LMS_FAIL,                          // Cholesky failures (non-positive pivot)
+  LMS_COPY,                          // 1: the last solve accepted; the next pass kernel copies the trial's
+                                     // reduced block into the best slot (deferred off the solve's path)
   LMS_FLOATS = LMS_FAIL + 8
 };
 

@@ -70,4 +70,5 @@ LMS_BEST = LMS_RED + 2 * LM_RED
 LMS_LAM = LMS_BEST + 1
 LMS_NACC = LMS_BEST + 2
 LMS_FAIL = LMS_BEST + 3
+LMS_COPY = LMS_BEST + 4
 LMS_FLOATS = LMS_FAIL + 8
