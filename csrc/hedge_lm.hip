@@ -420,7 +420,7 @@ struct CholWave {
   // C -= U U^T over the active tiles (column block >= bk), U = uL (two
   // v_mfma_f64_16x16x4_f64 per tile: K = 8), then the owners of column block
   // bk write the next panel's columns [off, off + 8) to cn
-  RPH_INLINE static void update(lm_d4* C, const double (*fu)[2], int bk, int off, double (*cn)[128], int lr,
+  RPH_INLINE static void update(lm_d4* C, const double (*fu)[2], int bk, int off, double (*cn)[16 * CT::NT], int lr,
                                 int lq) {
     lm_static_for<TPW>([&](auto jc) {
       constexpr int j = decltype(jc)::value, t = W + 4 * j;
@@ -455,7 +455,7 @@ struct CholWave {
 // Phase 1 is one copy of code for all waves; only the small tile code is
 // per-wave (one kernel body fits the instruction cache).
 template <int P, class SY>
-RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[8][128], double (*uL)[9],
+RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[16 * CholTiles<P>::NT], double (*uL)[9],
                                unsigned long long* stamps) {
   using CT = CholTiles<P>;
   constexpr int PB = CT::PB, NK = PB / 8, NT = CT::NT, TPW = CT::TPW;
@@ -471,7 +471,7 @@ RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[8][128], d
     const int k0 = 8 * K;
     __syncthreads();
     if (K == 6) RPH_STAMPB(8);
-    const double(*cb)[128] = colb[K & 1];
+    const double(*cb)[16 * NT] = colb;  // single buffer: phase 2 overwrites it after the barrier
     // ---- phase 1: row threads t in [k0, PB): diagonal block + L21 row ----------
     if (tid >= k0 && tid < PB) {
       double L[8][8], rl[8];
@@ -528,7 +528,7 @@ RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[8][128], d
     for (int X = 0; X < NT; ++X)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) fu[X][s2] = uL[16 * X + lr][4 * s2 + lq];
-    double(*cn)[128] = colb[(K + 1) & 1];
+    double(*cn)[16 * NT] = colb;
     switch (wid) {
       case 0: CholWave<P, SY, 0>::update(C, fu, bk, off, cn, lr, lq); break;
       case 1: CholWave<P, SY, 1>::update(C, fu, bk, off, cn, lr, lq); break;
@@ -549,14 +549,15 @@ template <int P, class SY>
 RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsigned long long* stamps) {
   constexpr int PB = (P + 7) / 8 * 8;
   constexpr int NK = PB / 8;
-  static_assert(PB <= 128, "blocked solver: up to 128 parameters");
-  __shared__ double colb[2][8][128];
-  __shared__ double uL[128][9];
+  constexpr int RW = 16 * CholTiles<P>::NT;  // rows of the tile grid
+  static_assert(PB <= 192, "blocked solver: up to 192 parameters");
+  __shared__ double colb[8][RW];
+  __shared__ double uL[RW][9];
   const int tid = threadIdx.x, wid = tid >> 6;
-  for (int t = tid; t < 128 * 9; t += 256) (&uL[0][0])[t] = 0.0;
-  for (int e = tid; e < 8 * 128; e += 256) {
-    const int c = e >> 7, i = e & 127;
-    colb[0][c][i] = (i < P && c <= i) ? A[SY::idx(i, c)] : ((i == c && i < PB) ? 1.0 : 0.0);
+  for (int t = tid; t < RW * 9; t += 256) (&uL[0][0])[t] = 0.0;
+  for (int e = tid; e < 8 * RW; e += 256) {
+    const int c = e / RW, i = e % RW;
+    colb[c][i] = (i < P && c <= i) ? A[SY::idx(i, c)] : ((i == c && i < PB) ? 1.0 : 0.0);
   }
   lm_chol_factor<P, SY>(A, s_fail, colb, uL, stamps);
   __syncthreads();
@@ -689,73 +690,22 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   RPH_STAMP(2);
   __syncthreads();  // the damped diagonal is in place
-  if constexpr (SY::DENSE) {
-    lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, d.stamps);
-    __syncthreads();
-    if (s_fail) {
-      // not positive definite at this damping: re-evaluate the best point with
-      // more damping (trial := best)
-      for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
-      if (tid == 0) {
-        st[LMS_BEST] = (double)best;
-        st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
-        st[LMS_FAIL] += 1.0;
-      }
-      return;
+  // blocked Cholesky (trailing update on the fp64 matrix cores) + one-wave
+  // triangular solves; dense LDS storage up to 128 parameters, packed above
+  lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, d.stamps);
+  __syncthreads();
+  if (s_fail) {
+    // not positive definite at this damping: re-evaluate the best point with
+    // more damping (trial := best)
+    for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
+    if (tid == 0) {
+      st[LMS_BEST] = (double)best;
+      st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
+      st[LMS_FAIL] += 1.0;
     }
-    RPH_STAMP(4);
-  } else {
-    // packed LDS storage (more than 128 parameters): column-by-column
-    // right-looking Cholesky, one barrier per column
-    const int ty = tid >> 4, tx = tid & 15;
-    for (int k = 0; k < P; ++k) {
-      __syncthreads();
-      const double akk = A[SY::idx(k, k)];
-      if (!(akk > 0.0)) {
-        if (tid == 0) s_fail = 1;
-        break;
-      }
-      const double rk = 1.0 / akk;
-      for (int i = k + 1 + ty; i < P; i += 16) {
-        const double aik = A[SY::idx(i, k)] * rk;
-        for (int j = k + 1 + tx; j <= i; j += 16) A[SY::idx(i, j)] -= aik * A[SY::idx(j, k)];
-      }
-    }
-    __syncthreads();
-    if (s_fail) {
-      // not positive definite at this damping: re-evaluate the best point with
-      // more damping (trial := best)
-      for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
-      if (tid == 0) {
-        st[LMS_BEST] = (double)best;
-        st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
-        st[LMS_FAIL] += 1.0;
-      }
-      return;
-    }
-    // L[i][k] = A[i][k] / sqrt(A[k][k]) (column values were final at step k);
-    // the pivots are read into their own array first (the diagonal is rewritten)
-    RPH_STAMP(3);
-    double* dgs = vec + P;
-    for (int k = tid; k < P; k += 256) dgs[k] = sqrt(A[SY::idx(k, k)]);
-    __syncthreads();
-    double* rdg = vec + 2 * P;  // reciprocal pivots for the solves
-    for (int k = tid; k < P; k += 256) rdg[k] = 1.0 / dgs[k];
-    __syncthreads();
-    for (int i = ty; i < P; i += 16)
-    for (int k = tx; k <= i; k += 16) {
-      double& a = A[SY::idx(i, k)];
-      a = (i == k) ? dgs[i] : a / dgs[k];
-    }
-    __syncthreads();
-    // ---- triangular solves in one wave, column-oriented: each lane keeps the
-    // right-hand side of rows lane, lane + 64, lane + 128 in registers; the
-    // solved entry of step m is broadcast with v_readlane (no LDS round trip on
-    // the dependency chain), the column / row of L comes from LDS
-    RPH_STAMP(4);
-    if (wid == 0) lm_tri_solve_wave<P, SY>(A, vec, rdg);
-    __syncthreads();
+    return;
   }
+  RPH_STAMP(4);
   RPH_STAMP(5);
   for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i] + vec[i];
   if (tid == 0) {

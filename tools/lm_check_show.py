@@ -12,5 +12,5 @@ print("ms/run", round(r["ms_per_step"], 3), "pnl", q["terminal_pnl_std"], "resid
 for row in list(csv.DictReader(open("gpurun_out/prof/run_kernel_stats.csv")))[:4]:
     print(" ", re.sub(r"\(.*", "", row["Name"])[:50], row["Calls"], row["AverageNs"], row["Percentage"])
 st = [ln for ln in open("gpurun_out/stamp.log").read().splitlines() if ln.startswith("{")]
-if st:
-    print(st[0][:900])
+for ln in st:
+    print(ln[:900])
