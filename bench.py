@@ -80,6 +80,7 @@ PRESETS = {
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
                     extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
+                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2,
                     label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
     "euro30_mfma": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-3, lr_rest=1e-3, lr_decay=0.1, hidden=32,
