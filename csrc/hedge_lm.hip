@@ -752,9 +752,89 @@ static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const 
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Data-parallel all-reduce of the LM reduced block [G | g | stats] over the
+// IPC-mapped peer mailboxes (the xGMI transport; RCCL otherwise).  Workgroup
+// wg owns one chunk of the block: it pushes its chunk into every peer's
+// mailbox with system-scope stores, drains, raises one flag per peer, waits
+// for every peer's flag of the same chunk, and sums the W chunks in fixed
+// rank order — every rank gets the bitwise-identical block (so the solves and
+// the accept / reject decisions agree).  The tag is a per-rank device
+// exchange counter (graph replays never see stale flags); the last workgroup
+// to finish advances it.  Spins are bounded (DP_SPIN_TICKS -> error[0]).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_lm_dp_exchange(const LmDpDesc x, double* __restrict__ red, const int ng,
+                                                         const int p) {
+  __shared__ unsigned s_seq;
+  const int tid = threadIdx.x, wg = blockIdx.x, W = x.world, me = x.rank;
+  if (tid == 0) s_seq = __hip_atomic_load(x.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const unsigned seq = s_seq;
+  const int slot = (int)(seq % DP_SLOTS);
+  const int len = ng + p + 4, chunk = (len + LM_DP_WGS - 1) / LM_DP_WGS;
+  const int e0 = wg * chunk, e1 = min(len, e0 + chunk);
+  auto off = [&](int e) {  // block entry -> offset in red
+    return e < ng ? e : (e < ng + p ? LM_GBLK_MAX + e - ng : LM_GBLK_MAX + LM_NPMAX + e - ng - p);
+  };
+  for (int e = e0 + tid; e < e1; e += 256) {
+    const double v = red[off(e)];
+    for (int q = 0; q < W; ++q)
+      if (q != me)
+        __hip_atomic_store(x.mbox[q] + ((size_t)slot * W + me) * x.pitch + e, v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (tid < W && tid != me) {
+    unsigned* fo = reinterpret_cast<unsigned*>(x.mbox[tid] + ((size_t)slot * W + me) * x.pitch + LM_RED + wg);
+    __hip_atomic_store(fo, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* fi =
+        reinterpret_cast<const unsigned*>(x.mbox[me] + ((size_t)slot * W + tid) * x.pitch + LM_RED + wg);
+    unsigned it = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(fi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++it & 255u) == 0u && (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS ||
+                                  __hip_atomic_load(x.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+        __hip_atomic_store(x.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = e0 + tid; e < e1; e += 256) {
+    const int o = off(e);
+    double s = 0.0;
+    for (int q = 0; q < W; ++q)
+      s += q == me ? red[o]
+                   : __hip_atomic_load(x.mbox[me] + ((size_t)slot * W + q) * x.pitch + e, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+    red[o] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(x.counter + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == LM_DP_WGS - 1) {
+      __hip_atomic_store(x.counter + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(x.counter, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace rph
 
 using namespace rph;
+
+extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p, void* stream) {
+  if (!x || !red || x->world < 2 || x->world > 8 || x->rank < 0 || x->rank >= x->world)
+    return rph_report("rph_lm_dp_exchange", "bad world / rank");
+  if (x->pitch < LM_RED + LM_DP_WGS || ng < 0 || ng > LM_GBLK_MAX || p < 1 || p > LM_NPMAX)
+    return rph_report("rph_lm_dp_exchange", "bad mailbox pitch / block geometry");
+  for (int q = 0; q < x->world; ++q)
+    if (!x->mbox[q]) return rph_report("rph_lm_dp_exchange", "null peer mailbox");
+  hipLaunchKernelGGL(k_lm_dp_exchange, dim3(LM_DP_WGS), dim3(256), 0, (hipStream_t)stream, *x, red, ng, p);
+  return (int)hipGetLastError();
+}
 
 #define RPH_LM_SHAPES(X)         \
   X(1, 8, 1, HEAD_COMPLEMENT)    \

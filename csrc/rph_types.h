@@ -221,6 +221,20 @@ struct LmDesc {
                                  // after an Adam fit, passes = 0)
 };
 
+// Data-parallel exchange of the LM reduced block over IPC-mapped peer
+// mailboxes (k_lm_dp_exchange): LM_DP_WGS workgroups, each owning a chunk of
+// the block; per (slot, sender) row `pitch` 8-byte entries = LM_RED data +
+// LM_DP_WGS per-workgroup flags.
+constexpr int LM_DP_WGS = 16;
+struct LmDpDesc {
+  double* mbox[8];               // every rank's mailbox [DP_SLOTS][world][pitch] (own = mbox[rank])
+  unsigned* counter;             // [0] exchanges completed by this rank, [1] workgroup arrival ticket
+  unsigned* error;               // [0] set on a peer timeout
+  int world, rank;
+  int pitch;                     // entries per (slot, sender) row (>= LM_RED + LM_DP_WGS)
+  int pad0;
+};
+
 // Eval stats slab columns
 enum EvalStat : int {
   ES_V = 0, ES_V2 = 1, ES_RES = 2, ES_RES2 = 3, ES_ABSRES = 4, ES_APE = 5, ES_PRED1 = 6,

@@ -241,6 +241,10 @@ class HedgeRun:
                 D.select_transport(self.di)  # once per process group (collective); may fall back to RCCL
             self.mailbox = D.make_mailbox(self.di, self.spec.red_width)
             kw["mailbox"] = self.mailbox
+            # LM fits / mean refits: the reduced [G | g | stats] block travels
+            # over its own mailbox (k_lm_dp_exchange) with the xGMI transport
+            self.lm_mailbox = D.make_mailbox(self.di, L.LM_RED + L.LM_DP_WGS, tag="rph_lmbox")
+            kw["lm_mailbox"] = self.lm_mailbox
         self.backend = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
                                     comm=self.di.comm, world=self.di.world, rank=self.di.rank, stream=self.stream,
                                     **kw)
@@ -333,10 +337,11 @@ class HedgeRun:
     def close(self):
         """Release the run's cross-rank resources (collective when data
         parallel: every rank's kernels finish before any mailbox is freed)."""
-        mb = getattr(self, "mailbox", None)
-        self.mailbox = None
-        if mb is not None:
-            D.close_mailbox(mb)
+        for name in ("mailbox", "lm_mailbox"):
+            mb = getattr(self, name, None)
+            setattr(self, name, None)
+            if mb is not None:
+                D.close_mailbox(mb)
 
     def resume(self, out_dir: str, date: int) -> RunResult:
         """Restart the backward scan at ``date-1`` from a saved run directory
@@ -401,8 +406,9 @@ class HedgeRun:
         c, w = self.cfg, self.di.world
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
-        if getattr(self, "mailbox", None) is not None:
-            self.mailbox.check()
+        for mb in (getattr(self, "mailbox", None), getattr(self, "lm_mailbox", None)):
+            if mb is not None:
+                mb.check()
         if hasattr(self.backend, "check"):
             self.backend.check()
         ind = self.induction.collect()

@@ -297,10 +297,11 @@ class HipBackend:
     name = "hip"
 
     def __init__(self, spec: NetSpec, n_local: int, tcfg: TrainConfig, device=None, comm=None,
-                 world: int = 1, rank: int = 0, stream=None, mailbox=None):
+                 world: int = 1, rank: int = 0, stream=None, mailbox=None, lm_mailbox=None):
         from .ops import native
 
         self.mailbox = mailbox  # native.IpcMailbox: fused xGMI all-reduce inside the step kernel
+        self.lm_mailbox = lm_mailbox  # native.IpcMailbox (LM_RED + LM_DP_WGS pitch): LM block exchange
         self.native = native
         native.load(required=True)
         self.spec, self.n_local, self.tcfg = spec, int(n_local), tcfg
@@ -525,11 +526,20 @@ class HipBackend:
         if self.world <= 1:
             n.lm_fit(d, lm, b["red"], self.stream)
             return
-        comm = self._lm_comm()
         for k in range(lm.passes + 1):
             n.lm_eval(d, lm, b["red"], k, self.stream)
-            comm.allreduce_(b["red"], self.stream)
+            self._lm_allreduce(b["red"])
             n.lm_solve(d, lm, b["red"], k, self.stream)
+
+    def _lm_allreduce(self, red: torch.Tensor):
+        """Sum the reduced LM block over the ranks: in-kernel exchange over the
+        IPC mailboxes (xGMI transport) or one RCCL all-reduce."""
+        if self.lm_mailbox is not None:
+            P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+            x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
+            self.native.lm_dp_exchange(x, red, nblk * 1024, P, self.stream)
+            return
+        self._lm_comm().allreduce_(red, self.stream)
 
     def bias_refit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
         """Exact refit of the bond holding's output bias after an Adam fit (one
@@ -548,7 +558,12 @@ class HipBackend:
             self.eval(wts, data, st)
             tot = st[:, [L.ES_RES, L.ES_COUNT]].sum(0)
             if self.world > 1:
-                self._lm_comm().allreduce_(tot, self.stream)
+                if self.lm_mailbox is not None:
+                    import torch.distributed as dist
+
+                    dist.all_reduce(tot)
+                else:
+                    self._lm_comm().allreduce_(tot, self.stream)
             delta = (tot[0] / tot[1].clamp_min(1.0) / float(data.bond_next)).to(torch.float32)
             wts[bi] += delta
             fit[L.F_WBEST + bi] = wts[bi]
@@ -572,7 +587,7 @@ class HipBackend:
             n.lm_fit(d, lm, b["red"], self.stream)
             return
         n.lm_eval(d, lm, b["red"], 0, self.stream)
-        self._lm_comm().allreduce_(b["red"], self.stream)
+        self._lm_allreduce(b["red"])
         n.lm_solve(d, lm, b["red"], 0, self.stream)
 
     def _lm_comm(self):
@@ -1070,6 +1085,7 @@ def make_backend(kind: str, spec: NetSpec, n_local: int, tcfg: TrainConfig, **kw
         return HipBackend(spec, n_local, tcfg, **kw)
     kw.pop("stream", None)
     kw.pop("mailbox", None)
+    kw.pop("lm_mailbox", None)
     return TorchBackend(spec, n_local, tcfg, **kw)
 
 

@@ -90,6 +90,13 @@ class LmDesc(C.Structure):
     ]
 
 
+class LmDpDesc(C.Structure):
+    _fields_ = [
+        ("mbox", VP * 8), ("counter", VP), ("error", VP),
+        ("world", C.c_int), ("rank", C.c_int), ("pitch", C.c_int), ("pad0", C.c_int),
+    ]
+
+
 class SimDesc(C.Structure):
     _fields_ = [
         ("model", C.c_int), ("n_local", C.c_int), ("path_offset", C.c_longlong),
@@ -129,6 +136,7 @@ def _expected_layout() -> list[int]:
         C.sizeof(LmDesc), LmDesc.slab_b.offset, LmDesc.slab_g.offset, LmDesc.num_wgs.offset,
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset,
+        C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
@@ -169,6 +177,7 @@ def _bind(lib):
         "rph_lm_eval": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_solve": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_fit": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, VP]),
+        "rph_lm_dp_exchange": (C.c_int, [C.POINTER(LmDpDesc), VP, C.c_int, C.c_int, VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
         "rph_payoff": (C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP, C.c_float, VP, VP, VP]),
@@ -333,6 +342,13 @@ def lm_fit(desc: TrainDesc, lm: LmDesc, red_new: torch.Tensor, stream=None):
     _check(_lib.rph_lm_fit(C.byref(desc), C.byref(lm), ptr(red_new), stream_handle(stream)), "rph_lm_fit")
 
 
+def lm_dp_exchange(x: LmDpDesc, red: torch.Tensor, ng: int, p: int, stream=None):
+    """All-reduce of the LM reduced block over the IPC mailboxes (k_lm_dp_exchange)."""
+    load(required=True)
+    _check(_lib.rph_lm_dp_exchange(C.byref(x), ptr(red), int(ng), int(p), stream_handle(stream)),
+           "rph_lm_dp_exchange")
+
+
 def pnl(desc: PnlDesc, stream=None):
     """Self-financing hedge P&L scan over the rebalancing dates (k_hedge_pnl)."""
     load(required=True)
@@ -481,6 +497,16 @@ class IpcMailbox:
             d.dp_flags[q] = self.ptrs[q] + self.flag_off
         d.dp_counter = self.counter.data_ptr()
         d.dp_error = self.error.data_ptr()
+
+    def lm_desc(self) -> "LmDpDesc":
+        """Descriptor of this mailbox for the LM block exchange (k_lm_dp_exchange;
+        allocated with R >= LM_RED + LM_DP_WGS entries per row)."""
+        x = LmDpDesc()
+        for q in range(self.world):
+            x.mbox[q] = self.ptrs[q]
+        x.counter, x.error = self.counter.data_ptr(), self.error.data_ptr()
+        x.world, x.rank, x.pitch = self.world, self.rank, self.R
+        return x
 
     def check(self):
         if int(self.error[0].item()) != 0:

@@ -135,3 +135,70 @@ def test_missing_peer_times_out_cleanly():
             assert p.exitcode == 0
         status = open(out + ".0.txt").read()
     assert status.startswith("error:") and "did not arrive" in status, status
+
+
+def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    per = n // world
+    f, p1, y = _data(n, dev, rank * per, per)
+    y = y + 0.02 * torch.sin(9 * f)
+    be = HipBackend(spec, per, TrainConfig(batch_size=per, lm_gram_paths=2048), device=dev, world=world,
+                    rank=rank, mailbox=mailbox, lm_mailbox=lm_mailbox)
+    data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f])
+    w, o, fs = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+    be.fit(w, o, fs, data, FitConfig(epochs=passes, optimizer="lm", early_stopping=False), seed=3)
+    torch.cuda.synchronize()
+    return current_weights(spec, w), be.lm_state()
+
+
+def _worker_lm(rank, world, port, n, passes, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from torch.distributed import distributed_c10d as c10d
+
+    from rphedge.ops import layout as L
+    from rphedge.ops.native import IpcMailbox
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = c10d._get_default_store()
+    mb = IpcMailbox(rank, world, 128, store, dev, tag="t_lm_a")
+    lmb = IpcMailbox(rank, world, L.LM_RED + L.LM_DP_WGS, store, dev, tag="t_lm_b")
+    dist.barrier()
+    w, st = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb)
+    lmb.check()
+    np.save(out + f".{rank}.npy", w)
+    with open(out + f".{rank}.txt", "w") as fh:
+        fh.write(f"{st['accepted']} {st['chol_failures']}")
+    dist.barrier()
+    mb.close()
+    lmb.close()
+    dist.destroy_process_group()
+
+
+def test_lm_mailbox_exchange_two_ranks_one_gpu():
+    """Levenberg-Marquardt fit over 2 ranks with the reduced [G | g | stats]
+    block exchanged by k_lm_dp_exchange (IPC mailboxes, the xGMI transport):
+    bitwise-identical replicas, and the 1-rank fit of the same global paths
+    (world-invariant Gram subsample; only the fp64 summation order differs)."""
+    n, passes, world = 1 << 15, 12, 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "w")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_lm, args=(r, world, port, n, passes, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+        s0, s1 = open(out + ".0.txt").read(), open(out + ".1.txt").read()
+    assert np.array_equal(w0, w1) and s0 == s1
+    ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0))
+    assert s0 == f"{st['accepted']} {st['chol_failures']}"
+    np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
