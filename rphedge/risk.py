@@ -43,33 +43,49 @@ def _hist_pass(x: torch.Tensor, pmask: int, prefix: int, shift: int, nbins: int,
     return h.cpu().numpy().astype(np.int64)
 
 
+def kth_smallest_many(x: torch.Tensor, ks, world: int = 1) -> list[float]:
+    """Exact k-th smallest (0-based) float32 values over all ranks for several
+    k at once: per radix pass one histogram per DISTINCT key prefix (the first
+    pass is shared by every k; neighbouring order statistics usually share
+    all three), so a 3-level VaR report costs a handful of histogram passes
+    instead of 3 per order statistic.  Every rank derives the same prefixes
+    from the all-reduced histograms, so the collective sequence matches."""
+    st = [[0, 0, int(k)] for k in ks]  # pmask, prefix, remaining rank
+    for shift, nbins in _PASSES:
+        cache = {}
+        for e in st:
+            key = (e[0], e[1])
+            if key not in cache:
+                cache[key] = np.cumsum(_hist_pass(x, e[0], e[1], shift, nbins, world))
+            c = cache[key]
+            b = int(np.searchsorted(c, e[2] + 1))
+            e[2] -= int(c[b - 1]) if b > 0 else 0
+            e[1] |= b << shift
+            e[0] |= (nbins - 1) << shift
+    return [_key_to_float(e[1]) for e in st]
+
+
 def kth_smallest(x: torch.Tensor, k: int, world: int = 1) -> float:
     """Exact k-th smallest (0-based) float32 value over all ranks."""
-    pmask, prefix = 0, 0
-    for shift, nbins in _PASSES:
-        h = _hist_pass(x, pmask, prefix, shift, nbins, world)
-        c = np.cumsum(h)
-        b = int(np.searchsorted(c, k + 1))
-        k -= int(c[b - 1]) if b > 0 else 0
-        prefix |= b << shift
-        pmask |= (nbins - 1) << shift
-    return _key_to_float(prefix)
+    return kth_smallest_many(x, [k], world)[0]
 
 
 def quantile(x: torch.Tensor, qs, world: int = 1, n_total: int | None = None) -> np.ndarray:
-    """np.quantile(x, qs) with linear interpolation, exact for float32 data."""
+    """np.quantile(x, qs) with linear interpolation, exact for float32 data
+    (all order statistics selected together, :func:`kth_smallest_many`)."""
     x = x.reshape(-1).float()
     n = int(n_total) if n_total is not None else x.numel() * world
-    out = []
+    plan = []
     for q in np.atleast_1d(qs):
         h = (n - 1) * float(q)
         lo = int(math.floor(h))
-        a = kth_smallest(x, lo, world)
-        if lo + 1 < n and h > lo:
-            b = kth_smallest(x, lo + 1, world)
-            out.append(a + (h - lo) * (b - a))
-        else:
-            out.append(a)
+        plan.append((h, lo, lo + 1 < n and h > lo))
+    ks = sorted({lo for _, lo, _ in plan} | {lo + 1 for _, lo, two in plan if two})
+    val = dict(zip(ks, kth_smallest_many(x, ks, world)))
+    out = []
+    for h, lo, two in plan:
+        a = val[lo]
+        out.append(a + (h - lo) * (val[lo + 1] - a) if two else a)
     return np.asarray(out)
 
 
