@@ -262,7 +262,7 @@ RPH_INLINE double lm_rsq(double x) {
 // redundantly on every lane (its L entries are LDS broadcasts), then every
 // lane applies the block to its own rows (8 independent products, tree sum).
 // rdg = reciprocal pivots.  The solution replaces vec.
-template <int P, class SY>
+template <int P, class SY, bool FWD = true>
 RPH_INLINE void lm_tri_solve_wave(const double* A, double* vec, const double* rdg) {
   static_assert(P <= 192, "three rows per lane");
   constexpr int NS = (P + 63) / 64, NB = (P + 7) / 8;
@@ -283,7 +283,7 @@ RPH_INLINE void lm_tri_solve_wave(const double* A, double* vec, const double* rd
     return v;
   };
   // ---- forward: L y = b --------------------------------------------------------
-  for (int K = 0; K < NB; ++K) {
+  for (int K = 0; K < (FWD ? NB : 0); ++K) {
     const int k0 = 8 * K, sK = k0 >> 6, l0 = k0 & 63;
     double lr[NS][8];  // this lane's rows of the block's columns (independent of the chain)
 #pragma unroll
@@ -370,6 +370,7 @@ struct CholTiles {
   static constexpr int NT = (PB + 15) / 16;
   static constexpr int NTILE = NT * (NT + 1) / 2;
   static constexpr int TPW = (NTILE + 3) / 4;
+  static constexpr int RWX = 16 * NT > PB ? 16 * NT : PB + 1;  // LDS rows: tile grid + the rhs row PB
   static constexpr int col(int t) {
     int b = 0;
     while (t >= NT - b) t -= NT - b++;
@@ -420,7 +421,7 @@ struct CholWave {
   // C -= U U^T over the active tiles (column block >= bk), U = uL (two
   // v_mfma_f64_16x16x4_f64 per tile: K = 8), then the owners of column block
   // bk write the next panel's columns [off, off + 8) to cn
-  RPH_INLINE static void update(lm_d4* C, const double (*fu)[2], int bk, int off, double (*cn)[16 * CT::NT], int lr,
+  RPH_INLINE static void update(lm_d4* C, const double (*fu)[2], int bk, int off, double (*cn)[CT::RWX], int lr,
                                 int lq) {
     lm_static_for<TPW>([&](auto jc) {
       constexpr int j = decltype(jc)::value, t = W + 4 * j;
@@ -455,8 +456,8 @@ struct CholWave {
 // Phase 1 is one copy of code for all waves; only the small tile code is
 // per-wave (one kernel body fits the instruction cache).
 template <int P, class SY>
-RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[16 * CholTiles<P>::NT], double (*uL)[9],
-                               unsigned long long* stamps) {
+RPH_INLINE void lm_chol_factor(double* A, double* vec, int* s_fail, double (*colb)[CholTiles<P>::RWX],
+                               double (*uL)[9], unsigned long long* stamps) {
   using CT = CholTiles<P>;
   constexpr int PB = CT::PB, NK = PB / 8, NT = CT::NT, TPW = CT::TPW;
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
@@ -467,13 +468,18 @@ RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[16 * CholT
     case 2: CholWave<P, SY, 2>::load(C, A, lr, lq); break;
     default: CholWave<P, SY, 3>::load(C, A, lr, lq); break;
   }
+  // the right-hand side rides along as row PB of the factorization (its L21
+  // row is y = L^-1 b): thread j < PB keeps element (PB, j) in a register and
+  // applies the rank-8 updates on the VALU
+  double rb = tid < P ? vec[tid] : 0.0;
   for (int K = 0; K < NK; ++K) {
     const int k0 = 8 * K;
     __syncthreads();
     if (K == 6) RPH_STAMPB(8);
-    const double(*cb)[16 * NT] = colb;  // single buffer: phase 2 overwrites it after the barrier
-    // ---- phase 1: row threads t in [k0, PB): diagonal block + L21 row ----------
-    if (tid >= k0 && tid < PB) {
+    const double(*cb)[CT::RWX] = colb;  // single buffer: phase 2 overwrites it after the barrier
+    // ---- phase 1: row threads t in [k0, PB]: diagonal block + L21 row ----------
+    // (thread PB is the right-hand side: its "L21 row" is y = L^-1 b)
+    if (tid >= k0 && tid <= PB) {
       double L[8][8], rl[8];
       bool ok = true;
 #pragma unroll
@@ -504,6 +510,7 @@ RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[16 * CholT
           u[c] = v * rl[c];
           uL[i][c] = u[c];
           if (i < P && k0 + c < P) A[SY::idx(i, k0 + c)] = u[c];
+          if (i == PB && k0 + c < P) vec[k0 + c] = u[c];  // forward solve, free
         }
       } else if (i < P) {
         const int rr = i - k0;
@@ -528,12 +535,19 @@ RPH_INLINE void lm_chol_factor(double* A, int* s_fail, double (*colb)[16 * CholT
     for (int X = 0; X < NT; ++X)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) fu[X][s2] = uL[16 * X + lr][4 * s2 + lq];
-    double(*cn)[16 * NT] = colb;
+    double(*cn)[CT::RWX] = colb;
     switch (wid) {
       case 0: CholWave<P, SY, 0>::update(C, fu, bk, off, cn, lr, lq); break;
       case 1: CholWave<P, SY, 1>::update(C, fu, bk, off, cn, lr, lq); break;
       case 2: CholWave<P, SY, 2>::update(C, fu, bk, off, cn, lr, lq); break;
       default: CholWave<P, SY, 3>::update(C, fu, bk, off, cn, lr, lq); break;
+    }
+    if (tid >= kn && tid < PB) {
+      double pr[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pr[q] = __builtin_fma(uL[PB][q + 4], uL[tid][q + 4], uL[PB][q] * uL[tid][q]);
+      rb -= (pr[0] + pr[1]) + (pr[2] + pr[3]);
+      if (tid < kn + 8) cn[tid - kn][PB] = rb;
     }
     if (K == 6) RPH_STAMPB(10);
   }
@@ -549,7 +563,7 @@ template <int P, class SY>
 RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsigned long long* stamps) {
   constexpr int PB = (P + 7) / 8 * 8;
   constexpr int NK = PB / 8;
-  constexpr int RW = 16 * CholTiles<P>::NT;  // rows of the tile grid
+  constexpr int RW = CholTiles<P>::RWX;  // rows of the tile grid + the right-hand side row PB
   static_assert(PB <= 192, "blocked solver: up to 192 parameters");
   __shared__ double colb[8][RW];
   __shared__ double uL[RW][9];
@@ -557,9 +571,11 @@ RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsig
   for (int t = tid; t < RW * 9; t += 256) (&uL[0][0])[t] = 0.0;
   for (int e = tid; e < 8 * RW; e += 256) {
     const int c = e / RW, i = e % RW;
-    colb[c][i] = (i < P && c <= i) ? A[SY::idx(i, c)] : ((i == c && i < PB) ? 1.0 : 0.0);
+    colb[c][i] = (i < P && c <= i) ? A[SY::idx(i, c)]
+                 : i == PB         ? (c < P ? vec[c] : 0.0)
+                                   : ((i == c && i < PB) ? 1.0 : 0.0);
   }
-  lm_chol_factor<P, SY>(A, s_fail, colb, uL, stamps);
+  lm_chol_factor<P, SY>(A, vec, s_fail, colb, uL, stamps);
   __syncthreads();
   if (*s_fail) return;
   RPH_STAMPB(6);
@@ -568,7 +584,7 @@ RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsig
   for (int k = tid; k < P; k += 256) rdg[k] = lm_rcp(A[SY::idx(k, k)]);
   __syncthreads();
   RPH_STAMPB(7);
-  if (wid == 0) lm_tri_solve_wave<P, SY>(A, vec, rdg);
+  if (wid == 0) lm_tri_solve_wave<P, SY, false>(A, vec, rdg);  // y = L^-1 b came out of the factorization
   __syncthreads();
   RPH_STAMPB(12);
 }
