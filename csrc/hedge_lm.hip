@@ -480,7 +480,9 @@ RPH_INLINE void lm_chol_factor(double* A, double* vec, int* s_fail, double (*col
     // ---- phase 1: row threads t in [k0, PB]: diagonal block + L21 row ----------
     // (thread PB is the right-hand side: its "L21 row" is y = L^-1 b)
     if (tid >= k0 && tid <= PB) {
-      double L[8][8], rl[8];
+      double L[8][8], rl[8], u[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) u[c] = cb[c][tid];  // this row's panel entries (latency under the diag chain)
       bool ok = true;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -501,16 +503,26 @@ RPH_INLINE void lm_chol_factor(double* A, double* vec, int* s_fail, double (*col
       if (!ok && tid == k0) *s_fail = 1;
       const int i = tid;
       if (i >= k0 + 8) {
-        double u[8];
+        // the row's 8 panel entries are read BEFORE any store (the stores to
+        // uL / A may alias the panel for the compiler, which would otherwise
+        // wait out one LDS round trip per column)
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          double v = cb[c][i];
+          double v = u[c];
 #pragma unroll
           for (int p = 0; p < c; ++p) v -= u[p] * L[c][p];
           u[c] = v * rl[c];
-          uL[i][c] = u[c];
-          if (i < P && k0 + c < P) A[SY::idx(i, k0 + c)] = u[c];
-          if (i == PB && k0 + c < P) vec[k0 + c] = u[c];  // forward solve, free
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) uL[i][c] = u[c];
+        if (i < P) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (k0 + c < P) A[SY::idx(i, k0 + c)] = u[c];
+        } else if (i == PB) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (k0 + c < P) vec[k0 + c] = u[c];  // forward solve, free
         }
       } else if (i < P) {
         const int rr = i - k0;
