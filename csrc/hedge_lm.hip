@@ -192,35 +192,51 @@ template <int P, int R>
 __global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __restrict__ red) {
   using LS = LmShape<P>;
   constexpr int NG = LS::NBLK * 1024;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e < NG) {
-    double s = 0.0;
+  __shared__ double part[256];
+  if ((int)blockIdx.x < NG / 64) {
+    // Gram: workgroup handles entries [64 b, 64 b + 64), thread (g, l) sums
+    // the slabs g, g + 4, ... of entry 64 b + l (16 loads in flight per
+    // thread for 64 slabs), the 4 partial sums combined in LDS in fixed order
+    const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + l;
     const float* col = lm.slab_g + e;
+    double s0 = 0.0, s1 = 0.0;
+    int w = g;
 #pragma unroll 4
-    for (int w = 0; w < lm.gram_wgs; ++w) s += (double)col[(size_t)w * NG];
-    red[e] = s * (double)lm.inv_ns;
+    for (; w + 4 < lm.gram_wgs; w += 8) {
+      s0 += (double)col[(size_t)w * NG];
+      s1 += (double)col[(size_t)(w + 4) * NG];
+    }
+    if (w < lm.gram_wgs) s0 += (double)col[(size_t)w * NG];
+    part[threadIdx.x] = s0 + s1;
+    __syncthreads();
+    if (g == 0) red[e] = ((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) * (double)lm.inv_ns;
     return;
   }
-  // gradient packet: workgroup pw handles entries [16 pw, 16 pw + 16), each
-  // over 16 row groups (rows g, g + 16, ...) combined in LDS in a fixed order
-  __shared__ double part[256];
-  const int pw = blockIdx.x - NG / 256;
-  const int i = pw * 16 + (threadIdx.x & 15), grp = threadIdx.x >> 4;
+  // gradient packet: workgroup pw handles entries [4 pw, 4 pw + 4); thread
+  // (grp, k) sums rows grp, grp + 64, ... of entry 4 pw + k (8 rows in flight
+  // at 512 workgroups), then a fixed-order LDS tree over the 64 row groups
+  const int pw = blockIdx.x - NG / 64;
+  const int k = threadIdx.x & 3, grp = threadIdx.x >> 2;
+  const int i = pw * 4 + k;
   double s0 = 0.0, s1 = 0.0;
   int w = grp;
-  for (; w + 16 < lm.num_wgs; w += 32) {
+  for (; w + 64 < lm.num_wgs; w += 128) {
     s0 += (double)lm.slab_b[(size_t)w * R + i];
-    s1 += (double)lm.slab_b[(size_t)(w + 16) * R + i];
+    s1 += (double)lm.slab_b[(size_t)(w + 64) * R + i];
   }
   if (w < lm.num_wgs) s0 += (double)lm.slab_b[(size_t)w * R + i];
   part[threadIdx.x] = s0 + s1;
   __syncthreads();
-  if (threadIdx.x < 16) {
-    double v = 0.0;
-    for (int q = 0; q < 16; ++q) v += part[q * 16 + threadIdx.x];
-    const int e2 = pw * 16 + threadIdx.x;
-    if (e2 < P) red[LM_GBLK_MAX + e2] = v;
-    else if (e2 < P + 4) red[LM_GBLK_MAX + LM_NPMAX + e2 - P] = v;
+#pragma unroll
+  for (int st = 32; st >= 1; st >>= 1) {
+    if (grp < st) part[threadIdx.x] += part[threadIdx.x + 4 * st];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) {
+    const double v = part[threadIdx.x];
+    if (i < P) red[LM_GBLK_MAX + i] = v;
+    else if (i < P + 4) red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
   }
 }
 
@@ -767,7 +783,7 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
     const long long last = ((ns - 1) / lm->gram_blk) * lm->gram_blk_stride + (ns - 1) % lm->gram_blk;
     if (last >= d->n_local) return rph_report("rph_lm", "Gram subsample leaves the shard");
   }
-  if (lm->red_wgs != nblk * 1024 / 256 + R / 16) return rph_report("rph_lm", "bad red_wgs");
+  if (lm->red_wgs != nblk * 1024 / 64 + R / 4) return rph_report("rph_lm", "bad red_wgs");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   (void)P;
   return 0;

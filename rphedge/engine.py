@@ -497,7 +497,7 @@ class HipBackend:
                         slab_b=torch.zeros(nw, R, dtype=torch.float32, device=dev),
                         slab_g=torch.zeros(gw, nblk * 1024, dtype=torch.float32, device=dev))
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
-            lm.num_wgs, lm.gram_wgs, lm.red_wgs = nw, gw, nblk * 1024 // 256 + R // 16
+            lm.num_wgs, lm.gram_wgs, lm.red_wgs = nw, gw, nblk * 1024 // 64 + R // 4
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, gw * L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(gw * L.LM_TILE * max(self.world, 1))
             lm.inv_n = 1.0 / float(self.n_local * max(self.world, 1))
