@@ -701,17 +701,35 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     return;
   }
   // ---- A = 2 G + lam diag(2 G) + ridge * mean diag, packed lower triangle -----
+  // every block of this wave is loaded first (one round trip for the whole
+  // Gram matrix, not one per block), then scattered into the LDS triangle
   const int h = lane >> 5, r = lane & 31;
-  for (int b = wid; b < NBLK; b += 4) {
+  constexpr int BPW = (NBLK + 3) / 4;
+  static_assert(P <= 256, "one parameter per thread");
+  const double gi = tid < P ? g[tid] : 0.0;                          // gradient (same round trip)
+  const double wbest = tid < P ? st[LMS_W + best * LM_NPMAX + tid] : 0.0;  // for the final update
+  double gv[BPW][16];
+#pragma unroll
+  for (int k = 0; k < BPW; ++k) {
+    const int b = wid + 4 * k;
+    if (b < NBLK) {
+      const double* blk = src + (size_t)b * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) gv[k][q] = blk[q * 64 + lane];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < BPW; ++k) {
+    const int b = wid + 4 * k;
+    if (b >= NBLK) continue;
     int mb, nb;
     lm_blk(b, NB, mb, nb);
-    const double* blk = src + (size_t)b * 1024;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int i = mb * 32 + lm_row(q, h), j = nb * 32 + r;  // i <= j when mb < nb
       if (i < P && j < P && (mb < nb || i >= j)) {
         const int hi = i > j ? i : j, lo = i > j ? j : i;
-        A[SY::idx(hi, lo)] = 2.0 * blk[q * 64 + lane];
+        A[SY::idx(hi, lo)] = 2.0 * gv[k][q];
       }
     }
   }
@@ -727,10 +745,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
   }
   __syncthreads();
-  for (int i = tid; i < P; i += 256) {
-    double& a = A[SY::idx(i, i)];
+  if (tid < P) {
+    double& a = A[SY::idx(tid, tid)];
     a = a * (1.0 + lam) + (double)lm.ridge * s_diag;
-    vec[i] = -g[i];
+    vec[tid] = -gi;
   }
   RPH_STAMP(2);
   __syncthreads();  // the damped diagonal is in place
@@ -751,7 +769,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   RPH_STAMP(4);
   RPH_STAMP(5);
-  for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i] + vec[i];
+  if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest + vec[tid];
   if (tid == 0) {
     st[LMS_BEST] = (double)best;
     st[LMS_LAM] = lam;
