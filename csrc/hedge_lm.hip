@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   using LS = LmShape<P>;
   constexpr int NP = LS::NP, NB = LS::NB, NBLK = LS::NBLK, JP = LS::JP;
   constexpr int NIN = B::NIN_, H = B::H_, NO = B::NO_, HEAD = B::HEAD_, NHOLD = B::NHOLD;
-  const uint32_t kat = prefetch_kernarg_begin<sizeof(TrainDesc) + sizeof(LmDesc) + 16>();
+  const uint32_t kat = prefetch_kernarg_begin<(sizeof(TrainDesc) + sizeof(LmDesc) + 16 < 640 ? sizeof(TrainDesc) + sizeof(LmDesc) + 16 : 640)>();
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
@@ -101,6 +101,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   if (pass == 0 && blockIdx.x == 0 && tid == 0) {
     st[LMS_BEST] = 1.0;
     st[LMS_LAM] = lm.lam0;
+    st[LMS_NU] = 2.0;
     st[LMS_NACC] = 0.0;
     st[LMS_FAIL] = 0.0;
   }
@@ -642,20 +643,33 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const double Lt = pkt(P + 0) / fmax(cnt, 1.0);
   const double Lb = pass == 0 ? INFINITY : st[LMS_RED + LM_GBLK_MAX + LM_NPMAX + 4];
   const bool accept = pass == 0 || (Lt == Lt && Lt < Lb);
-  double lam = st[LMS_LAM];
+  double lam = st[LMS_LAM], nu = st[LMS_NU];
   int best = best_old;
   if (accept) {
     best = trial;
-    if (pass > 0) lam = fmax(lam * lm.lam_down, (double)lm.lam_min);
+    if (pass > 0 && lm.damping == 1) {
+      // Nielsen: gain ratio of the actual to the model-predicted reduction
+      const double pred = st[LMS_PRED];
+      const double rho = pred > 0.0 ? (Lb - Lt) / pred : 1.0;
+      const double t = 2.0 * rho - 1.0;
+      lam = fmax(lam * fmax(1.0 / 3.0, 1.0 - t * t * t), (double)lm.lam_min);
+      nu = 2.0;
+    } else if (pass > 0) {
+      lam = fmax(lam * lm.lam_down, (double)lm.lam_min);
+    }
     // the best point's block := the trial's: read from red_new below, copied
     // by the next pass kernel (LMS_COPY); the best loss is recorded now
     if (tid == 0) {
       best_red[LM_GBLK_MAX + LM_NPMAX + 4] = Lt;
       st[LMS_NACC] += pass > 0 ? 1.0 : 0.0;
     }
+  } else if (lm.damping == 1) {
+    lam = fmin(lam * nu, (double)lm.lam_max);
+    nu *= 2.0;
   } else {
     lam = fmin(lam * lm.lam_up, (double)lm.lam_max);
   }
+  if (tid == 0) st[LMS_NU] = nu;
   if (tid == 0 && pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
   if (tid == 0) st[LMS_COPY] = accept ? 1.0 : 0.0;
   RPH_STAMP(1);
@@ -745,9 +759,11 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
   }
   __syncthreads();
+  double dmp = 0.0;  // this parameter's damping term lam 2G_ii + ridge (for the predicted reduction)
   if (tid < P) {
     double& a = A[SY::idx(tid, tid)];
-    a = a * (1.0 + lam) + (double)lm.ridge * s_diag;
+    dmp = a * lam + (double)lm.ridge * s_diag;
+    a = a + dmp;
     vec[tid] = -gi;
   }
   RPH_STAMP(2);
@@ -770,6 +786,21 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   RPH_STAMP(4);
   RPH_STAMP(5);
   if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest + vec[tid];
+  // predicted reduction of the quadratic model at the step d:
+  // -(g.d)/2 + d.(lam D + ridge) d / 2   ((2G + lam D + ridge) d = -g)
+  {
+    __shared__ double s_pred[4];
+    double pv = 0.0;
+    if (tid < P) {
+      const double dv = vec[tid];
+      pv = 0.5 * (dmp * dv * dv - gi * dv);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) pv += __shfl_xor(pv, o, 64);
+    if (lane == 0) s_pred[wid] = pv;
+    __syncthreads();
+    if (tid == 0) st[LMS_PRED] = (s_pred[0] + s_pred[1]) + (s_pred[2] + s_pred[3]);
+  }
   if (tid == 0) {
     st[LMS_BEST] = (double)best;
     st[LMS_LAM] = lam;

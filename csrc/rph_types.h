@@ -193,6 +193,8 @@ enum LmState : int {
   LMS_FAIL,                          // Cholesky failures (non-positive pivot)
   LMS_COPY,                          // 1: the last solve accepted; the next pass kernel copies the trial's
                                      // reduced block into the best slot (deferred off the solve's path)
+  LMS_NU,                            // Nielsen damping: growth factor of the next rejection
+  LMS_PRED,                          // predicted loss reduction of the pending trial (quadratic model)
   LMS_FLOATS = LMS_FAIL + 8
 };
 
@@ -219,6 +221,8 @@ struct LmDesc {
   int bias_index;
   int weights_only;              // 1: publish the weights only (no FitState / loss history: a bias refit
                                  // after an Adam fit, passes = 0)
+  int damping;                   // 0: lam x lam_down / x lam_up on accept / reject; 1: Nielsen (gain ratio)
+  int pad2;
 };
 
 // Data-parallel exchange of the LM reduced block over IPC-mapped peer

@@ -120,6 +120,10 @@ class TrainConfig:
     lm_lam_min: float = 1e-9
     lm_lam_max: float = 1e10
     lm_ridge: float = 1e-10
+    # damping update: "simple" (x lam_down on accept, x lam_up on reject) or
+    # "nielsen" (gain ratio rho of actual / predicted reduction: accept
+    # x max(1/3, 1 - (2 rho - 1)^3), reject x nu with nu doubling)
+    lm_damping: str = "simple"
     # after the last pass: exact Newton step on the bond holding's output bias
     # (free heads), so the fitted values' mean over all paths equals the
     # target's and no mean error drifts down the backward induction
@@ -504,6 +508,7 @@ class HipBackend:
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
             lm.bias_index = _lm_bias_index(self.spec, t)
+            lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
             bufs["desc"] = lm
             return bufs
         return self._cache.get(("lm",), make)
@@ -810,7 +815,8 @@ class TorchBackend:
 
         cur = int(wts[L.W_CUR].item())
         w_best = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
-        lam = float(t.lm_lam0)
+        lam, nu = float(t.lm_lam0), 2.0
+        nielsen = str(t.lm_damping).lower() == "nielsen"
         hist = []
         G, g, stb = evaluate(w_best)
         Lb = float(stb[0] / stb[3].clamp_min(1.0))
@@ -819,19 +825,31 @@ class TorchBackend:
         for k in range(1, int(fcfg.epochs) + 1):
             A = 2.0 * G
             dg = torch.diagonal(A).clone()
-            A = A + torch.diag(dg * lam + float(t.lm_ridge) * float(dg.mean()))
+            dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
+            A = A + torch.diag(dmp)
             Lc, info = torch.linalg.cholesky_ex(A)
+            pred = 0.0
             if int(info) != 0:
                 trial = w_best.clone()
                 lam = min(lam * t.lm_lam_up * t.lm_lam_up, t.lm_lam_max)
             else:
-                trial = w_best + torch.cholesky_solve(-g[:, None], Lc)[:, 0]
+                dlt = torch.cholesky_solve(-g[:, None], Lc)[:, 0]
+                trial = w_best + dlt
+                pred = float(0.5 * ((dmp * dlt * dlt).sum() - (g * dlt).sum()))
             Gt, gt, stt = evaluate(trial)
             Lt = float(stt[0] / stt[3].clamp_min(1.0))
             hist.append(Lt)
             if Lt == Lt and Lt < Lb:
+                if nielsen:
+                    rho = (Lb - Lt) / pred if pred > 0.0 else 1.0
+                    lam = max(lam * max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3), t.lm_lam_min)
+                    nu = 2.0
+                else:
+                    lam = max(lam * t.lm_lam_down, t.lm_lam_min)
                 w_best, G, g, stb, Lb = trial, Gt, gt, stt, Lt
-                lam = max(lam * t.lm_lam_down, t.lm_lam_min)
+            elif nielsen:
+                lam = min(lam * nu, t.lm_lam_max)
+                nu *= 2.0
             else:
                 lam = min(lam * t.lm_lam_up, t.lm_lam_max)
         bi = _lm_bias_index(spec, t)

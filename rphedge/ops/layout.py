@@ -71,5 +71,7 @@ LMS_LAM = LMS_BEST + 1
 LMS_NACC = LMS_BEST + 2
 LMS_FAIL = LMS_BEST + 3
 LMS_COPY = LMS_BEST + 4
+LMS_NU = LMS_BEST + 5
+LMS_PRED = LMS_BEST + 6
 LM_DP_WGS = 16
 LMS_FLOATS = LMS_FAIL + 8

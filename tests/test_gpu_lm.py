@@ -95,14 +95,19 @@ def test_lm_pass_block_matches_fp64(shape):
     assert st[0] == pytest.approx(float((e * e).sum()), rel=1e-5) and st[3] == n
 
 
-@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0), (5, 8, 6, 0)])
-def test_lm_fit_matches_torch_and_is_deterministic(shape):
+@pytest.mark.parametrize("shape,damping", [((1, 8, 2, 0), "simple"), ((3, 8, 2, 0), "simple"),
+                                           ((5, 8, 6, 0), "simple"), ((1, 8, 2, 0), "nielsen"),
+                                           ((3, 8, 2, 0), "nielsen")])
+def test_lm_fit_matches_torch_and_is_deterministic(shape, damping):
+    """HIP LM fit == fp64 torch reference (same accept / reject sequence and
+    damping rule: simple x1/3 / x4, or Nielsen's gain-ratio update with the
+    solve kernel's predicted reduction), bitwise run to run."""
     from rphedge.engine import FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
 
     dev = torch.device("cuda", 0)
     n = 1 << 14
     spec, feats, pr, y, data, w0 = _setup(shape, n, dev, seed=3)
-    tc = TrainConfig(batch_size=n, lm_gram_paths=2048)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=2048, lm_damping=damping)
     fc = FitConfig(epochs=12, optimizer="lm", early_stopping=False)
     outs = []
     for _ in range(2):
