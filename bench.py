@@ -118,6 +118,9 @@ def parse(argv=None):
     ap.add_argument("--lm-passes-rest", type=int, default=None)
     ap.add_argument("--lm-gram-paths", type=int, default=None)
     ap.add_argument("--lm-damping", default=None, choices=["simple", "nielsen"])
+    ap.add_argument("--lm-lam0", type=float, default=None)
+    ap.add_argument("--lm-lam-up", type=float, default=None)
+    ap.add_argument("--lm-lam-down", type=float, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -135,7 +138,7 @@ def parse(argv=None):
     if a.optimizer is None:
         a.optimizer = pre.get("optimizer", "adam")
     for k, dflt in (("lm_passes_first", 80), ("lm_passes_rest", 3), ("lm_gram_paths", 4096),
-                    ("lm_damping", "simple")):
+                    ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -153,7 +156,8 @@ def build_run(a, world: int):
                         chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision,
                         variant=a.variant, max_wgs=a.max_wgs, feature_norm=a.feature_norm,
                         optimizer=a.optimizer, lm_passes_first=a.lm_passes_first, lm_passes_rest=a.lm_passes_rest,
-                        lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping)
+                        lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping, lm_lam0=a.lm_lam0,
+                        lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -318,6 +322,7 @@ def main(argv=None):
                    "lm_passes_rest": a.lm_passes_rest if lm else None,
                    "lm_gram_paths": a.lm_gram_paths if lm else None,
                    "lm_damping": a.lm_damping if lm else None,
+                   "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
                    "steps_per_epoch": run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,
                    "step_schedule": run.backend.step_mode() if hasattr(run.backend, "step_mode") else "torch",

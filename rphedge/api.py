@@ -232,7 +232,9 @@ class HedgeRun:
         tcfg = TrainConfig(batch_size=tr.batch_size, shuffle=tr.shuffle, chunk_log2=tr.chunk_log2, seed=tr.seed,
                            lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs,
                            mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode,
-                           lm_gram_paths=int(tr.lm_gram_paths), lm_damping=str(tr.lm_damping))
+                           lm_gram_paths=int(tr.lm_gram_paths), lm_damping=str(tr.lm_damping),
+                           lm_lam0=float(tr.lm_lam0), lm_lam_up=float(tr.lm_lam_up),
+                           lm_lam_down=float(tr.lm_lam_down))
         if int(tr.variant) >= 0:
             tcfg.variant = int(tr.variant)
         kw = {}

@@ -90,6 +90,9 @@ class TrainingParams:
     lm_passes_rest: int = 3          # LM trial points on later dates (warm start, Q18)
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
     lm_damping: str = "simple"       # LM damping update: simple (x1/3 / x4) | nielsen (gain ratio)
+    lm_lam0: float = 1e-3            # LM initial damping of every fit
+    lm_lam_up: float = 4.0           # simple rule: damping x lam_up on a rejected trial
+    lm_lam_down: float = 1.0 / 3.0   #              x lam_down on an accepted one
     mean_refit: bool = True          # after each Adam MSE fit: exact refit of the bond holding's bias (the
                                      # residual mean over all paths -> 0; no mean error drifts into V0)
     feature_norm: str = "date"       # input standardisation: none | global | date (driver.feature_norms);
