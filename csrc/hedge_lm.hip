@@ -554,7 +554,8 @@ RPH_INLINE void lm_chol_factor(double* A, double* vec, int* s_fail, double (*col
     }
     __syncthreads();
     if (K == 6) RPH_STAMPB(9);
-    if (*s_fail) return;
+    // (a non-positive pivot only poisons the rest with NaNs: checked once after
+    // the loop, not with an LDS round trip per panel)
     // ---- phase 2: rank-8 update of the trailing tiles on the matrix cores -------
     const int kn = k0 + 8;
     if (kn >= PB) break;
