@@ -354,3 +354,19 @@ def test_phase_timer_does_not_leak():
     del t
     gc.collect()
     assert profiling.live_timers() == n0
+
+
+def test_cli_lm_example_config(tmp_path):
+    """examples/euro_call_30_lm.json (full-batch Levenberg-Marquardt fits)
+    through the CLI on the CPU oracle, at a reduced size."""
+    cfg = dict(json.load(open(os.path.join(ROOT, "examples", "euro_call_30_lm.json"))), n_paths=11,
+               rebalancing=0.25, dt=0.25, batch_size=2048, lm_passes_first=20, lm_passes_rest=2, device="cpu",
+               verbose=False)
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(cfg))
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "rphedge", "run", "--config", str(p)], capture_output=True, text=True,
+                         cwd=ROOT, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr
+    res = json.loads(out.stdout)
+    assert abs(res["V0"] - 10.3896) < 0.6, res
