@@ -28,6 +28,15 @@ STAMP = LIBDIR / "librphedge.sha256"
 ARCH = os.environ.get("RPH_OFFLOAD_ARCH", "gfx950")
 
 
+# per-translation-unit code-generation flags
+PER_FILE_FLAGS = {
+    # LM solve: keep the fp64 MFMA accumulators of the Cholesky trailing update
+    # in VGPRs (the default AGPR form copied them across every panel: ~650
+    # v_accvgpr moves per solve)
+    "hedge_lm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
 def _hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and Path(cand).exists():
@@ -70,7 +79,7 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False, asan:
     if asan:
         flags += ["-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
         lib, stamp = LIBDIR / "librphedge_asan.so", LIBDIR / "librphedge_asan.sha256"
-    digest = _digest(" ".join(flags))
+    digest = _digest(" ".join(flags) + repr(sorted(PER_FILE_FLAGS.items())))
     if not force and lib.exists() and stamp.exists() and stamp.read_text().strip() == digest:
         return lib
     tmp = lib.with_suffix(".so.tmp")
@@ -82,7 +91,7 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False, asan:
     jobs = []
     for src in sources():
         obj = objdir / (src.name + ".o")
-        jobs.append(([_hipcc(), *cflags, "-c", str(src), "-o", str(obj)], obj))
+        jobs.append(([_hipcc(), *cflags, *PER_FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)], obj))
     from concurrent.futures import ThreadPoolExecutor
 
     def _run(job):
