@@ -152,9 +152,12 @@ def close_mailbox(mb):
     mb.close()
 
 
-def _probe_xgmi_local(info: DistInfo, mb) -> tuple[bool, torch.Tensor | None]:
-    """This rank's half of the probe: a tiny data-parallel fit over the fused
-    xGMI exchange (the default lagged schedule).  Returns (ok, weights)."""
+def _probe_xgmi_local(info: DistInfo, mb, lmb) -> tuple[bool, torch.Tensor | None]:
+    """This rank's half of the probe: two tiny data-parallel fits, one per
+    in-kernel exchange the runs use - Keras-Adam steps over the fused packet
+    exchange (``mb``, the lagged schedule) and Levenberg-Marquardt passes over
+    the reduced-block exchange (``lmb``, k_lm_dp_exchange, the default
+    optimiser).  Returns (ok, both fits' weights concatenated)."""
     from ..engine import DateData, FitConfig, HipBackend, TrainConfig
     from ..models.hedge_mlp import NetSpec, init_weights
 
@@ -163,15 +166,20 @@ def _probe_xgmi_local(info: DistInfo, mb) -> tuple[bool, torch.Tensor | None]:
         n = 1 << 12
         g = torch.Generator().manual_seed(100 + info.rank)          # different data per rank
         x = (torch.rand(n, generator=g) * 0.6 + 0.7).to(info.device)
-        be = HipBackend(spec, n, TrainConfig(batch_size=n * info.world, chunk_log2=6), device=info.device,
-                        world=info.world, rank=info.rank, mailbox=mb)
+        be = HipBackend(spec, n, TrainConfig(batch_size=n * info.world, chunk_log2=6, lm_gram_paths=2048),
+                        device=info.device, world=info.world, rank=info.rank, mailbox=mb, lm_mailbox=lmb)
         data = DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=torch.relu(x - 1.0),
                         prices_now=[x])
-        w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
-        be.fit(w, o, f, data, FitConfig(epochs=4, patience=10 ** 6, early_stopping=False), seed=5)
+        outs = []
+        for fc in (FitConfig(epochs=4, patience=10 ** 6, early_stopping=False),
+                   FitConfig(epochs=3, optimizer="lm", early_stopping=False)):
+            w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+            be.fit(w, o, f, data, fc, seed=5)
+            outs.append(w[: spec.nparams].double())
         torch.cuda.synchronize(info.device)
-        wv = w[: spec.nparams].double()
-        return int(mb.error[0].item()) == 0 and bool(torch.isfinite(wv).all()), wv
+        wv = torch.cat(outs)
+        clean = int(mb.error[0].item()) == 0 and int(lmb.error[0].item()) == 0
+        return clean and bool(torch.isfinite(wv).all()), wv
     except Exception:
         return False, None
 
@@ -190,13 +198,19 @@ def select_transport(info: DistInfo) -> str:
         return info.dp_mode
     from ..models.hedge_mlp import NetSpec
 
-    P = NetSpec(nin=1, hidden=8, nout=2, head=0).nparams
-    mb = None
-    try:
-        mb = make_mailbox(info, NetSpec(nin=1, hidden=8, nout=2, head=0).red_width, tag="rph_probe")
-        ok_l, wv = _probe_xgmi_local(info, mb)
-    except Exception:
-        ok_l, wv = False, None
+    from ..ops import layout as L
+
+    def try_mailbox(R, tag):  # make_mailbox joins its barrier on every rank even when it raises
+        try:
+            return make_mailbox(info, R, tag=tag)
+        except Exception:
+            return None
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    P = 2 * spec.nparams
+    mb = try_mailbox(spec.red_width, "rph_probe")
+    lmb = try_mailbox(L.LM_RED + L.LM_DP_WGS, "rph_probe_lm")
+    ok_l, wv = _probe_xgmi_local(info, mb, lmb) if (mb is not None and lmb is not None) else (False, None)
     ok = torch.tensor([1.0 if ok_l else 0.0], dtype=torch.float64, device=info.device)
     all_reduce_(ok, "min")
     w = wv if (wv is not None and wv.numel() == P) else torch.zeros(P, dtype=torch.float64, device=info.device)
@@ -205,10 +219,11 @@ def select_transport(info: DistInfo) -> str:
     all_reduce_(mn, "min")
     same = torch.tensor([1.0 if bool(torch.equal(mx, mn)) else 0.0], dtype=torch.float64, device=info.device)
     all_reduce_(same, "min")
-    try:
-        close_mailbox(mb)
-    except Exception:
-        pass
+    for m in (mb, lmb):
+        try:
+            close_mailbox(m)
+        except Exception:
+            pass
     all_ok = float(ok.item()) >= 1.0 and float(same.item()) >= 1.0
     info.probe = {"local_ok": bool(ok_l), "all_ok": bool(float(ok.item()) >= 1.0),
                   "bitwise_equal_weights": bool(float(same.item()) >= 1.0), "chosen": "xgmi" if all_ok else "rccl"}

@@ -88,3 +88,20 @@ def test_bench_bare_gpus_self_launches(nproc):
         t = _bench(args, nproc=nproc)
         assert set(r) == set(t) and set(r["config"]) == set(t["config"]) and set(r["quality"]) == set(t["quality"])
         assert r["quality"]["V0"] == t["quality"]["V0"]  # same global paths, same ranks: same result
+
+
+@pytest.mark.gpu
+def test_bench_bare_two_ranks_one_gpu_lm():
+    """The driver's scaling invocation on the GPU path, rehearsed with two
+    ranks sharing one card: self-launch, the transport probe (Adam packet AND
+    LM reduced-block exchanges over the IPC mailboxes) picks xgmi, the default
+    LM preset runs data parallel, and the result is the 2-rank fit of the
+    doubled global path set (V0 on the BS price)."""
+    r = _bench(["--steps", "1", "--warmup", "1", "--paths-log2", "16", "--lm-passes-first", "30"],
+               nproc=2, bare=True)
+    c = r["config"]
+    assert r["n_gpus"] == 2 and c["dist_world"] == 2 and c["optimizer"] == "lm" and c["backend"] == "hip"
+    assert c["dp_probe"] == {"local_ok": True, "all_ok": True, "bitwise_equal_weights": True, "chosen": "xgmi"}
+    assert c["dp_transport"] == "xgmi" and c["paths_global"] == 2 << 16
+    assert abs(r["quality"]["V0"] - 10.3896) < 0.1, r["quality"]
+    assert math.isfinite(r["quality"]["terminal_pnl_std"]) and r["quality"]["terminal_pnl_std"] < 1.5
