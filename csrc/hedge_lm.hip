@@ -75,6 +75,14 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   prefetch_kernarg_end(kat);
+  // diagnostic phase stamps of every workgroup but 0 and 1 (tools/stamp_lm.py;
+  // rows 0 and 1 belong to k_lm_solve)
+  const bool stamp_wg = blockIdx.x >= 2;
+#define RPH_STAMPP(k)                 \
+  do {                                \
+    if (stamp_wg) RPH_STAMP(k);       \
+  } while (0)
+  RPH_STAMPP(0);
   double* st = lm.state;
   // trial point: pass 0 = the start point (canonical weights, published as
   // slot 0); later passes = the slot k_lm_solve wrote
@@ -106,6 +114,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     st[LMS_FAIL] = 0.0;
   }
   __syncthreads();
+  RPH_STAMPP(1);
   // ---- loss + exact gradient over every local path (VALU) -------------------
   typename B::Frags fr;
   B::make_frags(wl + S::OW2, fr);
@@ -114,6 +123,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 #pragma unroll
   for (int j = 0; j < NR; ++j)
     if (tid + 256 * j < R) lm.slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
+  RPH_STAMPP(2);
   if ((int)blockIdx.x >= lm.gram_wgs) return;
   // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
   if (wid == 0) {
@@ -170,6 +180,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     for (int i = P; i < NP; ++i) row[i] = 0.f;
   }
   __syncthreads();
+  RPH_STAMPP(3);
   const int h = lane >> 5, r = lane & 31;
   for (int b = wid; b < NBLK; b += 4) {
     int mb, nb;
@@ -184,6 +195,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 #pragma unroll
     for (int q = 0; q < 16; ++q) out[q * 64 + lane] = acc[q];
   }
+  RPH_STAMPP(4);
+#undef RPH_STAMPP
 }
 
 // ---------------------------------------------------------------------------

@@ -13,7 +13,7 @@ __device__ __forceinline__ double rsq1(double x) {
 }
 
 template <int V>
-__global__ __launch_bounds__(256) void k(double* out, unsigned long long* t, int iters) {
+__global__ __launch_bounds__(256) void k(double* out, unsigned long long* t, int iters, int kfix) {
   __shared__ double cb[8][128];
   __shared__ double uL[128][9];
   const int tid = threadIdx.x;
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* t, int
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long c0 = __builtin_readcyclecounter();
   for (int it = 0; it < iters; ++it) {
-    const int k0 = V == 5 ? 104 : 8 * (it % 13);
+    const int k0 = V == 5 ? 104 : V == 6 ? kfix : V == 7 ? 0 : V == 8 ? kfix + 0 * it : 8 * (it % 13);
     __syncthreads();
     if (V == 1) continue;
     if (tid >= k0 && tid < 112) {
@@ -41,6 +41,30 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* t, int
         for (int c = 0; c < 8; ++c) uL[tid][c] = s + cb[c][tid];
         continue;
       }
+      if (V == 9 || V == 10) {
+        // right-looking 8x8 factor: column c scaled, then the trailing
+        // entries updated at once (short dependency chain per pivot)
+        double a[8][8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+#pragma unroll
+          for (int r = c; r < 8; ++r) a[r][c] = cb[c][k0 + r];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          rl[c] = rsq1(a[c][c]);
+          L[c][c] = a[c][c] * rl[c];
+#pragma unroll
+          for (int r = c + 1; r < 8; ++r) L[r][c] = a[r][c] * rl[c];
+#pragma unroll
+          for (int q = c + 1; q < 8; ++q)
+#pragma unroll
+            for (int r = q; r < 8; ++r) a[r][q] = __builtin_fma(-L[r][c], L[q][c], a[r][q]);
+        }
+        if (V == 9) {
+          acc += L[7][7];
+          continue;
+        }
+      } else
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         double sc = cb[c][k0 + c];
@@ -86,13 +110,13 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* t, int
 }
 
 template <int V>
-void run(const char* name) {
+void run(const char* name, int kf = 0) {
   double* o; unsigned long long* t;
   hipMalloc(&o, 256 * 8); hipMalloc(&t, 16);
   const int iters = 1300;
-  hipLaunchKernelGGL(k<V>, dim3(1), dim3(256), 0, 0, o, t, iters);
+  hipLaunchKernelGGL(k<V>, dim3(1), dim3(256), 0, 0, o, t, iters, kf);
   hipDeviceSynchronize();
-  hipLaunchKernelGGL(k<V>, dim3(1), dim3(256), 0, 0, o, t, iters);
+  hipLaunchKernelGGL(k<V>, dim3(1), dim3(256), 0, 0, o, t, iters, kf);
   unsigned long long h[2]; hipMemcpy(h, t, 16, hipMemcpyDeviceToHost);
   printf("%-36s %.1f ns per panel  %.0f shader cycles per panel  (clock %.2f GHz)\n", name, h[0] * 10.0 / iters,
          (double)h[1] / iters, h[1] / (h[0] * 10.0));
@@ -106,5 +130,11 @@ int main() {
   run<0>("full phase 1");
   run<4>("full, raw rsq (no Newton)");
   run<5>("full, 8 row threads (k0=104)");
+  run<6>("full, runtime k0=104 (8 row threads)", 104);
+  run<7>("full, static k0=0 (112 row threads)");
+  run<8>("full, runtime k0=0 (112 row threads)", 0);
+  run<6>("full, runtime k0=56 (56 row threads)", 56);
+  run<9>("diag block factor only, right-looking");
+  run<10>("full phase 1, right-looking diag");
   return 0;
 }

@@ -49,6 +49,23 @@ def run(n_log2=20, nin=1, passes=40):
     if s1[3] and s1[4]:
         ph["forward_solve_us"] = (s1[3] - st[7]) / 100.0
         ph["backward_solve_us"] = (s1[4] - s1[3]) / 100.0
+    # k_lm_pass phases of the last pass over all workgroups >= 2 (rows 0/1 are the solve's)
+    import numpy as np
+    lmd = be._lm_buffers()["desc"]
+    S = be.stamps[2:lmd.num_wgs].cpu().numpy().astype(np.int64)
+    t0 = S[:, 0].min()
+    gram = np.arange(2, 2 + len(S)) < lmd.gram_wgs
+    end = np.where(gram, S[:, 4], S[:, 2])
+    q = lambda v: [round(float(np.percentile(v, x)) / 100.0, 2) for x in (0, 50, 100)]
+    ph["pass_wg_us_min_med_max"] = {"start": q(S[:, 0] - t0), "prologue": q(S[:, 1] - S[:, 0]),
+                                     "paths_gram_wgs": q((S[:, 2] - S[:, 1])[gram]),
+                                     "paths_other_wgs": q((S[:, 2] - S[:, 1])[~gram]),
+                                     "j_build": q((S[:, 3] - S[:, 2])[gram]), "gram_mfma": q((S[:, 4] - S[:, 3])[gram]),
+                                     "end_gram_wgs": q((end - t0)[gram]), "end_other_wgs": q((end - t0)[~gram])}
+    wg = np.arange(2, 2 + len(S))
+    pth = (S[:, 2] - S[:, 1]) / 100.0
+    ph["pass_paths_us_by_group"] = {f"{'second' if b else 'first'}_half_xcd{x}": round(float(pth[(wg % 8 == x) & ((wg >= len(S) // 2) == b)].mean()), 2)
+                                    for b in (False, True) for x in range(8)}
     return {"n_log2": n_log2, "nin": nin, "passes": passes, "us_per_pass": 1000.0 * e0.elapsed_time(e1) / (passes + 1),
             **ph, "lm": be.lm_state()}
 
