@@ -468,8 +468,11 @@ struct CholWave {
       if constexpr (t < CT::NTILE) {
         constexpr int ib = CT::row(t), jb = CT::col(t);
         if (jb == bk && lr >= off && lr < off + 8) {
+          // rows >= PB are padding of the tile grid; row PB of the panel is the
+          // right-hand side, written by its own threads (rb): never from a tile
 #pragma unroll
-          for (int r = 0; r < 4; ++r) cn[lr - off][16 * ib + lq + 4 * r] = C[j][r];
+          for (int r = 0; r < 4; ++r)
+            if (16 * ib + lq + 4 * r < CT::PB) cn[lr - off][16 * ib + lq + 4 * r] = C[j][r];
         }
       }
     });
@@ -830,7 +833,11 @@ struct LmKernels {
   static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
   using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
   using S = NetShape<NIN, H, NO, HEAD>;
-  static int smem() { return (int)((LmSys<S::P>::ELEMS + 3 * S::P) * sizeof(double)); }
+  static constexpr int smem() { return (int)((LmSys<S::P>::ELEMS + 3 * S::P) * sizeof(double)); }
+  // the solve's dynamic LDS (system matrix + vectors) and its static panel
+  // buffers (colb, uL of lm_chol_solve_blocked) share the CU's 160 KB
+  static_assert(smem() + (8 + 9) * CholTiles<S::P>::RWX * (int)sizeof(double) + 64 <= 160 * 1024,
+                "LM solve exceeds the LDS of one workgroup");
 };
 
 static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {
@@ -949,8 +956,10 @@ extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p,
   X(2, 8, 2, HEAD_FREE)          \
   X(3, 8, 2, HEAD_FREE)          \
   X(4, 8, 2, HEAD_FREE)          \
-  X(5, 8, 6, HEAD_FREE)          \
-  X(6, 8, 7, HEAD_FREE)
+  X(5, 8, 6, HEAD_FREE)
+// (6, 8, 7) (P = 191) is not listed: its packed system matrix (147 KB) plus the
+// panel buffers exceed the 160 KB of LDS of the one-workgroup solve; such nets
+// fit with Adam (HipBackend.lm_supported() is False)
 
 // Geometry of the LM kernels for a shape: returns 0 and fills (P, R, NBLK,
 // two workgroups per CU) or -1 for shapes without an LM solver.
@@ -996,7 +1005,10 @@ extern "C" int rph_lm_solve(const TrainDesc* d, const LmDesc* lm, const double* 
     if (!attr) {                                                                                       \
       hipError_t e = hipFuncSetAttribute((const void*)k_lm_solve<K::S::P, K::S::R>,                   \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, bytes);           \
-      if (e != hipSuccess) return (int)e;                                                              \
+      if (e != hipSuccess) {                                                                           \
+        (void)hipGetLastError(); /* do not leave the error for the next runtime call */                \
+        return rph_report("rph_lm_solve", "dynamic LDS request refused");                              \
+      }                                                                                                \
       attr = true;                                                                                     \
     }                                                                                                  \
     hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(1), dim3(256), bytes, s, *d, *lm, red_new, pass); \

@@ -488,7 +488,7 @@ class HipBackend:
         def make():
             shp = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             if shp is None:
-                raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets only)")
+                raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets up to 174 parameters)")
             P, R, nblk, two = shp
             t = self.tcfg
             nw = int(max(1, min(512 if two else 256, self.n_local // 256)))

@@ -12,7 +12,7 @@ from test_lm_cpu import _teacher_problem
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(1, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (5, 8, 6, 0), (6, 8, 7, 0)]
+SHAPES = [(1, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (5, 8, 6, 0)]
 
 
 def _lm_row(q, h):
@@ -97,6 +97,9 @@ def test_lm_pass_block_matches_fp64(shape):
 
 @pytest.mark.parametrize("shape,damping", [((1, 8, 2, 0), "simple"), ((3, 8, 2, 0), "simple"),
                                            ((5, 8, 6, 0), "simple"), ((1, 8, 2, 0), "nielsen"),
+                                           # padded tile grids (16 NT > PB: P = 97, 114, 130)
+                                           ((1, 8, 1, 1), "simple"), ((2, 8, 2, 0), "simple"),
+                                           ((4, 8, 2, 0), "simple"),
                                            ((3, 8, 2, 0), "nielsen")])
 def test_lm_fit_matches_torch_and_is_deterministic(shape, damping):
     """HIP LM fit == fp64 torch reference (same accept / reject sequence and
@@ -131,6 +134,23 @@ def test_lm_fit_matches_torch_and_is_deterministic(shape, damping):
     # fp64 step difference, so they are not compared)
     np.testing.assert_allclose(np.minimum.accumulate(hist_g)[:8], np.minimum.accumulate(hist_c)[:8], rtol=2e-3)
     assert min(hist_g) == pytest.approx(min(hist_c), rel=2e-2)
+
+
+def test_lm_unsupported_shape_rejected_cleanly():
+    """The 6-asset net (P = 191) has no LM solver (its system does not fit one
+    workgroup's LDS): lm_supported() is False, an LM fit raises ValueError
+    before any launch, and the runtime is left without a pending HIP error."""
+    from rphedge.engine import FitConfig, HipBackend, TrainConfig
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 12
+    spec, feats, pr, y, data, w0 = _setup((6, 8, 7, 0), n, dev)
+    be = HipBackend(spec, n, TrainConfig(batch_size=n), device=dev)
+    assert not be.lm_supported()
+    with pytest.raises(ValueError):
+        be.fit(be.new_weights(w0), be.new_opt(), be.new_fit(), data,
+               FitConfig(epochs=2, optimizer="lm", early_stopping=False), seed=0)
+    torch.zeros(8, device=dev).sum().item()  # no stale error surfaces here
 
 
 def test_lm_induction_quality_on_gpu():
