@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256) void k_hedge_eval(const EvalDesc d) {
 // ---------------------------------------------------------------------------
 // Self-financing hedge P&L scan (PnlDesc, rph_types.h): one thread per path
 // (PPT paths per thread), dates in lockstep per workgroup so each date's
-// network(s) are staged once in LDS.  Wealth starts at V_0, holds the traded-
+// network(s) are staged once in LDS; the path inputs run one date ahead.  Wealth starts at V_0, holds the traded-
 // asset holdings of date t's network and keeps the remainder in the bank
 // account; P&L_T = W_T - liability.  Per-workgroup fp64 statistics in the
 // eval-stats layout (ES_V = W_T, ES_RES = P&L).  Not a hot path (one pass per
@@ -370,8 +370,10 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) s_cur[j][a] = d.price[a][pidx[j]];
   }
-  for (int t = 0; t < d.n_dates; ++t) {
-    float xr[PNL_PPT][NIN], s_nxt[PNL_PPT][NA > 0 ? NA : 1];
+  // date t's inputs are loaded one date ahead (software pipeline): their
+  // latency hides under date t-1's network evaluation
+  float xr[PNL_PPT][NIN], s_nxt[PNL_PPT][NA > 0 ? NA : 1];
+  auto load_date = [&](int t) {
 #pragma unroll
     for (int j = 0; j < PNL_PPT; ++j) {
 #pragma unroll
@@ -379,6 +381,18 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
 #pragma unroll
       for (int a = 0; a < NA; ++a) s_nxt[j][a] = d.price[a][(long long)(t + 1) * d.price_ts[a] + pidx[j]];
     }
+  };
+  if (d.n_dates > 0) load_date(0);
+  for (int t = 0; t < d.n_dates; ++t) {
+    float xc[PNL_PPT][NIN], sc_nxt[PNL_PPT][NA > 0 ? NA : 1];
+#pragma unroll
+    for (int j = 0; j < PNL_PPT; ++j) {
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) xc[j][f] = xr[j][f];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) sc_nxt[j][a] = s_nxt[j][a];
+    }
+    if (t + 1 < d.n_dates) load_date(t + 1);
     __syncthreads();  // every thread is done with date t-1's weights
     const NetWeights* wt = d.snap + (size_t)t * 2;
     for (int i = tid; i < S::P; i += 256) {
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
       const float* __restrict__ WB = (const float*)__builtin_assume_aligned(wl + WBOFF + (zo & ~3u), 16);
       float x[NIN];
 #pragma unroll
-      for (int f = 0; f < NIN; ++f) x[f] = (xr[j][f] - mu[f]) * isd[f];
+      for (int f = 0; f < NIN; ++f) x[f] = (xc[j][f] - mu[f]) * isd[f];
       float z1[H], a1[H], z2[H], a2[H], hold[NHOLD], hb[NHOLD];
       net_forward<NIN, H, NO, HEAD>(WA, x, d.alpha, z1, a1, z2, a2, hold);
       if (has_b) {
@@ -412,8 +426,8 @@ __global__ __launch_bounds__(256) void k_hedge_pnl(const PnlDesc d) {
       float w = wealth[j] * grow;
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
-        w = fmaf(hold[a], s_nxt[j][a] - s_cur[j][a] * grow, w);
-        s_cur[j][a] = s_nxt[j][a];
+        w = fmaf(hold[a], sc_nxt[j][a] - s_cur[j][a] * grow, w);
+        s_cur[j][a] = sc_nxt[j][a];
       }
       wealth[j] = w;
     }
