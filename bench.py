@@ -327,6 +327,7 @@ def main(argv=None):
                    "backend": run.backend_kind,
                    "step_schedule": run.backend.step_mode() if hasattr(run.backend, "step_mode") else "torch",
                    "dp_transport": (("gloo" if a.cpu else run.di.dp_mode) if world > 1 else None),
+                   "lm_dp_transport": (("gloo" if a.cpu else run.di.lm_dp_mode) if world > 1 and lm else None),
                    "dp_probe": probe, "dist_world": D.dist_world(),
                    "launch": "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1 else "single"},
         "quality": {"terminal_pnl_std": res.terminal_pnl["std"], "terminal_pnl_mean": res.terminal_pnl["mean"],

@@ -245,8 +245,10 @@ class HedgeRun:
             kw["mailbox"] = self.mailbox
             # LM fits / mean refits: the reduced [G | g | stats] block travels
             # over its own mailbox (k_lm_dp_exchange) with the xGMI transport
-            self.lm_mailbox = D.make_mailbox(self.di, L.LM_RED + L.LM_DP_WGS, tag="rph_lmbox")
+            self.lm_mailbox = D.make_mailbox(self.di, L.LM_RED + L.LM_DP_WGS, tag="rph_lmbox",
+                                             mode=self.di.lm_dp_mode)
             kw["lm_mailbox"] = self.lm_mailbox
+            kw["lm_comm"] = self.di.lm_comm
         self.backend = make_backend(self.backend_kind, self.spec, self.n_local, tcfg, device=self.device,
                                     comm=self.di.comm, world=self.di.world, rank=self.di.rank, stream=self.stream,
                                     **kw)

@@ -301,11 +301,12 @@ class HipBackend:
     name = "hip"
 
     def __init__(self, spec: NetSpec, n_local: int, tcfg: TrainConfig, device=None, comm=None,
-                 world: int = 1, rank: int = 0, stream=None, mailbox=None, lm_mailbox=None):
+                 world: int = 1, rank: int = 0, stream=None, mailbox=None, lm_mailbox=None, lm_comm=None):
         from .ops import native
 
         self.mailbox = mailbox  # native.IpcMailbox: fused xGMI all-reduce inside the step kernel
         self.lm_mailbox = lm_mailbox  # native.IpcMailbox (LM_RED + LM_DP_WGS pitch): LM block exchange
+        self._lm_nccl = lm_comm       # RCCL communicator of the LM block when its xGMI probe failed
         self.native = native
         native.load(required=True)
         self.spec, self.n_local, self.tcfg = spec, int(n_local), tcfg
@@ -1104,6 +1105,7 @@ def make_backend(kind: str, spec: NetSpec, n_local: int, tcfg: TrainConfig, **kw
     kw.pop("stream", None)
     kw.pop("mailbox", None)
     kw.pop("lm_mailbox", None)
+    kw.pop("lm_comm", None)
     return TorchBackend(spec, n_local, tcfg, **kw)
 
 

@@ -35,6 +35,8 @@ class DistInfo:
     comm: object = None          # native RCCL communicator (HIP path)
     initialized_here: bool = False
     dp_mode: str = "xgmi"        # xgmi: fused IPC all-reduce in the step kernel; rccl: RCCL + update kernel
+    lm_dp_mode: str = "xgmi"     # LM reduced block: xgmi (k_lm_dp_exchange over IPC mailboxes) or rccl
+    lm_comm: object = None       # RCCL communicator of the LM block when only its probe failed
     shared_device: bool = False  # several local ranks on ONE GPU (single-GPU rehearsal of the DP path)
     probe: dict | None = None    # select_transport's probe result (per-rank ok flags, chosen transport)
 
@@ -75,8 +77,8 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
     # exchange is the default only when every rank is local (one node, <= 8 GPUs)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     one_node = local_world == world
-    info = DistInfo(rank=rank, world=world, local_rank=local, device=dev,
-                    dp_mode=os.environ.get("RPH_DP", "xgmi" if (world <= 8 and one_node) else "rccl"))
+    mode = os.environ.get("RPH_DP", "xgmi" if (world <= 8 and one_node) else "rccl")
+    info = DistInfo(rank=rank, world=world, local_rank=local, device=dev, dp_mode=mode, lm_dp_mode=mode)
     if use_gpu:
         info.shared_device = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) > torch.cuda.device_count()
     if world > 1:
@@ -114,7 +116,7 @@ def _store():
 _MBOX_GEN = [0]  # mailboxes created by this process (every rank creates them in the same order)
 
 
-def make_mailbox(info: DistInfo, R: int, tag: str = "rph_mbox"):
+def make_mailbox(info: DistInfo, R: int, tag: str = "rph_mbox", mode: str | None = None):
     """IPC mailbox for the fused xGMI all-reduce (None on 1 rank / CPU / rccl mode).
 
     Collective: every rank calls it in the same order.  The store key carries
@@ -122,7 +124,7 @@ def make_mailbox(info: DistInfo, R: int, tag: str = "rph_mbox"):
     sweep, repeated API calls) never picks up a peer's handle from an earlier
     run; the barrier after the exchange means no rank closes (frees) an old
     mailbox a peer might still be opening."""
-    if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
+    if info.world <= 1 or info.device.type != "cuda" or (mode or info.dp_mode) != "xgmi":
         return None
     from ..ops.native import IpcMailbox
 
@@ -152,52 +154,55 @@ def close_mailbox(mb):
     mb.close()
 
 
-def _probe_xgmi_local(info: DistInfo, mb, lmb) -> tuple[bool, torch.Tensor | None]:
-    """This rank's half of the probe: two tiny data-parallel fits, one per
-    in-kernel exchange the runs use - Keras-Adam steps over the fused packet
-    exchange (``mb``, the lagged schedule) and Levenberg-Marquardt passes over
-    the reduced-block exchange (``lmb``, k_lm_dp_exchange, the default
-    optimiser).  Returns (ok, both fits' weights concatenated)."""
+def _probe_xgmi_local(info: DistInfo, mb, lmb, lm: bool) -> tuple[bool, torch.Tensor | None]:
+    """This rank's half of one probe: a tiny data-parallel fit over one of the
+    in-kernel exchanges the runs use - Keras-Adam steps over the fused packet
+    exchange (``mb``, the lagged schedule) or, with ``lm``, Levenberg-Marquardt
+    passes over the reduced-block exchange (``lmb``, k_lm_dp_exchange, the
+    bench's optimiser).  Returns (ok, fitted weights)."""
     from ..engine import DateData, FitConfig, HipBackend, TrainConfig
     from ..models.hedge_mlp import NetSpec, init_weights
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    if mb is None or (lm and lmb is None):
+        return False, None
     try:
         n = 1 << 12
         g = torch.Generator().manual_seed(100 + info.rank)          # different data per rank
         x = (torch.rand(n, generator=g) * 0.6 + 0.7).to(info.device)
         be = HipBackend(spec, n, TrainConfig(batch_size=n * info.world, chunk_log2=6, lm_gram_paths=2048),
-                        device=info.device, world=info.world, rank=info.rank, mailbox=mb, lm_mailbox=lmb)
+                        device=info.device, world=info.world, rank=info.rank, mailbox=mb,
+                        lm_mailbox=lmb if lm else None)
         data = DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=torch.relu(x - 1.0),
                         prices_now=[x])
-        outs = []
-        for fc in (FitConfig(epochs=4, patience=10 ** 6, early_stopping=False),
-                   FitConfig(epochs=3, optimizer="lm", early_stopping=False)):
-            w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
-            be.fit(w, o, f, data, fc, seed=5)
-            outs.append(w[: spec.nparams].double())
+        fc = (FitConfig(epochs=3, optimizer="lm", early_stopping=False) if lm else
+              FitConfig(epochs=4, patience=10 ** 6, early_stopping=False))
+        w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, fc, seed=5)
         torch.cuda.synchronize(info.device)
-        wv = torch.cat(outs)
-        clean = int(mb.error[0].item()) == 0 and int(lmb.error[0].item()) == 0
+        wv = w[: spec.nparams].double()
+        clean = int((lmb if lm else mb).error[0].item()) == 0
         return clean and bool(torch.isfinite(wv).all()), wv
     except Exception:
         return False, None
 
 
 def select_transport(info: DistInfo) -> str:
-    """Probe-then-choose, like a collective library's transport selection: keep
-    the in-kernel xGMI exchange when a tiny DP fit over it is clean on every
-    rank, otherwise fall back to an RCCL all-reduce of the packet (+ update
-    kernel).  Runs once, outside any timed region; all ranks agree.
+    """Probe-then-choose, like a collective library's transport selection,
+    separately for the two in-kernel exchanges: the Keras-Adam gradient packet
+    (``info.dp_mode``) and the LM reduced block (``info.lm_dp_mode``).  Each
+    keeps its xGMI mailbox exchange when a tiny DP fit over it is clean on
+    every rank and the replicas agree bit for bit; otherwise that exchange
+    falls back to an RCCL all-reduce.  Runs once, outside any timed region;
+    all ranks agree.
 
     Every rank issues the SAME collective sequence whatever its local outcome
-    (min of the ok flags, then max/min of the weights, then min of the
+    (per probe: min of the ok flags, max/min of the weights, min of the
     equality flag), so a failure seen by only some ranks cannot pair
     mismatched collectives."""
     if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
         return info.dp_mode
     from ..models.hedge_mlp import NetSpec
-
     from ..ops import layout as L
 
     def try_mailbox(R, tag):  # make_mailbox joins its barrier on every rank even when it raises
@@ -207,31 +212,40 @@ def select_transport(info: DistInfo) -> str:
             return None
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
-    P = 2 * spec.nparams
     mb = try_mailbox(spec.red_width, "rph_probe")
     lmb = try_mailbox(L.LM_RED + L.LM_DP_WGS, "rph_probe_lm")
-    ok_l, wv = _probe_xgmi_local(info, mb, lmb) if (mb is not None and lmb is not None) else (False, None)
-    ok = torch.tensor([1.0 if ok_l else 0.0], dtype=torch.float64, device=info.device)
-    all_reduce_(ok, "min")
-    w = wv if (wv is not None and wv.numel() == P) else torch.zeros(P, dtype=torch.float64, device=info.device)
-    mx, mn = w.clone(), w.clone()
-    all_reduce_(mx, "max")
-    all_reduce_(mn, "min")
-    same = torch.tensor([1.0 if bool(torch.equal(mx, mn)) else 0.0], dtype=torch.float64, device=info.device)
-    all_reduce_(same, "min")
+    probe = {}
+    for name, lm in (("packet", False), ("lm", True)):
+        ok_l, wv = _probe_xgmi_local(info, mb, lmb, lm)
+        ok = torch.tensor([1.0 if ok_l else 0.0], dtype=torch.float64, device=info.device)
+        all_reduce_(ok, "min")
+        w = wv if (wv is not None and wv.numel() == spec.nparams) else \
+            torch.zeros(spec.nparams, dtype=torch.float64, device=info.device)
+        mx, mn = w.clone(), w.clone()
+        all_reduce_(mx, "max")
+        all_reduce_(mn, "min")
+        same = torch.tensor([1.0 if bool(torch.equal(mx, mn)) else 0.0], dtype=torch.float64, device=info.device)
+        all_reduce_(same, "min")
+        all_ok = float(ok.item()) >= 1.0 and float(same.item()) >= 1.0
+        probe[name] = {"local_ok": bool(ok_l), "all_ok": bool(float(ok.item()) >= 1.0),
+                       "bitwise_equal_weights": bool(float(same.item()) >= 1.0),
+                       "chosen": "xgmi" if all_ok else "rccl"}
     for m in (mb, lmb):
         try:
             close_mailbox(m)
         except Exception:
             pass
-    all_ok = float(ok.item()) >= 1.0 and float(same.item()) >= 1.0
-    info.probe = {"local_ok": bool(ok_l), "all_ok": bool(float(ok.item()) >= 1.0),
-                  "bitwise_equal_weights": bool(float(same.item()) >= 1.0), "chosen": "xgmi" if all_ok else "rccl"}
-    if not all_ok:
-        from ..ops.native import NcclComm
+    info.probe = probe
+    info.lm_dp_mode = probe["lm"]["chosen"]
+    from ..ops.native import NcclComm
 
+    # fallback communicators are created here, collectively and outside any
+    # graph capture (never lazily inside a captured fit)
+    if probe["packet"]["chosen"] != "xgmi":
         info.dp_mode = "rccl"
         info.comm = NcclComm(info.rank, info.world, _store(), tag="rph_fallback")
+    elif info.lm_dp_mode != "xgmi":
+        info.lm_comm = NcclComm(info.rank, info.world, _store(), tag="rph_lm_fallback")
     return info.dp_mode
 
 
@@ -283,11 +297,12 @@ def shutdown():
     global _INFO
     import torch.distributed as dist
 
-    if _INFO is not None and _INFO.comm is not None:
-        try:
-            _INFO.comm.close()
-        except Exception:
-            pass
+    for c in ((_INFO.comm, _INFO.lm_comm) if _INFO is not None else ()):
+        if c is not None:
+            try:
+                c.close()
+            except Exception:
+                pass
     if _INFO is not None and _INFO.initialized_here and dist.is_initialized():
         dist.destroy_process_group()
     _INFO = None
