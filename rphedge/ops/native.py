@@ -19,10 +19,11 @@ import torch  # noqa: F401  (must be loaded before librphedge.so)
 
 from . import layout as L
 
-# RPH_NATIVE_LIB=debug|asan selects the variant built by `python -m rphedge.build --debug|--asan`
-_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / (
-    {"debug": "librphedge_debug.so", "asan": "librphedge_asan.so"}.get(os.environ.get("RPH_NATIVE_LIB", ""),
-                                                                       "librphedge.so"))
+# RPH_NATIVE_LIB=debug|asan selects the variant built by `python -m rphedge.build --debug|--asan`;
+# a path ending in .so loads that exact library (A/B of two builds, tools/ab_presets.sh)
+_LIB_ENV = os.environ.get("RPH_NATIVE_LIB", "")
+_LIB_PATH = Path(_LIB_ENV).resolve() if _LIB_ENV.endswith(".so") else Path(__file__).resolve().parent.parent / "_lib" / (
+    {"debug": "librphedge_debug.so", "asan": "librphedge_asan.so"}.get(_LIB_ENV, "librphedge.so"))
 _lib = None
 _load_error: str | None = None
 
@@ -205,6 +206,8 @@ def load(required: bool | None = None):
     if required is None:
         required = torch.cuda.is_available()
     try:
+        if _LIB_ENV.endswith(".so") and not _LIB_PATH.exists():
+            raise FileNotFoundError(f"RPH_NATIVE_LIB={_LIB_ENV} does not exist (it is never built implicitly)")
         if not _LIB_PATH.exists() or os.environ.get("RPH_REBUILD"):
             from .. import build as _build
 
