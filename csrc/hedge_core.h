@@ -13,8 +13,6 @@
 
 namespace rph {
 
-typedef float rph_f2 __attribute__((ext_vector_type(2)));
-
 // Diagnostic phase stamps (s_memrealtime, 100 MHz): thread 0 of every
 // workgroup writes stamp k to d.stamps[blockIdx.x * 8 + k] when d.stamps is set.
 #define RPH_STAMP(k)                                                                    \
@@ -102,49 +100,29 @@ RPH_INLINE void net_forward(const float* __restrict__ W, const float (&x)[NIN], 
                             const float* __restrict__ W2 = nullptr /* source of the W2 block (default W) */) {
   using S = NetShape<NIN, H, NO, HEAD>;
   if (W2 == nullptr) W2 = W;
-  // unit pairs (j, j + 1) on the packed fp32 FMA (v_pk_fma_f32, the input
-  // activation broadcast to both halves): the same per-unit FMA chain as the
-  // scalar form, bit for bit, at half the instructions
-  static_assert(H % 2 == 0, "hidden width must be even (packed unit pairs)");
 #pragma unroll
-  for (int j = 0; j < H; j += 2) {
-    rph_f2 acc = {W[S::OB1 + j], W[S::OB1 + j + 1]};
+  for (int j = 0; j < H; ++j) {
+    float acc = W[S::OB1 + j];
 #pragma unroll
-    for (int f = 0; f < NIN; ++f)
-      acc = __builtin_elementwise_fma(rph_f2{x[f], x[f]}, rph_f2{W[S::OW1 + f * H + j], W[S::OW1 + f * H + j + 1]}, acc);
-    z1[j] = acc[0];
-    z1[j + 1] = acc[1];
-    a1[j] = lrelu(acc[0], alpha);
-    a1[j + 1] = lrelu(acc[1], alpha);
+    for (int f = 0; f < NIN; ++f) acc = fmaf(x[f], W[S::OW1 + f * H + j], acc);
+    z1[j] = acc;
+    a1[j] = lrelu(acc, alpha);
   }
 #pragma unroll
-  for (int j = 0; j < H; j += 2) {
-    rph_f2 acc = {W[S::OB2 + j], W[S::OB2 + j + 1]};
+  for (int j = 0; j < H; ++j) {
+    float acc = W[S::OB2 + j];
 #pragma unroll
-    for (int i = 0; i < H; ++i)
-      acc = __builtin_elementwise_fma(rph_f2{a1[i], a1[i]}, rph_f2{W2[S::OW2 + i * H + j], W2[S::OW2 + i * H + j + 1]},
-                                      acc);
-    z2[j] = acc[0];
-    z2[j + 1] = acc[1];
-    a2[j] = lrelu(acc[0], alpha);
-    a2[j + 1] = lrelu(acc[1], alpha);
+    for (int i = 0; i < H; ++i) acc = fmaf(a1[i], W2[S::OW2 + i * H + j], acc);
+    z2[j] = acc;
+    a2[j] = lrelu(acc, alpha);
   }
   float o[NO];
 #pragma unroll
-  for (int k = 0; k + 1 < NO; k += 2) {
-    rph_f2 acc = {W[S::OB3 + k], W[S::OB3 + k + 1]};
+  for (int k = 0; k < NO; ++k) {
+    float acc = W[S::OB3 + k];
 #pragma unroll
-    for (int j = 0; j < H; ++j)
-      acc = __builtin_elementwise_fma(rph_f2{a2[j], a2[j]}, rph_f2{W[S::OW3 + j * NO + k], W[S::OW3 + j * NO + k + 1]},
-                                      acc);
-    o[k] = acc[0];
-    o[k + 1] = acc[1];
-  }
-  if (NO % 2) {
-    float acc = W[S::OB3 + NO - 1];
-#pragma unroll
-    for (int j = 0; j < H; ++j) acc = fmaf(a2[j], W[S::OW3 + j * NO + NO - 1], acc);
-    o[NO - 1] = acc;
+    for (int j = 0; j < H; ++j) acc = fmaf(a2[j], W[S::OW3 + j * NO + k], acc);
+    o[k] = acc;
   }
   if (HEAD == HEAD_COMPLEMENT) {  // EO: psi = 1 - phi  ("European Options.ipynb" cell 12)
     hold[0] = o[0];
