@@ -230,11 +230,16 @@ def select_transport(info: DistInfo) -> str:
         probe[name] = {"local_ok": bool(ok_l), "all_ok": bool(float(ok.item()) >= 1.0),
                        "bitwise_equal_weights": bool(float(same.item()) >= 1.0),
                        "chosen": "xgmi" if all_ok else "rccl"}
+    # collective teardown with ONE unconditional barrier (a rank whose mailbox
+    # creation failed holds None and must still join it)
+    torch.cuda.synchronize(info.device)
+    barrier()
     for m in (mb, lmb):
-        try:
-            close_mailbox(m)
-        except Exception:
-            pass
+        if m is not None:
+            try:
+                m.close()
+            except Exception:
+                pass
     info.probe = probe
     info.lm_dp_mode = probe["lm"]["chosen"]
     from ..ops.native import NcclComm
