@@ -635,12 +635,55 @@ RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsig
   RPH_STAMPB(12);
 }
 
+// Arrival of one k_lm_solve workgroup after it has read the shared solver
+// scalars (every thread's loads drained by the barrier, then one agent-scope
+// release add): every launch has exactly LM_SPEC workgroups and every one of
+// them arrives once, so the counter reaches a multiple of LM_SPEC at the end
+// of each launch.  Returns the ticket (thread 0; others 0).
+RPH_INLINE unsigned lm_arrive(double* st) {
+  __shared__ unsigned s_ticket;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_ticket = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(st + LMS_SYNC), 1u, __ATOMIC_RELEASE,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return s_ticket;
+}
+
+// Workgroup 0 waits until every workgroup of this launch has arrived (they
+// read the scalars it is about to overwrite).  Bounded: a timeout is
+// recorded as a large FAIL count and the solve proceeds.
+RPH_INLINE void lm_wait_all(double* st, unsigned ticket) {
+  if (threadIdx.x == 0) {
+    const unsigned target = (ticket / LM_SPEC + 1u) * LM_SPEC;
+    const unsigned* c = reinterpret_cast<const unsigned*>(st + LMS_SYNC);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS / 20) {
+        st[LMS_FAIL] += 1.0e6;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// Solve kernel, LM_SPEC workgroups.  Every workgroup takes the same
+// accept / reject decision from the same inputs.  Then:
+//  * final pass: workgroup 0 publishes the best point;
+//  * a rejection whose damping was precomputed (LMS_SPEC_IDX): workgroup 0
+//    publishes that step, no factorisation;
+//  * otherwise (accept, or no precomputed step): workgroup m factorises the
+//    system at the damping after m further consecutive rejections (m = 0 is
+//    this solve's own step) — the same arithmetic a later serial solve would
+//    do, so the results are bitwise those of one-solve-per-pass.
 template <int P, int R>
 __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDesc lm, const double* __restrict__ red_new,
                                                   const int pass) {
   using LS = LmShape<P>;
   constexpr int NB = LS::NB, NBLK = LS::NBLK;
-  constexpr int NG = NBLK * 1024;
   using SY = LmSys<P>;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* A = lds;                          // system matrix, lower triangle (LmSys layout)
@@ -648,9 +691,15 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   __shared__ int s_fail;
   __shared__ double s_diag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  RPH_STAMP(0);
+  const int m = blockIdx.x;
+#define RPH_STAMPS(k)               \
+  do {                              \
+    if (m == 0) RPH_STAMP(k);       \
+  } while (0)
+  RPH_STAMPS(0);
   double* st = lm.state;
   double* best_red = st + LMS_RED;  // the best point's reduced block
+  // ---- shared scalars (read once, before the arrival) -------------------------
   const int best_old = pass == 0 ? 1 : (int)st[LMS_BEST];
   const int trial = 1 - best_old;
   auto pkt = [&](int i) -> double {  // packet entries of the trial: [g (P) | loss, |e|, ape, count]
@@ -661,24 +710,20 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const double Lb = pass == 0 ? INFINITY : st[LMS_RED + LM_GBLK_MAX + LM_NPMAX + 4];
   const bool accept = pass == 0 || (Lt == Lt && Lt < Lb);
   double lam = st[LMS_LAM], nu = st[LMS_NU];
+  const double pred_prev = st[LMS_PRED];
+  const double nacc = st[LMS_NACC];
+  const int sidx = (int)st[LMS_SPEC_IDX];
   int best = best_old;
   if (accept) {
     best = trial;
     if (pass > 0 && lm.damping == 1) {
       // Nielsen: gain ratio of the actual to the model-predicted reduction
-      const double pred = st[LMS_PRED];
-      const double rho = pred > 0.0 ? (Lb - Lt) / pred : 1.0;
+      const double rho = pred_prev > 0.0 ? (Lb - Lt) / pred_prev : 1.0;
       const double t = 2.0 * rho - 1.0;
       lam = fmax(lam * fmax(1.0 / 3.0, 1.0 - t * t * t), (double)lm.lam_min);
       nu = 2.0;
     } else if (pass > 0) {
       lam = fmax(lam * lm.lam_down, (double)lm.lam_min);
-    }
-    // the best point's block := the trial's: read from red_new below, copied
-    // by the next pass kernel (LMS_COPY); the best loss is recorded now
-    if (tid == 0) {
-      best_red[LM_GBLK_MAX + LM_NPMAX + 4] = Lt;
-      st[LMS_NACC] += pass > 0 ? 1.0 : 0.0;
     }
   } else if (lm.damping == 1) {
     lam = fmin(lam * nu, (double)lm.lam_max);
@@ -686,13 +731,44 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   } else {
     lam = fmin(lam * lm.lam_up, (double)lm.lam_max);
   }
-  if (tid == 0) st[LMS_NU] = nu;
-  if (tid == 0 && pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
-  if (tid == 0) st[LMS_COPY] = accept ? 1.0 : 0.0;
-  RPH_STAMP(1);
+  const bool final_pass = pass == lm.passes;
+  // a rejection whose step the last full solve precomputed (same damping,
+  // same best point: rejections do not move it)
+  const bool spec = !final_pass && !accept && pass > 0 && sidx >= 1 && sidx < LM_SPEC && st[LMS_SPEC_LAM + sidx] == lam;
+  const int spec_ok = spec ? (st[LMS_SPEC_OK + sidx] != 0.0) : 0;
+  const double spec_pred = spec ? st[LMS_SPEC_PRED + sidx] : 0.0;
+  const unsigned ticket = lm_arrive(st);
+  // the damping of this workgroup's system: m further rejections
+  double lam_m = lam, nu_m = nu;
+  for (int k = 0; k < m; ++k) {
+    if (lm.damping == 1) {
+      lam_m = fmin(lam_m * nu_m, (double)lm.lam_max);
+      nu_m *= 2.0;
+    } else {
+      lam_m = fmin(lam_m * lm.lam_up, (double)lm.lam_max);
+    }
+  }
+  // bookkeeping of the decision (workgroup 0, after every workgroup read the scalars)
+  auto publish_decision = [&]() {
+    if (tid == 0) {
+      if (accept) {
+        // the best point's block := the trial's: read from red_new below, copied
+        // by the next pass kernel (LMS_COPY); the best loss is recorded now
+        best_red[LM_GBLK_MAX + LM_NPMAX + 4] = Lt;
+        st[LMS_NACC] = nacc + (pass > 0 ? 1.0 : 0.0);
+      }
+      st[LMS_NU] = nu;
+      if (pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
+      st[LMS_COPY] = accept ? 1.0 : 0.0;
+    }
+  };
+  RPH_STAMPS(1);
   const double* src = accept ? red_new : best_red;  // the best point's block
   const double* g = src + LM_GBLK_MAX;
-  if (pass == lm.passes) {  // final pass: publish the best point
+  if (final_pass) {  // publish the best point
+    if (m != 0) return;
+    lm_wait_all(st, ticket);
+    publish_decision();
     for (int i = tid; i < P; i += 256) {
       double wd = st[LMS_W + best * LM_NPMAX + i];
       if (i == lm.bias_index) {
@@ -700,7 +776,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
         // d = -g_i / (2 G_ii), G_ii from the diagonal 32x32 Gram block
         const int kb = i >> 5, ri = i & 31;
         int b = 0;
-        for (int m = 0; m < kb; ++m) b += LS::NB - m;
+        for (int q = 0; q < kb; ++q) b += LS::NB - q;
         const int q = (ri >> 3) * 4 + (ri & 3), hh = (ri >> 2) & 1;
         const double gii = src[(size_t)b * 1024 + q * 64 + hh * 32 + ri];
         if (gii > 0.0) wd -= g[i] / (2.0 * gii);
@@ -716,7 +792,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       const double* sb = src + LM_GBLK_MAX + LM_NPMAX;
       const double c = fmax(sb[3], 1.0);
       FitState* f = d.fit;
-      const double lbest = best_red[LM_GBLK_MAX + LM_NPMAX + 4];  // written above by this thread
+      const double lbest = accept ? Lt : Lb;
       f->best_loss = (float)lbest;
       f->last_loss = (float)lbest;
       f->last_mae = (float)(sb[1] / c);
@@ -731,6 +807,29 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
     return;
   }
+  if (spec) {  // rejection with a precomputed step: publish it
+    if (m != 0) return;
+    lm_wait_all(st, ticket);
+    publish_decision();
+    for (int i = tid; i < P; i += 256)
+      st[LMS_W + (1 - best) * LM_NPMAX + i] =
+          spec_ok ? st[LMS_SPEC_W + sidx * LM_NPMAX + i] : st[LMS_W + best * LM_NPMAX + i];
+    if (tid == 0) {
+      st[LMS_BEST] = (double)best;
+      if (spec_ok) {
+        st[LMS_LAM] = lam;
+        st[LMS_PRED] = spec_pred;
+        st[LMS_SPEC_IDX] = (double)(sidx + 1);
+      } else {  // not positive definite at this damping: as the serial solve's failure branch
+        st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
+        st[LMS_FAIL] += 1.0;
+        st[LMS_SPEC_IDX] = (double)LM_SPEC;
+      }
+    }
+    return;
+  }
+  // a precomputed step is used at the solve of pass + m (< passes): skip the rest
+  if (m > 0 && pass + m > lm.passes - 1) return;
   // ---- A = 2 G + lam diag(2 G) + ridge * mean diag, packed lower triangle -----
   // every block of this wave is loaded first (one round trip for the whole
   // Gram matrix, not one per block), then scattered into the LDS triangle
@@ -779,34 +878,21 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   double dmp = 0.0;  // this parameter's damping term lam 2G_ii + ridge (for the predicted reduction)
   if (tid < P) {
     double& a = A[SY::idx(tid, tid)];
-    dmp = a * lam + (double)lm.ridge * s_diag;
+    dmp = a * lam_m + (double)lm.ridge * s_diag;
     a = a + dmp;
     vec[tid] = -gi;
   }
-  RPH_STAMP(2);
+  RPH_STAMPS(2);
   __syncthreads();  // the damped diagonal is in place
   // blocked Cholesky (trailing update on the fp64 matrix cores) + one-wave
   // triangular solves; dense LDS storage up to 128 parameters, packed above
-  lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, d.stamps);
+  lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, m == 0 ? d.stamps : nullptr);
   __syncthreads();
-  if (s_fail) {
-    // not positive definite at this damping: re-evaluate the best point with
-    // more damping (trial := best)
-    for (int i = tid; i < P; i += 256) st[LMS_W + (1 - best) * LM_NPMAX + i] = st[LMS_W + best * LM_NPMAX + i];
-    if (tid == 0) {
-      st[LMS_BEST] = (double)best;
-      st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
-      st[LMS_FAIL] += 1.0;
-    }
-    return;
-  }
-  RPH_STAMP(4);
-  RPH_STAMP(5);
-  if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest + vec[tid];
+  const bool failed = s_fail != 0;
   // predicted reduction of the quadratic model at the step d:
   // -(g.d)/2 + d.(lam D + ridge) d / 2   ((2G + lam D + ridge) d = -g)
-  {
-    __shared__ double s_pred[4];
+  __shared__ double s_pred[4];
+  if (!failed) {
     double pv = 0.0;
     if (tid < P) {
       const double dv = vec[tid];
@@ -816,12 +902,41 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     for (int o = 32; o >= 1; o >>= 1) pv += __shfl_xor(pv, o, 64);
     if (lane == 0) s_pred[wid] = pv;
     __syncthreads();
-    if (tid == 0) st[LMS_PRED] = (s_pred[0] + s_pred[1]) + (s_pred[2] + s_pred[3]);
   }
+  const double pred = (s_pred[0] + s_pred[1]) + (s_pred[2] + s_pred[3]);
+  if (m > 0) {  // speculative step: its own slot of the state
+    if (tid < P) st[LMS_SPEC_W + m * LM_NPMAX + tid] = failed ? wbest : wbest + vec[tid];
+    if (tid == 0) {
+      st[LMS_SPEC_LAM + m] = lam_m;
+      st[LMS_SPEC_PRED + m] = failed ? 0.0 : pred;
+      st[LMS_SPEC_OK + m] = failed ? 0.0 : 1.0;
+    }
+    return;
+  }
+  lm_wait_all(st, ticket);
+  publish_decision();
+  RPH_STAMPS(4);
+  if (failed) {
+    // not positive definite at this damping: re-evaluate the best point with
+    // more damping (trial := best)
+    if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest;
+    if (tid == 0) {
+      st[LMS_BEST] = (double)best;
+      st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
+      st[LMS_FAIL] += 1.0;
+      st[LMS_SPEC_IDX] = (double)LM_SPEC;
+    }
+    return;
+  }
+  RPH_STAMPS(5);
+  if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest + vec[tid];
   if (tid == 0) {
+    st[LMS_PRED] = pred;
     st[LMS_BEST] = (double)best;
     st[LMS_LAM] = lam;
+    st[LMS_SPEC_IDX] = 1.0;
   }
+#undef RPH_STAMPS
 }
 
 // ---------------------------------------------------------------------------
@@ -1011,7 +1126,7 @@ extern "C" int rph_lm_solve(const TrainDesc* d, const LmDesc* lm, const double* 
       }                                                                                                \
       attr = true;                                                                                     \
     }                                                                                                  \
-    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(1), dim3(256), bytes, s, *d, *lm, red_new, pass); \
+    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(LM_SPEC), dim3(256), bytes, s, *d, *lm, red_new, pass); \
     return (int)hipGetLastError();                                                                     \
   }
   RPH_LM_SHAPES(X)

@@ -183,6 +183,10 @@ constexpr int LM_TILE = 64;          // Gram subsample paths per gram workgroup 
 //   g: gradient of mean((V - y)^2) [LM_NPMAX]; stats: loss sum, |e| sum, ape sum, count
 constexpr int LM_GBLK_MAX = 21 * 1024;
 constexpr int LM_RED = LM_GBLK_MAX + LM_NPMAX + 8;
+// k_lm_solve workgroups of a full solve: workgroup m factorises the system at
+// the damping that m consecutive rejections would reach, so a rejection's
+// solve only publishes a step computed ahead (speculative reject branch)
+constexpr int LM_SPEC = 4;
 // solver state (doubles)
 enum LmState : int {
   LMS_W = 0,                         // [2][LM_NPMAX] weights of the two slots (trial / best)
@@ -195,7 +199,13 @@ enum LmState : int {
                                      // reduced block into the best slot (deferred off the solve's path)
   LMS_NU,                            // Nielsen damping: growth factor of the next rejection
   LMS_PRED,                          // predicted loss reduction of the pending trial (quadratic model)
-  LMS_FLOATS = LMS_FAIL + 8
+  LMS_SPEC_IDX = LMS_FAIL + 8,       // next precomputed reject-branch step (>= LM_SPEC: none)
+  LMS_SYNC,                          // (uint32) arrival counter of k_lm_solve's workgroups
+  LMS_SPEC_LAM,                      // [LM_SPEC] damping of precomputed step m
+  LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC,  // [LM_SPEC] its predicted reduction
+  LMS_SPEC_OK = LMS_SPEC_PRED + LM_SPEC,   // [LM_SPEC] 1: positive definite (step valid)
+  LMS_SPEC_W = LMS_SPEC_OK + LM_SPEC,       // [LM_SPEC][LM_NPMAX] trial weights best + d_m
+  LMS_FLOATS = LMS_SPEC_W + LM_SPEC * LM_NPMAX
 };
 
 struct LmDesc {

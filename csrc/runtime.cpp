@@ -71,6 +71,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(LmDesc, passes), OFF(LmDesc, gram_blk), OFF(LmDesc, inv_ns), OFF(LmDesc, lam0), OFF(LmDesc, ridge), OFF(LmDesc, bias_index), OFF(LmDesc, weights_only), OFF(LmDesc, damping),
       (long long)sizeof(LmDpDesc), OFF(LmDpDesc, counter), OFF(LmDpDesc, world), OFF(LmDpDesc, pitch),
       (long long)LM_NPMAX, (long long)LM_RED, (long long)LMS_BEST, (long long)LMS_FLOATS,
+      (long long)LM_SPEC, (long long)LMS_SPEC_IDX, (long long)LMS_SPEC_W,
       // SimDesc
       (long long)sizeof(SimDesc), OFF(SimDesc, path_offset), OFF(SimDesc, sv1), OFF(SimDesc, dims1),
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),

@@ -74,4 +74,11 @@ LMS_COPY = LMS_BEST + 4
 LMS_NU = LMS_BEST + 5
 LMS_PRED = LMS_BEST + 6
 LM_DP_WGS = 16
-LMS_FLOATS = LMS_FAIL + 8
+LM_SPEC = 4
+LMS_SPEC_IDX = LMS_FAIL + 8
+LMS_SYNC = LMS_SPEC_IDX + 1
+LMS_SPEC_LAM = LMS_SYNC + 1
+LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC
+LMS_SPEC_OK = LMS_SPEC_PRED + LM_SPEC
+LMS_SPEC_W = LMS_SPEC_OK + LM_SPEC
+LMS_FLOATS = LMS_SPEC_W + LM_SPEC * LM_NPMAX

@@ -140,6 +140,7 @@ def _expected_layout() -> list[int]:
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
+        L.LM_SPEC, L.LMS_SPEC_IDX, L.LMS_SPEC_W,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
         S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset, S.sv_tscale.offset, S.scheme.offset,

@@ -1,0 +1,288 @@
+"""Direct tests of the Levenberg-Marquardt solve kernel (k_lm_solve,
+csrc/hedge_lm.hip): on a synthetic reduced block and solver state, one call
+must take the accept / reject decision, update the damping, and write the
+trial point theta + d with d the fp64 solution of
+
+    (2 G + lam' diag(2 G) + ridge * mean(diag(2 G)) I) d = -g
+
+for every supported parameter count (97, 106, 114, 122, 130, 174), on
+well-conditioned, ill-conditioned and rank-deficient Gram matrices; an
+indefinite system must take the failure branch (damping raised, FAIL counter
+bumped, trial := best).  The fit this replaces is the Keras fit of
+Replicating_Portfolio.py:211."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# (shape, P)
+SHAPES = [((1, 8, 1, 1), 97), ((1, 8, 2, 0), 106), ((2, 8, 2, 0), 114), ((3, 8, 2, 0), 122),
+          ((4, 8, 2, 0), 130), ((5, 8, 6, 0), 174)]
+
+
+def _lm_row(q, h):
+    return (q & 3) + 8 * (q >> 2) + 4 * h
+
+
+def encode_gram(G):
+    """Dense symmetric G -> upper-triangular 32x32 blocks in MFMA register order
+    (the layout k_lm_reduce writes; inverse of test_gpu_lm.decode_gram)."""
+    P = G.shape[0]
+    NP = (P + 31) // 32 * 32
+    NB = NP // 32
+    Gp = np.zeros((NP, NP))
+    Gp[:P, :P] = G
+    out = []
+    q = np.arange(16)[:, None]
+    lane = np.arange(64)[None, :]
+    for mb in range(NB):
+        for nb in range(mb, NB):
+            i = mb * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)
+            j = nb * 32 + (lane & 31)
+            out.append(Gp[i, j].reshape(-1))
+    return np.concatenate(out)
+
+
+def make_block(L, G, g, loss_mean, count=1000.0):
+    """Reduced LM block [G | g | stats] (layout of rph_types.h LM_RED)."""
+    red = np.zeros(L.LM_RED)
+    enc = encode_gram(G)
+    red[:enc.size] = enc
+    P = G.shape[0]
+    red[L.LM_GBLK_MAX:L.LM_GBLK_MAX + P] = g
+    s = L.LM_GBLK_MAX + L.LM_NPMAX
+    red[s:s + 4] = [loss_mean * count, 0.5, 0.25, count]
+    return red
+
+
+def gram(kind, P, rng):
+    if kind == "spd":
+        J = rng.standard_normal((4 * P, P)) * rng.uniform(0.2, 3.0, P)
+        return J.T @ J / (4 * P)
+    if kind == "illcond":
+        Q, _ = np.linalg.qr(rng.standard_normal((P, P)))
+        ev = np.logspace(0, -9, P)
+        return (Q * ev) @ Q.T
+    if kind == "rankdef":  # duplicated Jacobian columns: singular G, PD only through the damping
+        J = rng.standard_normal((3 * P, P - P // 2))
+        J = np.concatenate([J, J[:, : P // 2] * 0.5], axis=1)
+        return J.T @ J / (3 * P)
+    if kind == "indefinite":
+        G = np.diag(rng.uniform(1.0, 2.0, P))
+        G[3, 4] = G[4, 3] = 10.0 * np.sqrt(G[3, 3] * G[4, 4])
+        return G
+    raise ValueError(kind)
+
+
+def _backend(shape, dev, damping="simple"):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(*shape)
+    n = 1 << 12
+    feats = [torch.rand(n, device=dev) for _ in range(spec.nin)]
+    pr = [torch.rand(n, device=dev) + 0.5 for _ in range(spec.nhold - 1)]
+    data = DateData(feats=feats, prices_next=pr, bond_next=1.0, target=torch.rand(n, device=dev), prices_now=pr)
+    tc = TrainConfig(batch_size=n, lm_ridge=1e-10, lm_damping=damping)
+    be = HipBackend(spec, n, tc, device=dev)
+    w = be.new_weights(init_weights(spec, [0.5] * spec.nout, seed=1))
+    d = be._train_desc(w, be.new_opt(), be.new_fit(), data, FitConfig(optimizer="lm"), 0, None)
+    d.batch, d.steps_per_epoch, d.shuffle = n, 1, 0
+    b = be._lm_buffers()
+    b["desc"].passes = 4
+    return spec, be, d, b, tc
+
+
+def run_solve(L, be, d, b, *, P, best, w_best, w_trial, red_best, red_new, lam, pass_=1):
+    st = np.zeros(L.LMS_FLOATS)
+    st[L.LMS_W + best * L.LM_NPMAX:L.LMS_W + best * L.LM_NPMAX + P] = w_best
+    st[L.LMS_W + (1 - best) * L.LM_NPMAX:L.LMS_W + (1 - best) * L.LM_NPMAX + P] = w_trial
+    st[L.LMS_RED:L.LMS_RED + L.LM_RED] = red_best
+    s = L.LMS_RED + L.LM_GBLK_MAX + L.LM_NPMAX
+    st[s + 4] = red_best[L.LM_GBLK_MAX + L.LM_NPMAX] / red_best[L.LM_GBLK_MAX + L.LM_NPMAX + 3]  # best loss
+    st[L.LMS_BEST] = best
+    st[L.LMS_LAM] = lam
+    st[L.LMS_NU] = 2.0
+    b["state"].copy_(torch.from_numpy(st))
+    red = torch.from_numpy(red_new).to(b["red"].device)
+    be.native.lm_solve(d, b["desc"], red, pass_, None)
+    torch.cuda.synchronize()
+    return b["state"].cpu().numpy()
+
+
+def expected_step(G, g, lam, ridge):
+    A = 2.0 * G
+    dg = np.diag(A).copy()
+    dmp = dg * lam + ridge * dg.mean()
+    A = A + np.diag(dmp)
+    try:
+        np.linalg.cholesky(A)
+    except np.linalg.LinAlgError:
+        return None, None, A
+    dv = np.linalg.solve(A, -g)
+    pred = 0.5 * (np.sum(dmp * dv * dv) - g @ dv)
+    return dv, pred, A
+
+
+@pytest.mark.parametrize("shape,P", SHAPES)
+@pytest.mark.parametrize("kind", ["spd", "illcond", "rankdef"])
+@pytest.mark.parametrize("accept", [True, False])
+def test_lm_solve_step_matches_fp64(shape, P, kind, accept):
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    spec, be, d, b, tc = _backend(shape, dev)
+    assert spec.nparams == P
+    rng = np.random.default_rng(P * 7 + len(kind) + accept)
+    lm = b["desc"]
+    for it, lam in enumerate([1e-3, 0.7, 30.0]):
+        Gb, Gt = gram(kind, P, rng), gram(kind, P, rng)
+        gb, gt = rng.standard_normal(P) * 1e-2, rng.standard_normal(P) * 1e-2
+        Lb = 1.0e-4
+        Lt = Lb * (0.5 if accept else 2.0)
+        # small weights: trial - base then carries the step at full precision
+        w_best, w_trial = rng.standard_normal(P) * 2.0 ** -20, rng.standard_normal(P) * 2.0 ** -20
+        best = it % 2
+        st = run_solve(L, be, d, b, P=P, best=best, w_best=w_best, w_trial=w_trial,
+                       red_best=make_block(L, Gb, gb, Lb), red_new=make_block(L, Gt, gt, Lt), lam=lam)
+        if accept:
+            G, g, base = Gt, gt, w_trial
+            lam2, best2 = max(lam * lm.lam_down, lm.lam_min), 1 - best
+        else:
+            G, g, base = Gb, gb, w_best
+            lam2, best2 = min(lam * lm.lam_up, lm.lam_max), best
+        dv, pred, A = expected_step(G, g, lam2, tc.lm_ridge)
+        assert dv is not None
+        assert int(st[L.LMS_BEST]) == best2
+        assert st[L.LMS_LAM] == pytest.approx(lam2, rel=1e-15)
+        assert st[L.LMS_COPY] == (1.0 if accept else 0.0)
+        assert st[L.LMS_FAIL] == 0.0
+        tr = 1 - best2
+        got = st[L.LMS_W + tr * L.LM_NPMAX:L.LMS_W + tr * L.LM_NPMAX + P] - base
+        # backward stable: small residual of the computed step in the system it solves
+        res = np.linalg.norm(A @ got + g) / (np.linalg.norm(A, 2) * np.linalg.norm(got) + np.linalg.norm(g))
+        assert res < 1e-13, (lam, res)
+        # forward error within the conditioning of the damped system
+        cond = np.linalg.cond(A)
+        err = np.linalg.norm(got - dv) / np.linalg.norm(dv)
+        assert err < max(1e-9, 1e-14 * cond), (lam, err, cond)
+        assert st[L.LMS_PRED] == pytest.approx(pred, rel=max(1e-9, 1e-14 * cond))
+        # the best slot's weights are untouched
+        bw = st[L.LMS_W + best2 * L.LM_NPMAX:L.LMS_W + best2 * L.LM_NPMAX + P]
+        np.testing.assert_array_equal(bw, w_trial if accept else w_best)
+
+
+@pytest.mark.parametrize("shape,P", [SHAPES[0], SHAPES[1], SHAPES[5]])
+@pytest.mark.parametrize("accept", [True, False])
+def test_lm_solve_indefinite_takes_failure_branch(shape, P, accept):
+    """A system that is not positive definite at the new damping: no step,
+    trial := best, damping x lam_up^2 on top of the accept / reject update,
+    FAIL counter + 1."""
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    spec, be, d, b, tc = _backend(shape, dev)
+    rng = np.random.default_rng(11 + P)
+    lm = b["desc"]
+    G = gram("indefinite", P, rng)
+    g = rng.standard_normal(P)
+    lam = 1e-3
+    Lb = 1e-4
+    Lt = Lb * (0.5 if accept else 2.0)
+    w_best, w_trial = rng.standard_normal(P), rng.standard_normal(P)
+    best = 0
+    st = run_solve(L, be, d, b, P=P, best=best, w_best=w_best, w_trial=w_trial,
+                   red_best=make_block(L, G, g, Lb), red_new=make_block(L, G, g, Lt), lam=lam)
+    lam2 = max(lam * lm.lam_down, lm.lam_min) if accept else min(lam * lm.lam_up, lm.lam_max)
+    dv, _, _ = expected_step(G, g, lam2, tc.lm_ridge)
+    assert dv is None  # numpy agrees the damped system is indefinite
+    best2 = 1 - best if accept else best
+    assert st[L.LMS_FAIL] == 1.0
+    assert int(st[L.LMS_BEST]) == best2
+    assert st[L.LMS_LAM] == pytest.approx(min(lam2 * lm.lam_up * lm.lam_up, lm.lam_max), rel=1e-15)
+    keep = w_trial if accept else w_best
+    for slot in (0, 1):
+        np.testing.assert_array_equal(st[L.LMS_W + slot * L.LM_NPMAX:L.LMS_W + slot * L.LM_NPMAX + P], keep)
+
+
+@pytest.mark.parametrize("shape,P", [SHAPES[1], SHAPES[5]])
+@pytest.mark.parametrize("damping", ["simple", "nielsen"])
+def test_lm_solve_speculative_chain_is_bitwise_serial(shape, P, damping):
+    """A full solve also factorises the systems of the next LM_SPEC - 1
+    consecutive rejections (one workgroup each); the solves of those
+    rejections only publish the precomputed steps.  The trial sequence must be
+    bitwise the one-full-solve-per-pass sequence (LMS_SPEC_IDX invalidated
+    before every call), including a rejection chain longer than LM_SPEC - 1."""
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    spec, be, d, b, tc = _backend(shape, dev, damping)
+    b["desc"].passes = 8
+    rng = np.random.default_rng(3 + P)
+    G = gram("spd", P, rng)
+    Gt = gram("spd", P, rng)
+    g, gt = rng.standard_normal(P) * 1e-2, rng.standard_normal(P) * 1e-2
+    # pass 1 accepted (full solve), passes 2..6 rejected
+    losses = [0.5e-4] + [9e-4] * 5
+    runs = []
+    for serial in (False, True):
+        st0 = np.zeros(L.LMS_FLOATS)
+        st0[L.LMS_W:L.LMS_W + P] = rng.standard_normal(P) if not runs else runs[0]["w0"]
+        w0 = st0[L.LMS_W:L.LMS_W + P].copy()
+        st0[L.LMS_RED:L.LMS_RED + L.LM_RED] = make_block(L, G, g, 1e-4)
+        st0[L.LMS_RED + L.LM_GBLK_MAX + L.LM_NPMAX + 4] = 1e-4
+        st0[L.LMS_BEST] = 0
+        st0[L.LMS_LAM] = 1e-3
+        st0[L.LMS_NU] = 2.0
+        st0[L.LMS_PRED] = 1e-5
+        b["state"].copy_(torch.from_numpy(st0))
+        trials, lams, idx = [], [], []
+        for k, Lt in enumerate(losses):
+            if serial:
+                b["state"][L.LMS_SPEC_IDX] = float(L.LM_SPEC)
+            red = torch.from_numpy(make_block(L, Gt, gt, Lt)).to(dev)
+            be.native.lm_solve(d, b["desc"], red, k + 1, None)
+            torch.cuda.synchronize()
+            st = b["state"].cpu().numpy()
+            tr = 1 - int(st[L.LMS_BEST])
+            trials.append(st[L.LMS_W + tr * L.LM_NPMAX:L.LMS_W + tr * L.LM_NPMAX + P].copy())
+            lams.append(st[L.LMS_LAM])
+            idx.append(st[L.LMS_SPEC_IDX])
+            assert st[L.LMS_FAIL] == 0.0
+        runs.append(dict(w0=w0, trials=trials, lams=lams, idx=idx))
+    spec_run, ser = runs
+    # the speculative run used precomputed steps for rejections 1..3, then a full solve
+    assert spec_run["idx"][:5] == [1.0, 2.0, 3.0, 4.0, 1.0], spec_run["idx"]
+    for a_, b_ in zip(spec_run["trials"], ser["trials"]):
+        np.testing.assert_array_equal(a_, b_)
+    assert spec_run["lams"] == ser["lams"]
+
+
+def test_lm_solve_time_per_shape(capsys):
+    """Per-call time of the solve (eager launches, GPU-bound); printed for the
+    record (profiles/), asserted only loosely so a regression shows up."""
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    out = {}
+    for shape, P in SHAPES:
+        spec, be, d, b, tc = _backend(shape, dev)
+        rng = np.random.default_rng(5)
+        G = gram("spd", P, rng)
+        g = rng.standard_normal(P) * 1e-2
+        blk = make_block(L, G, g, 1e-4)
+        run_solve(L, be, d, b, P=P, best=0, w_best=np.zeros(P), w_trial=np.zeros(P),
+                  red_best=blk, red_new=make_block(L, G, g, 2e-4), lam=1e-3)
+        red = torch.from_numpy(make_block(L, G, g, 2e-4)).to(dev)
+        n = 400
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            be.native.lm_solve(d, b["desc"], red, 1, None)  # reject branch: one full solve per call
+        e1.record()
+        torch.cuda.synchronize()
+        out[P] = 1000.0 * e0.elapsed_time(e1) / n
+    with capsys.disabled():
+        print("\nk_lm_solve us/call:", {k: round(v, 2) for k, v in out.items()})
+    assert all(v < 200.0 for v in out.values()), out

@@ -1,0 +1,203 @@
+"""CPU laboratory for Levenberg-Marquardt variants of the hedge fits.
+
+Runs ``bench.py --cpu`` (torch backend, float64 LM oracle) with
+``TorchBackend._lm_fit`` replaced by a variant and prints one JSON line per
+variant: SF P&L std, residual std, V0 and the per-date acceptance counts.
+
+  python tools/lm_lab.py --variants base,stale --paths-log2 16
+
+Variants (combinable with '+'):
+  base    the HIP solver's sequence (csrc/hedge_lm.hip)
+  stale   pipelined factorisation: the accept branch steps with the PREVIOUS
+          best point's Gram matrix (factorised while the pass runs), the
+          reject branch is exact (its Gram is the best point's)
+  varpro  accept / reject on the loss projected over the (linear) output
+          layer: the exact output-layer minimiser is applied to every
+          evaluated point before the comparison
+"""
+from __future__ import annotations
+
+import argparse
+import io
+import json
+import os
+import sys
+from contextlib import redirect_stdout
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from rphedge import engine as E  # noqa: E402
+from rphedge.ops import layout as L  # noqa: E402
+from rphedge.models.hedge_mlp import torch_forward  # noqa: E402
+
+VARIANT = {"flags": set(), "log": []}
+
+
+def _out_slice(spec):
+    """Indices of the output layer (W3, b3) in the flat parameter vector."""
+    P = spec.nparams
+    n_out = spec.hidden * spec.nout + spec.nout
+    return list(range(P - n_out, P))
+
+
+def lab_lm_fit(self, wts, fit, data, fcfg):
+    from torch.func import jacrev, vmap
+
+    flags = VARIANT["flags"]
+    spec, t = self.spec, self.tcfg
+    P = spec.nparams
+    dt = torch.float64
+    X = E._normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
+    pr = torch.stack([p.to(dt) for p in data.prices_next] +
+                     [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
+    y = data.target.to(dt)
+    n_glob = float(self.n_local)
+    ns = max(L.LM_TILE, min(int(t.lm_gram_paths), self.n_local)) // L.LM_TILE * L.LM_TILE
+    blk, bstride = E.lm_gram_geometry(self.n_local, ns, 1)
+    sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
+
+    oi = torch.tensor(_out_slice(spec))
+
+    def v_one(w, x, p):
+        return (torch_forward(spec, w, x[None])[0] * p).sum()
+
+    def evaluate(w):
+        wg = w.detach().clone().requires_grad_(True)
+        e = (torch_forward(spec, wg, X) * pr).sum(1) - y
+        lsum = (e * e).sum()
+        (lsum / n_glob).backward()
+        J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X[sub], pr[sub])
+        G = (J.T @ J) / ns
+        if "varpro" in flags:
+            # output-layer Gram over EVERY path (the loss is exactly quadratic
+            # in the output layer): its features are a2 x (price combination)
+            with torch.no_grad():
+                Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X, pr)[:, oi]
+                G = G.clone()
+                G[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
+        return G, wg.grad.detach(), float(lsum) / n_glob
+
+    def project(w, G, g, Lv):
+        """Exact minimiser over the output layer (loss quadratic in it, Gram
+        from the subsample): w_o += -G_oo^-1 g_o / 2, loss and gradient
+        updated to first order."""
+        Goo = G[oi][:, oi]
+        try:
+            do = torch.linalg.solve(2.0 * Goo + 1e-9 * torch.eye(len(oi), dtype=dt) * Goo.diagonal().mean(), -g[oi])
+        except RuntimeError:
+            return w, g, Lv
+        w2 = w.clone()
+        w2[oi] += do
+        g2 = g + 2.0 * G[:, oi] @ do
+        L2 = Lv + 0.5 * float(g[oi] @ do)
+        return w2, g2, L2
+
+    def factor(G, lam):
+        A = 2.0 * G
+        dg = torch.diagonal(A).clone()
+        dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
+        Lc, info = torch.linalg.cholesky_ex(A + torch.diag(dmp))
+        return (Lc if int(info) == 0 else None), dmp
+
+    cur = int(wts[L.W_CUR].item())
+    w_best = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
+    prev = VARIANT.get("norm")
+    if "renorm" in flags and prev is not None and data.fmu:
+        # keep the warm start's function of the RAW features: x_new = (s - mu_n) isd_n
+        o = spec.offsets
+        W1 = w_best[o["W1"]:o["b1"]].view(spec.nin, spec.hidden)
+        b1 = w_best[o["b1"]:o["W2"]]
+        for f in range(spec.nin):
+            mo, io = prev[0][f], prev[1][f]
+            mn, inn = data.fmu[f], data.fisd[f]
+            b1 += W1[f] * io * (mn - mo)
+            W1[f] *= io / inn
+    VARIANT["norm"] = (tuple(data.fmu), tuple(data.fisd)) if data.fmu else None
+    kv = dict(f.split("=") for f in flags if "=" in f)
+    first = not VARIANT["log"]
+    lam = float(kv["lf"]) if (first and "lf" in kv) else float(t.lm_lam0)
+    if not first and "carry" in kv:
+        lam = max(VARIANT["lam_end"] * float(kv["carry"]), t.lm_lam_min)
+    G, g, Lb = evaluate(w_best)
+    if "varpro" in flags:
+        w_best, g, Lb = project(w_best, G, g, Lb)
+    hist = [Lb]
+    nacc = 0
+    stale = "stale" in flags
+    pend = None  # stale accept-branch factor (pipelined variant)
+    for k in range(1, int(fcfg.epochs) + 1):
+        if pend is not None:
+            Lc, pend = pend, None
+        else:
+            Lc, _ = factor(G, lam)
+        if Lc is None:
+            trial = w_best.clone()
+            lam = min(lam * t.lm_lam_up * t.lm_lam_up, t.lm_lam_max)
+        else:
+            trial = w_best + torch.cholesky_solve(-g[:, None], Lc)[:, 0]
+        Gt, gt, Lt = evaluate(trial)
+        if "varpro" in flags:
+            trial, gt, Lt = project(trial, Gt, gt, Lt)
+        hist.append(Lt)
+        if Lt == Lt and Lt < Lb:
+            nacc += 1
+            lam = max(lam * t.lm_lam_down, t.lm_lam_min)
+            if stale:
+                # factorised while this pass ran: the previous best Gram
+                pend, _ = factor(G, lam)
+            w_best, G, g, Lb = trial, Gt, gt, Lt
+        else:
+            lam = min(lam * t.lm_lam_up, t.lm_lam_max)
+    if os.environ.get("LAB_DEBUG"): print("HIST", json.dumps([float("%.4g" % h) for h in hist]), file=sys.stderr)
+    bi = E._lm_bias_index(spec, t)
+    if bi >= 0 and float(G[bi, bi]) > 0.0:
+        w_best = w_best.clone()
+        w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
+    w32 = w_best.to(torch.float32)
+    wts[:P] = w32
+    wts[L.PMAX:L.PMAX + P] = w32
+    wts[L.W_CUR] = 0.0
+    fit.zero_()
+    fit[L.F_WBEST:L.F_WBEST + P] = w32
+    fit[L.F_BEST] = Lb
+    fit[L.F_LAST_LOSS] = Lb
+    fit[L.F_EPOCH] = len(hist)
+    fit[L.F_STOPPED] = 1.0
+    fit[L.F_HASBEST] = 1.0
+    VARIANT["lam_end"] = lam
+    VARIANT["log"].append({"passes": len(hist) - 1, "acc": nacc, "L0": hist[0], "L": Lb, "lam": lam})
+
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="base")
+    ap.add_argument("--preset", default="euro30")
+    ap.add_argument("--paths-log2", type=int, default=16)
+    ap.add_argument("--extra", default="", help="extra bench.py args")
+    a = ap.parse_args()
+    import bench
+
+    for v in a.variants.split(","):
+        VARIANT["flags"] = set(v.split("+"))
+        VARIANT["log"] = []
+        VARIANT["norm"] = None
+        E.TorchBackend._lm_fit = lab_lm_fit
+        buf = io.StringIO()
+        argv = ["--cpu", "--preset", a.preset, "--paths-log2", str(a.paths_log2), "--steps", "1", "--warmup", "0"]
+        argv += a.extra.split()
+        with redirect_stdout(buf):
+            bench.main(argv)
+        res = json.loads(buf.getvalue().strip().splitlines()[-1])
+        q = res["quality"]
+        log = VARIANT["log"]
+        print(json.dumps({"variant": v, "extra": a.extra, "pnl_std": round(q["terminal_pnl_std"], 4),
+                          "resid_std": round(q["terminal_residual_std"], 4), "V0": round(q["V0"], 4),
+                          "first": log[0] if log else None,
+                          "acc_rest": sum(x["acc"] for x in log[1:]), "fits": len(log)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
