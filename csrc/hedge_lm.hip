@@ -425,6 +425,10 @@ RPH_INLINE void lm_static_for(F&& f) {
   lm_static_for(f, std::make_integer_sequence<int, N>{});
 }
 
+}  // namespace rph
+#include "lm_chol.h"
+namespace rph {
+
 // Trailing-matrix tiles of wave W (tile ownership is a compile-time function
 // of W, so every tile and fragment index is a static register index):
 // load from A, rank-8 update on the fp64 matrix cores, publish of the next
@@ -684,10 +688,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
                                                   const int pass) {
   using LS = LmShape<P>;
   constexpr int NB = LS::NB, NBLK = LS::NBLK;
-  using SY = LmSys<P>;
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* A = lds;                          // system matrix, lower triangle (LmSys layout)
-  double* vec = lds + SY::ELEMS;            // [P] rhs / solution, [P] pivots, [P] reciprocal pivots
   __shared__ int s_fail;
   __shared__ double s_diag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -830,6 +831,50 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   // a precomputed step is used at the solve of pass + m (< passes): skip the rest
   if (m > 0 && pass + m > lm.passes - 1) return;
+#ifndef RPH_LM_CHOL_V1
+  // ---- tile-store Cholesky (lm_chol.h): panel wave 0, owner waves 1..3 ------
+  using TG = TileGrid<P>;
+  double* T = lds;
+  double* vec = lds + TG::OFF_D;  // the solution d
+  unsigned* pub = reinterpret_cast<unsigned*>(lds + TG::OFF_FLAGS);
+  unsigned* fac = pub + TG::NT + 1;
+  static_assert(P <= 256, "one parameter per thread");
+  const double gi = tid < P ? g[tid] : 0.0;
+  const double wbest = tid < P ? st[LMS_W + best * LM_NPMAX + tid] : 0.0;  // for the final update
+  const double a_ii = tid < P ? 2.0 * lmc_gram<TG::NBG>(src, tid, tid) : 0.0;
+  if (wid == 0) {
+    double s = 0.0;
+    for (int i = lane; i < P; i += 64) s += 2.0 * lmc_gram<TG::NBG>(src, i, i);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) {
+      s_diag = s / P;
+      s_fail = 0;
+    }
+  }
+  if (tid < 2 * (TG::NT + 1)) pub[tid] = 0u;
+  __syncthreads();
+  double dmp = 0.0;  // this parameter's damping term lam 2G_ii + ridge (for the predicted reduction)
+  if (tid < P) {
+    dmp = a_ii * lam_m + (double)lm.ridge * s_diag;
+    lds[TG::OFF_DIAG + tid] = a_ii + dmp;
+  }
+  RPH_STAMPS(2);
+  __syncthreads();  // the damped diagonal is in place
+  switch (wid) {
+    case 0:
+      lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail);
+      lmc_backward<P>(T, lds + TG::OFF_RDG, vec);
+      break;
+    case 1: LmcOwner<P, 0>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+    case 2: LmcOwner<P, 1>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+    default: LmcOwner<P, 2>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+  }
+  __syncthreads();
+#else
+  using SY = LmSys<P>;
+  double* A = lds;                          // system matrix, lower triangle (LmSys layout)
+  double* vec = lds + SY::ELEMS;            // [P] rhs / solution, [P] pivots, [P] reciprocal pivots
   // ---- A = 2 G + lam diag(2 G) + ridge * mean diag, packed lower triangle -----
   // every block of this wave is loaded first (one round trip for the whole
   // Gram matrix, not one per block), then scattered into the LDS triangle
@@ -888,6 +933,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   // triangular solves; dense LDS storage up to 128 parameters, packed above
   lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, m == 0 ? d.stamps : nullptr);
   __syncthreads();
+#endif
   const bool failed = s_fail != 0;
   // predicted reduction of the quadratic model at the step d:
   // -(g.d)/2 + d.(lam D + ridge) d / 2   ((2G + lam D + ridge) d = -g)
@@ -948,11 +994,17 @@ struct LmKernels {
   static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
   using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
   using S = NetShape<NIN, H, NO, HEAD>;
+#ifndef RPH_LM_CHOL_V1
+  // the tile store + vectors + hand-off counters (lm_chol.h)
+  static constexpr int smem() { return TileGrid<S::P>::LDS_BYTES; }
+  static_assert(smem() + 128 <= 160 * 1024, "LM solve exceeds the LDS of one workgroup");
+#else
   static constexpr int smem() { return (int)((LmSys<S::P>::ELEMS + 3 * S::P) * sizeof(double)); }
   // the solve's dynamic LDS (system matrix + vectors) and its static panel
   // buffers (colb, uL of lm_chol_solve_blocked) share the CU's 160 KB
   static_assert(smem() + (8 + 9) * CholTiles<S::P>::RWX * (int)sizeof(double) + 64 <= 160 * 1024,
                 "LM solve exceeds the LDS of one workgroup");
+#endif
 };
 
 static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {

@@ -1,0 +1,298 @@
+// rphedge — fp64 Cholesky solve of the Levenberg-Marquardt system on ONE
+// workgroup of gfx950 (k_lm_solve): tile store + panel wave + owner waves.
+//
+// The augmented matrix M = [[A, .], [b^T, 1]] (A = 2G + damping, P x P; b = -g
+// as row P) is cut into 16 x 16 tiles (lower triangle, NT x NT tile grid
+// padded with identity rows).  Its Cholesky factor's last row is y = L^-1 b,
+// so the forward solve rides along; the backward solve L^T d = y follows.
+//
+//  * owner waves 1..3 keep every lower tile in fp64 MFMA accumulator
+//    registers (tile t -> wave 1 + t % 3, column-major order: the tiles still
+//    active at panel K are a suffix, so the owners stay balanced) and apply
+//    the rank-16 trailing update of panel K with v_mfma_f64_16x16x4_f64
+//    (4 per tile), the next panel's column block FIRST (look-ahead), which
+//    they publish to the LDS tile store before updating the rest;
+//  * the panel wave 0 takes each published 16-column panel (one or more rows
+//    per lane), factors it column by column (the pivot by v_readlane, its
+//    reciprocal square root from v_rsq_f64 + one Newton step, the column
+//    broadcast through LDS), writes L back to the store and signals.
+// Panel and owner waves hand off through LDS counters (workgroup-scope
+// release / acquire, bounded spins): no workgroup barrier inside the loop.
+// The store swizzles the columns of each tile row by 2 * (row >> 1), so the
+// owners' MFMA fragment reads (16 rows x 2 columns per half-wave) and the
+// panel wave's row reads (ds_read_b128) are free of bank conflicts.
+#pragma once
+#include "rph_common.h"
+
+namespace rph {
+
+typedef double lmc_d4 __attribute__((ext_vector_type(4)));
+
+template <int P>
+struct TileGrid {
+  static constexpr int PR = P + 1;              // rows: the system + the right-hand side
+  static constexpr int NT = (PR + 15) / 16;     // tile rows / columns
+  static constexpr int PT = 16 * NT;
+  static constexpr int NK = (P + 15) / 16;      // panels (columns < P are factored)
+  static constexpr int NTILE = NT * (NT + 1) / 2;
+  static constexpr int NSLOT = (PT + 63) / 64;  // panel rows per lane of the panel wave
+  static constexpr int NOWN = 3;                // owner waves
+  static constexpr int TPW = (NTILE + NOWN - 1) / NOWN;
+  static constexpr int NBG = (P + 31) / 32;     // 32 x 32 Gram blocks per row (k_lm_reduce layout)
+  // dynamic LDS (doubles): tile store | d [PT] | 1/L_kk [PT] | damped diagonal [PT] | column broadcast [16]
+  static constexpr int OFF_D = NTILE * 256;
+  static constexpr int OFF_RDG = OFF_D + PT;
+  static constexpr int OFF_DIAG = OFF_RDG + PT;
+  static constexpr int OFF_BC = OFF_DIAG + PT;
+  static constexpr int OFF_FLAGS = OFF_BC + 16;  // (as unsigned) pub[NT + 1], fac[NT + 1]
+  static constexpr int LDS_BYTES = OFF_FLAGS * 8 + 2 * (NT + 1) * 4 + 16;
+  // lower tile t (column-major) <-> (row block, column block)
+  static constexpr int tidx(int ib, int jb) { return jb * NT - jb * (jb - 1) / 2 + (ib - jb); }
+  static constexpr int tcol(int t) {
+    int b = 0;
+    while (t >= NT - b) t -= NT - b++;
+    return b;
+  }
+  static constexpr int trow(int t) {
+    int b = 0;
+    while (t >= NT - b) t -= NT - b++;
+    return b + t;
+  }
+};
+
+// element (r, c) of a tile -> double offset inside the tile
+RPH_INLINE int tg_off(int r, int c) { return r * 16 + (c ^ ((r >> 1) << 1)); }
+
+// fp64 reciprocal square root: v_rsq_f64 (rel. err 5.2e-8) + one Newton step
+RPH_INLINE double lmc_rsq(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return y * __builtin_fma(-0.5 * x * y, y, 1.5);
+}
+
+RPH_INLINE double lmc_readlane(double v, int l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// Gram entry G[i][j] (symmetric) from the reduced block: upper-triangular
+// 32 x 32 blocks in MFMA register order (k_lm_reduce / k_lm_pass layout)
+template <int NBG>
+RPH_INLINE double lmc_gram(const double* src, int i, int j) {
+  const int lo = i < j ? i : j, hi = i < j ? j : i;  // row lo, column hi of the upper triangle
+  const int mb = lo >> 5, nb = hi >> 5;
+  const int b = mb * NBG - (mb * (mb - 1)) / 2 + (nb - mb);
+  const int jj = lo & 31;
+  const int q = (jj & 3) + 4 * (jj >> 3), h = (jj >> 2) & 1;
+  return src[(size_t)b * 1024 + q * 64 + h * 32 + (hi & 31)];
+}
+
+RPH_INLINE void lmc_signal(unsigned* flag) {
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// bounded wait for *flag >= target (one wave); false on timeout
+RPH_INLINE bool lmc_wait(const unsigned* flag, unsigned target) {
+  for (unsigned it = 0; it < (1u << 24); ++it) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    __builtin_amdgcn_s_sleep(0);
+  }
+  return false;
+}
+
+// Owner wave O (0..2): its tiles are t = O + 3 j (compile-time), so every
+// register index is static.
+template <int P, int O>
+struct LmcOwner {
+  using TG = TileGrid<P>;
+  static constexpr int TPW = TG::TPW;
+
+  // initial tiles from the Gram block (x2), damped diagonal, rhs row, identity padding
+  RPH_INLINE static void load(lmc_d4* C, const double* src, const double* diag, const double* g, int lr, int lq) {
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = O + 3 * j;
+      if constexpr (t < TG::NTILE) {
+        constexpr int ib = TG::trow(t), jb = TG::tcol(t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * ib + lq + 4 * r, c = 16 * jb + lr;
+          double v = 0.0;
+          if (i < P && c < P) {
+            if (i == c) v = diag[i];
+            else if (c < i) v = 2.0 * lmc_gram<TG::NBG>(src, i, c);
+          } else if (i == P && c < P) {
+            v = -g[c];
+          } else if (i == c) {
+            v = 1.0;
+          }
+          C[j][r] = v;
+        }
+      }
+    });
+  }
+
+  // publish the tiles of column block jb (their current values) to the store
+  RPH_INLINE static void publish(const lmc_d4* C, double* T, int jbk, int lr, int lq) {
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = O + 3 * j;
+      if constexpr (t < TG::NTILE) {
+        constexpr int jb = TG::tcol(t);
+        if (jb == jbk) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) T[t * 256 + tg_off(lq + 4 * r, lr)] = C[j][r];
+        }
+      }
+    });
+  }
+
+  // C -= L(ib, K) L(jb, K)^T for the tiles with column block in [jlo, jhi]
+  RPH_INLINE static void update(lmc_d4* C, const double* T, int K, int jlo, int jhi, int lr, int lq) {
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = O + 3 * j;
+      if constexpr (t < TG::NTILE) {
+        constexpr int ib = TG::trow(t), jb = TG::tcol(t);
+        if (jb >= jlo && jb <= jhi) {
+          const double* Ta = T + TG::tidx(ib, K) * 256;
+          const double* Tb = T + TG::tidx(jb, K) * 256;
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int o = tg_off(lr, 4 * s + lq);
+            C[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ta[o], Tb[o], C[j], 0, 0, 0);
+          }
+        }
+      }
+    });
+  }
+
+  RPH_INLINE static void run(const double* src, const double* diag, const double* g, double* T, unsigned* pub,
+                             const unsigned* fac, int* s_fail) {
+    const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+    lmc_d4 C[TPW];
+    load(C, src, diag, g, lr, lq);
+    publish(C, T, 0, lr, lq);
+    lmc_signal(&pub[0]);
+    for (int K = 0; K + 1 < TG::NK; ++K) {
+      if (!lmc_wait(&fac[K], 1u)) {
+        *s_fail = 2;
+        return;
+      }
+      update(C, T, K, K + 1, K + 1, lr, lq);  // look-ahead: the next panel's column block
+      publish(C, T, K + 1, lr, lq);
+      lmc_signal(&pub[K + 1]);
+      update(C, T, K, K + 2, TG::NT - 1, lr, lq);
+    }
+  }
+};
+
+// Panel wave: factor the NK panels; L (lower, zero above the diagonal) to
+// the store, 1 / L_kk to rdg.
+template <int P>
+RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail) {
+  using TG = TileGrid<P>;
+  constexpr int NS = TG::NSLOT;
+  const int lane = threadIdx.x & 63;
+  bool ok = true;
+  for (int K = 0; K < TG::NK; ++K) {
+    if (!lmc_wait(&pub[K], 3u)) {
+      *s_fail = 2;
+      return;
+    }
+    const int nc = P - 16 * K < 16 ? P - 16 * K : 16;
+    double a[NS][16];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int row = 16 * K + lane + 64 * s;
+      if (row < TG::PT) {
+        const double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
+        const int sw = ((row & 15) >> 1) << 1;
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(tr + (c ^ sw));
+          a[s][c] = v.x;
+          a[s][c + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
+      }
+    }
+    double pnext = a[0][0];  // pivot candidate of the next column (valid in its lane)
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if (c < nc) {
+        const double piv = lmc_readlane(pnext, c);
+        ok = ok && piv > 0.0;
+        const double rl = lmc_rsq(piv);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) a[s][c] *= rl;
+        if (lane < 16) bc[lane] = a[0][c];
+        if (c + 1 < 16) pnext = __builtin_fma(-a[0][c], a[0][c], a[0][c + 1]);
+        if (lane == c) rdg[16 * K + c] = rl;
+#pragma unroll
+        for (int j = c + 1; j < 16; ++j) {
+          const double lj = bc[j];  // L[16K + j][16K + c] (LDS broadcast)
+#pragma unroll
+          for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
+        }
+      }
+    }
+    // write L back (the diagonal tile's upper triangle as zeros)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int row = 16 * K + lane + 64 * s;
+      if (row < TG::PT) {
+        double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
+        const int sw = ((row & 15) >> 1) << 1;
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) {
+          double2 v;
+          v.x = (s == 0 && c > lane) ? 0.0 : a[s][c];
+          v.y = (s == 0 && c + 1 > lane) ? 0.0 : a[s][c + 1];
+          *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
+        }
+      }
+    }
+    lmc_signal(&fac[K]);
+  }
+  if (!ok && lane == 0) *s_fail = 1;
+}
+
+// Backward solve L^T d = y (y = row P of L) by the panel wave, blocks of 16
+// columns from the last: z = y_K - sum_{i >= 16(K+1)} L[i][K-block] d_i (lane
+// = (column, row residue mod 4), reduced by shuffles), then the 16 x 16
+// triangular block by a readlane chain.  d -> dv[0, P).
+template <int P>
+RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv) {
+  using TG = TileGrid<P>;
+  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+  for (int K = TG::NK - 1; K >= 0; --K) {
+    const int col = 16 * K + c;
+    double z = 0.0;
+    for (int i = 16 * (K + 1) + q; i < P; i += 4)
+      z = __builtin_fma(T[TG::tidx(i >> 4, K) * 256 + tg_off(i & 15, c)], dv[i], z);
+    z += __shfl_xor(z, 16, 64);
+    z += __shfl_xor(z, 32, 64);
+    const double y = col < P ? T[TG::tidx(P >> 4, K) * 256 + tg_off(P & 15, c)] : 0.0;
+    z = y - z;
+    // column c of the diagonal tile: L[16K + j][16K + c], j = 0..15
+    double lc[16];
+    const double* td = T + TG::tidx(K, K) * 256;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) lc[j] = td[tg_off(j, c)];
+    const double rd = col < P ? rdg[col] : 0.0;
+    const int nc = P - 16 * K < 16 ? P - 16 * K : 16;
+    double dk = 0.0;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+      if (j < nc) {
+        const double dj = lmc_readlane(z * rd, j);  // d[16K + j] (final in lane j)
+        if (c == j) dk = dj;
+        z = __builtin_fma(-lc[j], dj, z);  // lanes c < j
+      }
+    }
+    if (q == 0 && col < P) dv[col] = dk;
+  }
+}
+
+}  // namespace rph

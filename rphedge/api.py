@@ -260,7 +260,7 @@ class HedgeRun:
                                lr=tr.lr, lr_rest=tr.lr_rest, lr_decay=tr.lr_decay,
                                q99=tr.q99, quantile=tr.quantile, cost_of_capital=tr.cost_of_capital,
                                shared_q99_model=pf.shared_q99_model,
-                               holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start,
+                               holdings_blend_sign_rp=pf.holdings_blend_sign_rp, warm_start=pf.warm_start, carry_optimizer=pf.carry_optimizer,
                                restore_best_at_end=pf.restore_best_at_end, keep_paths=c.keep_paths,
                                poll_every=tr.poll_every, seed=tr.seed,
                                feature_norm="none" if pf.raw_features else tr.feature_norm,

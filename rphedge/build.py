@@ -56,7 +56,8 @@ def _digest(extra: str) -> str:
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = False, debug: bool = False, asan: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, debug: bool = False, asan: bool = False,
+          defines: tuple = (), name: str | None = None) -> Path:
     """Compile csrc/ for gfx950.  ``asan`` builds a host-AddressSanitizer variant
     (``librphedge_asan.so``; device code is not instrumented — GPU ASan is not
     available on this pool) for host-side race/memory debugging."""
@@ -79,13 +80,17 @@ def build(force: bool = False, verbose: bool = False, debug: bool = False, asan:
     if asan:
         flags += ["-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
         lib, stamp = LIBDIR / "librphedge_asan.so", LIBDIR / "librphedge_asan.sha256"
+    if name:  # A/B variant: extra -D defines, rphedge/_lib/ab/librphedge_<name>.so (RPH_NATIVE_LIB=<path>)
+        flags += [f"-D{x}" for x in defines]
+        (LIBDIR / "ab").mkdir(exist_ok=True)
+        lib, stamp = LIBDIR / "ab" / f"librphedge_{name}.so", LIBDIR / "ab" / f"librphedge_{name}.sha256"
     digest = _digest(" ".join(flags) + repr(sorted(PER_FILE_FLAGS.items())))
     if not force and lib.exists() and stamp.exists() and stamp.read_text().strip() == digest:
         return lib
     tmp = lib.with_suffix(".so.tmp")
     # one hipcc per translation unit in parallel (the kernels are template-heavy),
     # then one link into the shared object
-    objdir = LIBDIR / ("obj_asan" if asan else "obj_debug" if debug else "obj")
+    objdir = LIBDIR / ("obj_asan" if asan else "obj_debug" if debug else f"obj_{name}" if name else "obj")
     objdir.mkdir(exist_ok=True)
     cflags = [f for f in flags if f not in ("-shared", "-lrccl") and not f.startswith("-L")]
     jobs = []
@@ -121,9 +126,12 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan", action="store_true", help="host AddressSanitizer variant")
+    ap.add_argument("--variant", default=None, help="A/B library name (with --define)")
+    ap.add_argument("--define", action="append", default=[], help="extra preprocessor define (A/B variant)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
-    lib = build(force=a.force, verbose=a.verbose, debug=a.debug, asan=a.asan)
+    lib = build(force=a.force, verbose=a.verbose, debug=a.debug, asan=a.asan, defines=tuple(a.define),
+                name=a.variant)
     print(lib)
     return 0
 

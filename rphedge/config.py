@@ -31,6 +31,7 @@ class ParityFlags:
     fine_terminal_payoff: bool = True   # payoff from the last FINE point even if the coarse grid misses it
     lr_schedule_first_only: bool = True  # Q17: LR schedule + patience 50 only on the first date
     warm_start: bool = True             # Q18: one network refit at every date (weights + Adam persist)
+    carry_optimizer: bool = True        # Q18: the Adam moments / step count persist across dates (False: reset per date)
     restore_best_at_end: bool = False   # Keras-2: restore best weights only on early stop
     numpy_binomial: bool = False        # Q20: numpy MT19937 reseeded 1234+t (CPU oracle only)
     local_residual_pnl: bool = False    # Q24: report the one-step residual as "the P&L at T" (reference);

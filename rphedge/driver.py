@@ -47,6 +47,7 @@ class InductionConfig:
     shared_q99_model: bool = False       # Q1
     holdings_blend_sign_rp: bool = False  # Q2
     warm_start: bool = True              # Q18
+    carry_optimizer: bool = True         # Q18: Adam state persists across dates
     restore_best_at_end: bool = False
     keep_paths: bool = True              # values / holdings / residual arrays
     poll_every: int = 0                  # host early-stop polling (0 = async)
@@ -206,6 +207,10 @@ class BackwardInduction:
         for t in self.ran:
             first = t == nc - 2
             data = self.date_data(t)
+            if not c.carry_optimizer and c.warm_start and not first:
+                self.opt_mse.copy_(self.opt_init)
+                if c.q99:
+                    self.opt_q.copy_(self.opt_init)
             if not c.warm_start and not first:
                 self.w_mse.copy_(self.w_init)
                 self.opt_mse.copy_(self.opt_init)

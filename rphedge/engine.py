@@ -128,6 +128,10 @@ class TrainConfig:
     # (free heads), so the fitted values' mean over all paths equals the
     # target's and no mean error drifts down the backward induction
     lm_bias_fix: bool = True
+    # run the data-parallel LM sequence (pass + reduce -> all-reduce of the
+    # reduced block -> solve, one launch each) even on one rank: the test hook
+    # that exercises the RCCL / mailbox exchange path at world size 1
+    lm_split: bool = False
     expose_packet: bool = False    # lagged fits: the finalize kernel writes the last step's summed (and
                                    # data-parallel exchanged) gradient packet to HipBackend.grad (tests)
     # optimizer-step schedule on the GPU:
@@ -185,6 +189,19 @@ def _lm_bias_index(spec, t) -> int:
     """LmDesc.bias_index: the bond holding's output bias (the last parameter of
     a free-head net), -1 for the complement head or with lm_bias_fix off."""
     return spec.nparams - 1 if (t.lm_bias_fix and spec.head == L.HEAD_FREE) else -1
+
+
+def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
+    """Workgroups of the LM pass kernel (HipBackend._lm_buffers; the torch
+    oracle derives its Gram subsample from the same number): 512 where two
+    pass workgroups fit per CU (1-3 input nets), else 256, at most one per
+    256 local paths."""
+    return int(max(1, min(512 if two_per_cu else 256, n_local // 256)))
+
+
+def lm_two_per_cu(spec) -> bool:
+    """csrc/hedge_lm.hip LmKernels::TWO for a net shape (no native library needed)."""
+    return spec.hidden == 8 and spec.nin <= 3 and spec.red_width <= 128
 
 
 def lm_gram_geometry(n_local: int, ns_local: int, world: int) -> tuple[int, int]:
@@ -492,7 +509,7 @@ class HipBackend:
                 raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets up to 174 parameters)")
             P, R, nblk, two = shp
             t = self.tcfg
-            nw = int(max(1, min(512 if two else 256, self.n_local // 256)))
+            nw = lm_pass_wgs(self.n_local, bool(two))
             ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // max(self.world, 1), self.n_local))
             gw = int(max(1, min(ns_local // L.LM_TILE, nw)))
             dev = self.device
@@ -529,7 +546,7 @@ class HipBackend:
         d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
         d.loss = L.LOSS_MSE
         n = self.native
-        if self.world <= 1:
+        if self.world <= 1 and not self.tcfg.lm_split:
             n.lm_fit(d, lm, b["red"], self.stream)
             return
         for k in range(lm.passes + 1):
@@ -559,20 +576,28 @@ class HipBackend:
             return
         if not self.lm_supported():
             # nets without an LM solver (32-unit MFMA family): the eval kernel's
-            # residual sum (res = target - prediction) gives the same step
-            st = self._cache.get(("refit_stats",), self.new_stats)
+            # residual sum (res = target - prediction) gives the same step.
+            # Every buffer is preallocated and every op writes into it (nothing
+            # is allocated inside a graph capture); data parallel, the two sums
+            # travel like an LM block: k_lm_dp_exchange over the LM mailbox
+            # (xGMI) or the RCCL communicator chosen by select_transport
+            c = self._cache.get(("refit",), self._refit_buffers)
+            st, red = c["stats"], c["red"]
+            G, S = L.LM_GBLK_MAX, L.LM_GBLK_MAX + L.LM_NPMAX
             self.eval(wts, data, st)
-            tot = st[:, [L.ES_RES, L.ES_COUNT]].sum(0)
+            torch.sum(st[:, L.ES_RES], dim=0, out=red[G])
+            torch.sum(st[:, L.ES_COUNT], dim=0, out=red[S])
             if self.world > 1:
                 if self.lm_mailbox is not None:
-                    import torch.distributed as dist
-
-                    dist.all_reduce(tot)
+                    x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
+                    self.native.lm_dp_exchange(x, red, 0, 1, self.stream)
                 else:
-                    self._lm_comm().allreduce_(tot, self.stream)
-            delta = (tot[0] / tot[1].clamp_min(1.0) / float(data.bond_next)).to(torch.float32)
-            wts[bi] += delta
-            fit[L.F_WBEST + bi] = wts[bi]
+                    self._lm_comm().allreduce_(red[G:S + 1], self.stream)
+            torch.clamp_min(red[S:S + 1], 1.0, out=c["cnt"])
+            torch.div(red[G:G + 1], c["cnt"], out=c["delta"])
+            c["delta"].mul_(1.0 / float(data.bond_next))
+            wts[bi:bi + 1].add_(c["delta"])
+            fit[L.F_WBEST + bi:L.F_WBEST + bi + 1].copy_(wts[bi:bi + 1])
             return
         b = self._lm_buffers()
 
@@ -596,16 +621,23 @@ class HipBackend:
         self._lm_allreduce(b["red"])
         n.lm_solve(d, lm, b["red"], 0, self.stream)
 
+    def _refit_buffers(self) -> dict:
+        dev = self.device
+        return {"stats": self.new_stats(), "red": torch.zeros(L.LM_RED, dtype=torch.float64, device=dev),
+                "cnt": torch.zeros(1, dtype=torch.float64, device=dev),
+                "delta": torch.zeros(1, dtype=torch.float64, device=dev)}
+
     def _lm_comm(self):
-        """Communicator for the LM reduced block: the backend's RCCL comm, or
-        one created on first use (collective: every rank runs the same fits)."""
+        """RCCL communicator of the LM reduced block: the one select_transport
+        created when the block's xGMI probe failed (``lm_comm``), else the
+        backend's RCCL communicator.  Never created lazily here (it could be
+        inside a graph capture)."""
+        if self._lm_nccl is not None:
+            return self._lm_nccl
         if self.comm is not None:
             return self.comm
-        if getattr(self, "_lm_nccl", None) is None:
-            from .parallel.dist import _store
-
-            self._lm_nccl = self.native.NcclComm(self.rank, self.world, _store(), tag="rph_lm")
-        return self._lm_nccl
+        raise RuntimeError("LM reduced-block exchange without an xGMI mailbox or an RCCL communicator: build "
+                           "data-parallel backends through rphedge.parallel.dist.select_transport (or pass lm_comm)")
 
     def lm_state(self) -> dict:
         """Host view of the last LM fit (accepted steps, Cholesky failures, damping)."""
@@ -786,7 +818,7 @@ class TorchBackend:
         y = data.target.to(dt)
         W = max(self.world, 1)
         n_glob = float(self.n_local * W)
-        nw = max(1, min(512, self.n_local // 256))
+        nw = lm_pass_wgs(self.n_local, lm_two_per_cu(spec))
         ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // W, self.n_local))
         gw = max(1, min(ns_local // L.LM_TILE, nw))
         ns = gw * L.LM_TILE

@@ -66,6 +66,10 @@ def init(backend: str | None = None, device: str | None = None, native_comm: boo
 
     import torch.distributed as dist
 
+    # the host driver supports dmabuf IPC only: the mailboxes' and RCCL's
+    # cross-process mappings need the non-legacy IPC mode, set before the HIP
+    # runtime initialises (external torchrun launches included)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     world = env_world()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -165,6 +169,13 @@ def _probe_xgmi_local(info: DistInfo, mb, lmb, lm: bool) -> tuple[bool, torch.Te
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
     if mb is None or (lm and lmb is None):
+        return False, None
+    # fault injection (tests): RPH_PROBE_FAIL = packet | lm | both fails that
+    # probe on every rank, or only on RPH_PROBE_FAIL_RANK
+    inj = os.environ.get("RPH_PROBE_FAIL", "")
+    inj_rank = os.environ.get("RPH_PROBE_FAIL_RANK")
+    if inj and (inj == "both" or inj == ("lm" if lm else "packet")) and (
+            inj_rank is None or int(inj_rank) == info.rank):
         return False, None
     try:
         n = 1 << 12
