@@ -125,6 +125,9 @@ def parse(argv=None):
     ap.add_argument("--lm-lam0", type=float, default=None)
     ap.add_argument("--lm-lam-up", type=float, default=None)
     ap.add_argument("--lm-lam-down", type=float, default=None)
+    ap.add_argument("--lm-stop-tol", type=float, default=None,
+                    help="later dates: adaptive LM pass budget (relative best-loss gain that ends a fit; 0: off)")
+    ap.add_argument("--lm-stop-min", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -142,7 +145,8 @@ def parse(argv=None):
     if a.optimizer is None:
         a.optimizer = pre.get("optimizer", "adam")
     for k, dflt in (("lm_passes_first", 80), ("lm_passes_rest", 3), ("lm_gram_paths", 4096),
-                    ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0)):
+                    ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0),
+                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -161,7 +165,8 @@ def build_run(a, world: int):
                         variant=a.variant, max_wgs=a.max_wgs, feature_norm=a.feature_norm,
                         optimizer=a.optimizer, lm_passes_first=a.lm_passes_first, lm_passes_rest=a.lm_passes_rest,
                         lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping, lm_lam0=a.lm_lam0,
-                        lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down)
+                        lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down, lm_stop_tol=a.lm_stop_tol,
+                        lm_stop_min=a.lm_stop_min)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -343,6 +348,8 @@ def main(argv=None):
     # full passes over the paths per run: Adam epochs, or LM evaluations (start point + trials)
     passes = (a.lm_passes_first + 1 + (n_dates - 1) * (a.lm_passes_rest + 1)) if lm else \
         (a.epochs_first + (n_dates - 1) * a.epochs_rest)
+    if lm and lm_stats and a.lm_stop_tol > 0:  # adaptive budget: the evaluations actually run
+        passes = sum(p + 1 for p in lm_stats["passes_per_date"])
     path_samples = float(n_total) * passes / (ms / 1000.0)
     value = float(n_total) / (ms / 1000.0)
     out = {
@@ -378,6 +385,7 @@ def main(argv=None):
                    "lm_gram_paths": a.lm_gram_paths if lm else None,
                    "lm_damping": a.lm_damping if lm else None,
                    "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
+                   "lm_stop": [a.lm_stop_tol, a.lm_stop_min] if (lm and a.lm_stop_tol > 0) else None,
                    "steps_per_epoch": None if lm else run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,
                    "step_schedule": None if lm else (run.backend.step_mode() if hasattr(run.backend, "step_mode")

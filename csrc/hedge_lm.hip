@@ -84,9 +84,10 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   } while (0)
   RPH_STAMPP(0);
   double* st = lm.state;
+  double* sl = st + LMS_SLOTS + LM_SLOT * (pass & 1);  // this pass's scalars (written by the last solve)
   // trial point: pass 0 = the start point (canonical weights, published as
   // slot 0); later passes = the slot k_lm_solve wrote
-  const int trial = pass == 0 ? 0 : 1 - (int)st[LMS_BEST];
+  const int trial = pass == 0 ? 0 : 1 - (int)sl[LSS_BEST];
   const Perm perm = make_perm(1u, 0u, 0u, false);
   typename B::Pre pre;
   B::load(d, 0, perm, B::first(wid), lane, pre);
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     wl[i] = w;
     if (pass == 0 && blockIdx.x == 0) st[LMS_W + i] = (double)w;
   }
-  if (pass > 0 && st[LMS_COPY] != 0.0) {
+  if (pass > 0 && sl[LSS_COPY] != 0.0) {
     // the previous solve accepted its trial: best block := that trial's
     // reduced block (G, g, stats), spread over the grid; red_new is rewritten
     // only by this pass's reduce kernel, which runs after this one
@@ -106,10 +107,16 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
       best_red[o] = red_new[o];
     }
   }
+  if (pass > 0 && sl[LSS_STOP] != 0.0) return;  // adaptive budget spent: nothing to evaluate
   if (pass == 0 && blockIdx.x == 0 && tid == 0) {
-    st[LMS_BEST] = 1.0;
-    st[LMS_LAM] = lm.lam0;
-    st[LMS_NU] = 2.0;
+    sl[LSS_BEST] = 1.0;
+    sl[LSS_LAM] = lm.lam0;
+    sl[LSS_NU] = 2.0;
+    sl[LSS_PRED] = 0.0;
+    sl[LSS_COPY] = 0.0;
+    sl[LSS_SPEC_IDX] = (double)LM_SPEC;
+    sl[LSS_LBEST] = INFINITY;
+    sl[LSS_STOP] = 0.0;
     st[LMS_NACC] = 0.0;
     st[LMS_FAIL] = 0.0;
   }
@@ -203,10 +210,11 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 // Reduce kernel: red[e] = fixed-order sums of the slabs.
 // ---------------------------------------------------------------------------
 template <int P, int R>
-__global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __restrict__ red) {
+__global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
   using LS = LmShape<P>;
   constexpr int NG = LS::NBLK * 1024;
   __shared__ double part[256];
+  if (pass > 0 && lm.state[LMS_SLOTS + LM_SLOT * (pass & 1) + LSS_STOP] != 0.0) return;
   if ((int)blockIdx.x < NG / 64) {
     // Gram: workgroup handles entries [64 b, 64 b + 64), thread (g, l) sums
     // the slabs g, g + 4, ... of entry 64 b + l (16 loads in flight per
@@ -639,45 +647,12 @@ RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsig
   RPH_STAMPB(12);
 }
 
-// Arrival of one k_lm_solve workgroup after it has read the shared solver
-// scalars (every thread's loads drained by the barrier, then one agent-scope
-// release add): every launch has exactly LM_SPEC workgroups and every one of
-// them arrives once, so the counter reaches a multiple of LM_SPEC at the end
-// of each launch.  Returns the ticket (thread 0; others 0).
-RPH_INLINE unsigned lm_arrive(double* st) {
-  __shared__ unsigned s_ticket;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_ticket = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(st + LMS_SYNC), 1u, __ATOMIC_RELEASE,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  return s_ticket;
-}
-
-// Workgroup 0 waits until every workgroup of this launch has arrived (they
-// read the scalars it is about to overwrite).  Bounded: a timeout is
-// recorded as a large FAIL count and the solve proceeds.
-RPH_INLINE void lm_wait_all(double* st, unsigned ticket) {
-  if (threadIdx.x == 0) {
-    const unsigned target = (ticket / LM_SPEC + 1u) * LM_SPEC;
-    const unsigned* c = reinterpret_cast<const unsigned*>(st + LMS_SYNC);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS / 20) {
-        st[LMS_FAIL] += 1.0e6;
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
 // Solve kernel, LM_SPEC workgroups.  Every workgroup takes the same
-// accept / reject decision from the same inputs.  Then:
+// accept / reject decision from the same inputs (the scalar slot of this
+// pass's parity, which no workgroup of this launch writes: workgroup 0
+// writes the other slot).  Then:
 //  * final pass: workgroup 0 publishes the best point;
-//  * a rejection whose damping was precomputed (LMS_SPEC_IDX): workgroup 0
+//  * a rejection whose damping was precomputed (LSS_SPEC_IDX): workgroup 0
 //    publishes that step, no factorisation;
 //  * otherwise (accept, or no precomputed step): workgroup m factorises the
 //    system at the damping after m further consecutive rejections (m = 0 is
@@ -686,6 +661,9 @@ RPH_INLINE void lm_wait_all(double* st, unsigned ticket) {
 template <int P, int R>
 __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDesc lm, const double* __restrict__ red_new,
                                                   const int pass) {
+  // no implicit fma contraction: every workgroup (own step or a speculative
+  // one) must round identically, whatever code copy the compiler makes
+#pragma clang fp contract(off)
   using LS = LmShape<P>;
   constexpr int NB = LS::NB, NBLK = LS::NBLK;
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -700,22 +678,26 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   RPH_STAMPS(0);
   double* st = lm.state;
   double* best_red = st + LMS_RED;  // the best point's reduced block
-  // ---- shared scalars (read once, before the arrival) -------------------------
-  const int best_old = pass == 0 ? 1 : (int)st[LMS_BEST];
+  const double* sin = st + LMS_SLOTS + LM_SLOT * (pass & 1);  // read by every workgroup
+  double* sout = st + LMS_SLOTS + LM_SLOT * ((pass + 1) & 1);  // written by workgroup 0
+  // ---- scalars of this pass ------------------------------------------------------
+  const int best_old = pass == 0 ? 1 : (int)sin[LSS_BEST];
   const int trial = 1 - best_old;
   auto pkt = [&](int i) -> double {  // packet entries of the trial: [g (P) | loss, |e|, ape, count]
     return i < P ? red_new[LM_GBLK_MAX + i] : red_new[LM_GBLK_MAX + LM_NPMAX + i - P];
   };
   const double cnt = pkt(P + 3);
   const double Lt = pkt(P + 0) / fmax(cnt, 1.0);
-  const double Lb = pass == 0 ? INFINITY : st[LMS_RED + LM_GBLK_MAX + LM_NPMAX + 4];
-  const bool accept = pass == 0 || (Lt == Lt && Lt < Lb);
-  double lam = st[LMS_LAM], nu = st[LMS_NU];
-  const double pred_prev = st[LMS_PRED];
-  const double nacc = st[LMS_NACC];
-  const int sidx = (int)st[LMS_SPEC_IDX];
+  const double Lb = pass == 0 ? INFINITY : sin[LSS_LBEST];
+  // adaptive budget spent at an earlier solve: the trial block is stale
+  const bool stopped = pass > 0 && sin[LSS_STOP] != 0.0;
+  const bool accept = !stopped && (pass == 0 || (Lt == Lt && Lt < Lb));
+  double lam = sin[LSS_LAM], nu = sin[LSS_NU];
+  const double pred_prev = sin[LSS_PRED];
+  const int sidx = (int)sin[LSS_SPEC_IDX];
   int best = best_old;
-  if (accept) {
+  if (stopped) {
+  } else if (accept) {
     best = trial;
     if (pass > 0 && lm.damping == 1) {
       // Nielsen: gain ratio of the actual to the model-predicted reduction
@@ -738,7 +720,6 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const bool spec = !final_pass && !accept && pass > 0 && sidx >= 1 && sidx < LM_SPEC && st[LMS_SPEC_LAM + sidx] == lam;
   const int spec_ok = spec ? (st[LMS_SPEC_OK + sidx] != 0.0) : 0;
   const double spec_pred = spec ? st[LMS_SPEC_PRED + sidx] : 0.0;
-  const unsigned ticket = lm_arrive(st);
   // the damping of this workgroup's system: m further rejections
   double lam_m = lam, nu_m = nu;
   for (int k = 0; k < m; ++k) {
@@ -749,27 +730,45 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       lam_m = fmin(lam_m * lm.lam_up, (double)lm.lam_max);
     }
   }
-  // bookkeeping of the decision (workgroup 0, after every workgroup read the scalars)
-  auto publish_decision = [&]() {
+  // the next pass's scalars (workgroup 0, thread 0): best slot, damping, growth
+  // factor, predicted reduction, copy flag (the best point's block := the
+  // trial's, copied by the next pass kernel), next precomputed step, best loss
+  auto publish = [&](double lam_out, double pred_out, double sidx_out) {
     if (tid == 0) {
-      if (accept) {
-        // the best point's block := the trial's: read from red_new below, copied
-        // by the next pass kernel (LMS_COPY); the best loss is recorded now
-        best_red[LM_GBLK_MAX + LM_NPMAX + 4] = Lt;
-        st[LMS_NACC] = nacc + (pass > 0 ? 1.0 : 0.0);
-      }
-      st[LMS_NU] = nu;
+      // adaptive budget: this pass lowered the best loss by less than stop_tol
+      const double lnew = accept ? Lt : Lb;
+      const bool stop_now = lm.stop_tol > 0.f && pass >= lm.stop_min && !(Lb - lnew > (double)lm.stop_tol * lnew);
+      sout[LSS_STOP] = stop_now ? (double)pass : 0.0;
+      sout[LSS_BEST] = (double)best;
+      sout[LSS_LAM] = lam_out;
+      sout[LSS_NU] = nu;
+      sout[LSS_PRED] = pred_out;
+      sout[LSS_COPY] = accept ? 1.0 : 0.0;
+      sout[LSS_SPEC_IDX] = sidx_out;
+      sout[LSS_LBEST] = accept ? Lt : Lb;
+      st[LMS_BEST] = (double)best;  // host mirrors
+      st[LMS_LAM] = lam_out;
+      if (accept && pass > 0) st[LMS_NACC] += 1.0;
       if (pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
-      st[LMS_COPY] = accept ? 1.0 : 0.0;
     }
   };
+  if (stopped && !final_pass) {  // carry the scalars to the next pass (no copy of the stale block)
+    if (m == 0 && tid < LM_SLOT) sout[tid] = tid == LSS_COPY ? 0.0 : sin[tid];
+    return;
+  }
   RPH_STAMPS(1);
   const double* src = accept ? red_new : best_red;  // the best point's block
   const double* g = src + LM_GBLK_MAX;
   if (final_pass) {  // publish the best point
     if (m != 0) return;
-    lm_wait_all(st, ticket);
-    publish_decision();
+    if (stopped) {
+      if (tid == 0) {
+        st[LMS_BEST] = (double)best;
+        st[LMS_LAM] = lam;
+      }
+    } else {
+      publish(lam, pred_prev, (double)LM_SPEC);
+    }
     for (int i = tid; i < P; i += 256) {
       double wd = st[LMS_W + best * LM_NPMAX + i];
       if (i == lm.bias_index) {
@@ -786,10 +785,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       d.wts->w[0][i] = w;
       d.fit->w_best[i] = w;
     }
-    if (tid == 0 && lm.weights_only) {
-      st[LMS_BEST] = (double)best;
-      st[LMS_LAM] = lam;
-    } else if (tid == 0) {
+    if (tid == 0 && !lm.weights_only) {
       const double* sb = src + LM_GBLK_MAX + LM_NPMAX;
       const double c = fmax(sb[3], 1.0);
       FitState* f = d.fit;
@@ -798,34 +794,24 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       f->last_loss = (float)lbest;
       f->last_mae = (float)(sb[1] / c);
       f->last_mape = (float)(100.0 * sb[2] / c);
-      f->epoch = (float)(pass + 1);
+      f->epoch = (float)((stopped ? (int)sin[LSS_STOP] : pass) + 1);  // points evaluated
       f->stopped = 1.f;
       f->has_best = 1.f;
       f->wait = 0.f;
       f->loss_sum = f->abs_sum = f->ape_sum = f->loss_cnt = 0.f;
-      st[LMS_BEST] = (double)best;
-      st[LMS_LAM] = lam;
     }
     return;
   }
   if (spec) {  // rejection with a precomputed step: publish it
     if (m != 0) return;
-    lm_wait_all(st, ticket);
-    publish_decision();
     for (int i = tid; i < P; i += 256)
       st[LMS_W + (1 - best) * LM_NPMAX + i] =
           spec_ok ? st[LMS_SPEC_W + sidx * LM_NPMAX + i] : st[LMS_W + best * LM_NPMAX + i];
-    if (tid == 0) {
-      st[LMS_BEST] = (double)best;
-      if (spec_ok) {
-        st[LMS_LAM] = lam;
-        st[LMS_PRED] = spec_pred;
-        st[LMS_SPEC_IDX] = (double)(sidx + 1);
-      } else {  // not positive definite at this damping: as the serial solve's failure branch
-        st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
-        st[LMS_FAIL] += 1.0;
-        st[LMS_SPEC_IDX] = (double)LM_SPEC;
-      }
+    if (spec_ok) {
+      publish(lam, spec_pred, (double)(sidx + 1));
+    } else {  // not positive definite at this damping: as the serial solve's failure branch
+      publish(fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max), pred_prev, (double)LM_SPEC);
+      if (tid == 0) st[LMS_FAIL] += 1.0;
     }
     return;
   }
@@ -863,14 +849,18 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   __syncthreads();  // the damped diagonal is in place
   switch (wid) {
     case 0:
-      lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail);
+      lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail,
+                    (m == 0 && d.stamps != nullptr) ? reinterpret_cast<unsigned long long*>(d.stamps) + 8 : nullptr);
+      RPH_STAMPS(6);
       lmc_backward<P>(T, lds + TG::OFF_RDG, vec);
+      RPH_STAMPS(7);
       break;
     case 1: LmcOwner<P, 0>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
     case 2: LmcOwner<P, 1>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
     default: LmcOwner<P, 2>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
   }
   __syncthreads();
+  RPH_STAMPS(3);
 #else
   using SY = LmSys<P>;
   double* A = lds;                          // system matrix, lower triangle (LmSys layout)
@@ -959,29 +949,18 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
     return;
   }
-  lm_wait_all(st, ticket);
-  publish_decision();
   RPH_STAMPS(4);
   if (failed) {
     // not positive definite at this damping: re-evaluate the best point with
     // more damping (trial := best)
     if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest;
-    if (tid == 0) {
-      st[LMS_BEST] = (double)best;
-      st[LMS_LAM] = fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max);
-      st[LMS_FAIL] += 1.0;
-      st[LMS_SPEC_IDX] = (double)LM_SPEC;
-    }
+    publish(fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max), pred_prev, (double)LM_SPEC);
+    if (tid == 0) st[LMS_FAIL] += 1.0;
     return;
   }
   RPH_STAMPS(5);
   if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest + vec[tid];
-  if (tid == 0) {
-    st[LMS_PRED] = pred;
-    st[LMS_BEST] = (double)best;
-    st[LMS_LAM] = lam;
-    st[LMS_SPEC_IDX] = 1.0;
-  }
+  publish(lam, pred, 1.0);
 #undef RPH_STAMPS
 }
 
@@ -1117,16 +1096,22 @@ extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p,
   return (int)hipGetLastError();
 }
 
+#ifndef RPH_LM_CHOL_V1
+#define RPH_LM_SHAPE_191(X) X(6, 8, 7, HEAD_FREE)
+#else
+#define RPH_LM_SHAPE_191(X)
+#endif
 #define RPH_LM_SHAPES(X)         \
   X(1, 8, 1, HEAD_COMPLEMENT)    \
   X(1, 8, 2, HEAD_FREE)          \
   X(2, 8, 2, HEAD_FREE)          \
   X(3, 8, 2, HEAD_FREE)          \
   X(4, 8, 2, HEAD_FREE)          \
-  X(5, 8, 6, HEAD_FREE)
-// (6, 8, 7) (P = 191) is not listed: its packed system matrix (147 KB) plus the
-// panel buffers exceed the 160 KB of LDS of the one-workgroup solve; such nets
-// fit with Adam (HipBackend.lm_supported() is False)
+  X(5, 8, 6, HEAD_FREE)          \
+  RPH_LM_SHAPE_191(X)
+// (6, 8, 7): P = 191, 78 tiles of the tile store = 156 KB of the CU's 160 KB
+// (lm_chol.h); larger nets have no LM solver and fit with Adam
+// (HipBackend.lm_supported() is False)
 
 // Geometry of the LM kernels for a shape: returns 0 and fills (P, R, NBLK,
 // two workgroups per CU) or -1 for shapes without an LM solver.
@@ -1154,7 +1139,7 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK)) return rc;      \
     if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs), dim3(256), 0, s, *lm, red_new); \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs), dim3(256), 0, s, *lm, red_new, pass); \
     return (int)hipGetLastError();                                                              \
   }
   RPH_LM_SHAPES(X)

@@ -39,11 +39,13 @@ struct TileGrid {
   static constexpr int NOWN = 3;                // owner waves
   static constexpr int TPW = (NTILE + NOWN - 1) / NOWN;
   static constexpr int NBG = (P + 31) / 32;     // 32 x 32 Gram blocks per row (k_lm_reduce layout)
-  // dynamic LDS (doubles): tile store | d [PT] | 1/L_kk [PT] | damped diagonal [PT] | column broadcast [16]
+  // dynamic LDS (doubles): tile store | d [PT] | 1/L_kk [PT] | column broadcast [16]; the damped
+  // diagonal shares d's slot (read by the owners' initial loads only, d written by the backward
+  // solve after the last panel), so the 6-asset net (P = 191, 78 tiles) fits the 160 KB
   static constexpr int OFF_D = NTILE * 256;
+  static constexpr int OFF_DIAG = OFF_D;
   static constexpr int OFF_RDG = OFF_D + PT;
-  static constexpr int OFF_DIAG = OFF_RDG + PT;
-  static constexpr int OFF_BC = OFF_DIAG + PT;
+  static constexpr int OFF_BC = OFF_RDG + PT;
   static constexpr int OFF_FLAGS = OFF_BC + 16;  // (as unsigned) pub[NT + 1], fac[NT + 1]
   static constexpr int LDS_BYTES = OFF_FLAGS * 8 + 2 * (NT + 1) * 4 + 16;
   // lower tile t (column-major) <-> (row block, column block)
@@ -117,15 +119,14 @@ struct LmcOwner {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 16 * ib + lq + 4 * r, c = 16 * jb + lr;
-          double v = 0.0;
-          if (i < P && c < P) {
-            if (i == c) v = diag[i];
-            else if (c < i) v = 2.0 * lmc_gram<TG::NBG>(src, i, c);
-          } else if (i == P && c < P) {
-            v = -g[c];
-          } else if (i == c) {
-            v = 1.0;
-          }
+          // every load unconditional (clamped, in bounds): a per-element
+          // branch around the load would wait out each one separately
+          const int ic = i < P ? i : P - 1, cc = c < P ? c : P - 1;
+          const double gv = lmc_gram<TG::NBG>(src, ic, cc), gr = g[cc], dg = diag[ic];
+          double v;
+          if (i < P && c < P) v = i == c ? dg : (c < i ? 2.0 * gv : 0.0);
+          else if (i == P && c < P) v = -gr;
+          else v = i == c ? 1.0 : 0.0;
           C[j][r] = v;
         }
       }
@@ -187,8 +188,18 @@ struct LmcOwner {
 
 // Panel wave: factor the NK panels; L (lower, zero above the diagonal) to
 // the store, 1 / L_kk to rdg.
+// diagnostic stamps (row of d.stamps, thread 0 = lane 0 of the panel wave;
+// tools/stamp_lm.py): 0/1 panel 0 wait passed / written back, 2/3 panel 1,
+// 4/5 last panel
+#define LMC_STAMP(k)                                                                    \
+  do {                                                                                  \
+    if (stamps != nullptr && lane == 0) stamps[k] = __builtin_amdgcn_s_memrealtime();  \
+  } while (0)
+
 template <int P>
-RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail) {
+RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail,
+                           unsigned long long* stamps) {
+#pragma clang fp contract(off)
   using TG = TileGrid<P>;
   constexpr int NS = TG::NSLOT;
   const int lane = threadIdx.x & 63;
@@ -198,6 +209,8 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
       *s_fail = 2;
       return;
     }
+    if (K < 2) LMC_STAMP(2 * K);
+    else if (K == TG::NK - 1) LMC_STAMP(4);
     const int nc = P - 16 * K < 16 ? P - 16 * K : 16;
     double a[NS][16];
 #pragma unroll
@@ -217,17 +230,21 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
         for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
       }
     }
-    double pnext = a[0][0];  // pivot candidate of the next column (valid in its lane)
+    // the lane's own diagonal entry (lanes 0..15: row 16K + lane of the diagonal
+    // tile), updated with its OWN L entries - the same fma sequence the
+    // broadcast update applies to it (bc[lane] is this lane's value), so the
+    // pivot chain never waits for the LDS broadcast round trip
+    double dg = lane < 16 ? T[TG::tidx(K, K) * 256 + tg_off(lane, lane)] : 1.0;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       if (c < nc) {
-        const double piv = lmc_readlane(pnext, c);
+        const double piv = lmc_readlane(dg, c);
         ok = ok && piv > 0.0;
         const double rl = lmc_rsq(piv);
 #pragma unroll
         for (int s = 0; s < NS; ++s) a[s][c] *= rl;
+        dg = __builtin_fma(-a[0][c], a[0][c], dg);  // lanes > c: their diagonal's column-c update
         if (lane < 16) bc[lane] = a[0][c];
-        if (c + 1 < 16) pnext = __builtin_fma(-a[0][c], a[0][c], a[0][c + 1]);
         if (lane == c) rdg[16 * K + c] = rl;
 #pragma unroll
         for (int j = c + 1; j < 16; ++j) {
@@ -254,9 +271,12 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
       }
     }
     lmc_signal(&fac[K]);
+    if (K < 2) LMC_STAMP(2 * K + 1);
+    else if (K == TG::NK - 1) LMC_STAMP(5);
   }
   if (!ok && lane == 0) *s_fail = 1;
 }
+#undef LMC_STAMP
 
 // Backward solve L^T d = y (y = row P of L) by the panel wave, blocks of 16
 // columns from the last: z = y_K - sum_{i >= 16(K+1)} L[i][K-block] d_i (lane
@@ -264,6 +284,7 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
 // triangular block by a readlane chain.  d -> dv[0, P).
 template <int P>
 RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv) {
+#pragma clang fp contract(off)
   using TG = TileGrid<P>;
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
   for (int K = TG::NK - 1; K >= 0; --K) {

@@ -190,22 +190,32 @@ constexpr int LM_SPEC = 4;
 // solver state (doubles)
 enum LmState : int {
   LMS_W = 0,                         // [2][LM_NPMAX] weights of the two slots (trial / best)
-  LMS_RED = 2 * LM_NPMAX,            // [2][LM_RED] reduced blocks of the two slots
-  LMS_BEST = LMS_RED + 2 * LM_RED,   // index of the best slot
-  LMS_LAM,                           // damping
-  LMS_NACC,                          // accepted steps
+  LMS_RED = 2 * LM_NPMAX,            // [2][LM_RED] reduced blocks (the best point's at LMS_RED)
+  LMS_BEST = LMS_RED + 2 * LM_RED,   // host mirror: index of the best weight slot (last solve)
+  LMS_LAM,                           // host mirror: damping after the last solve
+  LMS_NACC,                          // accepted steps of the current fit
   LMS_FAIL,                          // Cholesky failures (non-positive pivot)
-  LMS_COPY,                          // 1: the last solve accepted; the next pass kernel copies the trial's
-                                     // reduced block into the best slot (deferred off the solve's path)
-  LMS_NU,                            // Nielsen damping: growth factor of the next rejection
-  LMS_PRED,                          // predicted loss reduction of the pending trial (quadratic model)
-  LMS_SPEC_IDX = LMS_FAIL + 8,       // next precomputed reject-branch step (>= LM_SPEC: none)
-  LMS_SYNC,                          // (uint32) arrival counter of k_lm_solve's workgroups
-  LMS_SPEC_LAM,                      // [LM_SPEC] damping of precomputed step m
+  LMS_SPEC_LAM = LMS_FAIL + 8,       // [LM_SPEC] damping of precomputed reject-branch step m
   LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC,  // [LM_SPEC] its predicted reduction
   LMS_SPEC_OK = LMS_SPEC_PRED + LM_SPEC,   // [LM_SPEC] 1: positive definite (step valid)
   LMS_SPEC_W = LMS_SPEC_OK + LM_SPEC,       // [LM_SPEC][LM_NPMAX] trial weights best + d_m
-  LMS_FLOATS = LMS_SPEC_W + LM_SPEC * LM_NPMAX
+  // [2][LM_SLOT] solver scalars by pass parity: the pass and solve kernels of
+  // pass p read slot p & 1, the solve writes slot (p + 1) & 1 - so no
+  // workgroup of a solve ever reads a scalar another one is writing
+  LMS_SLOTS = LMS_SPEC_W + LM_SPEC * LM_NPMAX,
+  LMS_FLOATS = LMS_SLOTS + 16
+};
+constexpr int LM_SLOT = 8;
+enum LmSlot : int {
+  LSS_BEST = 0,    // index of the best weight slot
+  LSS_LAM,         // damping
+  LSS_NU,          // Nielsen damping: growth factor of the next rejection
+  LSS_PRED,        // predicted loss reduction of the pending trial (quadratic model)
+  LSS_COPY,        // 1: that solve accepted; the next pass kernel copies the trial's reduced
+                   // block into the best block (deferred off the solve's path)
+  LSS_SPEC_IDX,    // next precomputed reject-branch step (>= LM_SPEC: none)
+  LSS_LBEST,       // the best point's loss
+  LSS_STOP,        // > 0: the fit stopped at the solve of this pass (adaptive budget)
 };
 
 struct LmDesc {
@@ -232,6 +242,11 @@ struct LmDesc {
   int weights_only;              // 1: publish the weights only (no FitState / loss history: a bias refit
                                  // after an Adam fit, passes = 0)
   int damping;                   // 0: lam x lam_down / x lam_up on accept / reject; 1: Nielsen (gain ratio)
+  // adaptive pass budget: from the solve of pass stop_min on, a pass that
+  // lowers the best loss by less than stop_tol (relative) ends the fit; the
+  // remaining launches of the fit return at once (stop_tol = 0: off)
+  int stop_min;
+  float stop_tol;
   int pad2;
 };
 

@@ -265,7 +265,8 @@ class HedgeRun:
                                poll_every=tr.poll_every, seed=tr.seed,
                                feature_norm="none" if pf.raw_features else tr.feature_norm,
                                optimizer=str(tr.optimizer).lower(), lm_passes_first=int(tr.lm_passes_first),
-                               lm_passes_rest=int(tr.lm_passes_rest),
+                               lm_passes_rest=int(tr.lm_passes_rest), lm_stop_tol=float(tr.lm_stop_tol),
+                               lm_stop_min=int(tr.lm_stop_min),
                                mean_refit=bool(tr.mean_refit) and not pf.keras_fit_only)
         backend_q = None
         if (self.backend_kind == "hip" and self.di.world == 1 and icfg.q99 and not icfg.shared_q99_model

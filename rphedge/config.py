@@ -89,6 +89,9 @@ class TrainingParams:
                                      # Levenberg-Marquardt on the GPU: csrc/hedge_lm.hip; pinball fits stay Adam)
     lm_passes_first: int = 80        # LM trial points on the first date (from the random init)
     lm_passes_rest: int = 3          # LM trial points on later dates (warm start, Q18)
+    lm_stop_tol: float = 0.0         # later dates: adaptive pass budget, lm_passes_rest = the cap; a pass that
+                                     # lowers the best loss by < lm_stop_tol (relative) ends the fit (0: off)
+    lm_stop_min: int = 2             # ... never before this pass
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
     lm_damping: str = "simple"       # LM damping update: simple (x1/3 / x4) | nielsen (gain ratio)
     lm_lam0: float = 1e-3            # LM initial damping of every fit

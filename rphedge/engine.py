@@ -86,6 +86,11 @@ class FitConfig:
     # Levenberg-Marquardt passes (MSE fits of the 8-unit nets; ``epochs`` = the
     # number of trial points after the start point; csrc/hedge_lm.hip)
     optimizer: str = "adam"
+    # LM adaptive pass budget: from pass lm_stop_min on, a pass that lowers the
+    # best loss by less than lm_stop_tol (relative) ends the fit (0: off;
+    # ``epochs`` stays the cap)
+    lm_stop_tol: float = 0.0
+    lm_stop_min: int = 2
 
     def key(self):
         return (self.epochs, self.patience if self.early_stopping else 1 << 30, self.restore_best,
@@ -541,6 +546,7 @@ class HipBackend:
         b = self._lm_buffers()
         lm = b["desc"]
         lm.passes = int(fcfg.epochs)
+        lm.stop_tol, lm.stop_min = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
         d = self._train_desc(wts, opt, fit, data, fcfg, 0, None)
         d.batch, d.steps_per_epoch, d.shuffle = self.n_local, 1, 0
         d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
@@ -604,7 +610,7 @@ class HipBackend:
         def make():
             src = b["desc"]
             lm = type(src).from_buffer_copy(src)
-            lm.passes, lm.weights_only, lm.gram_wgs = 0, 1, 1
+            lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol = 0, 1, 1, 0.0
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
             return lm
@@ -855,7 +861,9 @@ class TorchBackend:
         Lb = float(stb[0] / stb[3].clamp_min(1.0))
         hist.append(Lb)
         trial = None
+        tol, kmin = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
         for k in range(1, int(fcfg.epochs) + 1):
+            Lb_old = Lb
             A = 2.0 * G
             dg = torch.diagonal(A).clone()
             dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
@@ -885,6 +893,9 @@ class TorchBackend:
                 nu *= 2.0
             else:
                 lam = min(lam * t.lm_lam_up, t.lm_lam_max)
+            # adaptive budget (the solve kernel's LSS_STOP rule; fp32 tolerance)
+            if tol > 0.0 and k >= kmin and not (Lb_old - Lb > float(np.float32(tol)) * Lb):
+                break
         bi = _lm_bias_index(spec, t)
         if bi >= 0 and float(G[bi, bi]) > 0.0:
             w_best = w_best.clone()

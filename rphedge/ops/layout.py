@@ -66,19 +66,22 @@ LM_GBLK_MAX = 21 * 1024
 LM_RED = LM_GBLK_MAX + LM_NPMAX + 8
 LMS_W = 0
 LMS_RED = 2 * LM_NPMAX
-LMS_BEST = LMS_RED + 2 * LM_RED
+LMS_BEST = LMS_RED + 2 * LM_RED      # host mirrors of the last solve
 LMS_LAM = LMS_BEST + 1
 LMS_NACC = LMS_BEST + 2
 LMS_FAIL = LMS_BEST + 3
-LMS_COPY = LMS_BEST + 4
-LMS_NU = LMS_BEST + 5
-LMS_PRED = LMS_BEST + 6
 LM_DP_WGS = 16
 LM_SPEC = 4
-LMS_SPEC_IDX = LMS_FAIL + 8
-LMS_SYNC = LMS_SPEC_IDX + 1
-LMS_SPEC_LAM = LMS_SYNC + 1
+LMS_SPEC_LAM = LMS_FAIL + 8
 LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC
 LMS_SPEC_OK = LMS_SPEC_PRED + LM_SPEC
 LMS_SPEC_W = LMS_SPEC_OK + LM_SPEC
-LMS_FLOATS = LMS_SPEC_W + LM_SPEC * LM_NPMAX
+LMS_SLOTS = LMS_SPEC_W + LM_SPEC * LM_NPMAX  # [2][LM_SLOT] scalars by pass parity
+LMS_FLOATS = LMS_SLOTS + 16
+LM_SLOT = 8
+LSS_BEST, LSS_LAM, LSS_NU, LSS_PRED, LSS_COPY, LSS_SPEC_IDX, LSS_LBEST, LSS_STOP = range(8)
+
+
+def lm_slot(pass_: int) -> int:
+    """State index of the scalar slot the pass / solve kernels of pass ``pass_`` read."""
+    return LMS_SLOTS + LM_SLOT * (int(pass_) & 1)

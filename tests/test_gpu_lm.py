@@ -12,7 +12,7 @@ from test_lm_cpu import _teacher_problem
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(1, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (5, 8, 6, 0)]
+SHAPES = [(1, 8, 2, 0), (1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (5, 8, 6, 0), (6, 8, 7, 0)]
 
 
 def _lm_row(q, h):
@@ -136,15 +136,70 @@ def test_lm_fit_matches_torch_and_is_deterministic(shape, damping):
     assert min(hist_g) == pytest.approx(min(hist_c), rel=2e-2)
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_lm_adaptive_budget_matches_fixed_budget(graph):
+    """Device-side adaptive pass budget (LmDesc.stop_tol, slot LSS_STOP): the
+    fit stops at the pass the torch oracle stops at, the remaining launches
+    return at once, and the result is BITWISE the fixed-budget fit of that
+    many passes (weights, FitState epoch and loss history); eager and
+    hipGraph-captured."""
+    from rphedge.engine import FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights, DateData
+    from rphedge.ops import layout as L
+    from rphedge.ops.native import Graph
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 14
+    spec, feats, pr, y, data, w0 = _setup((1, 8, 2, 0), n, dev, seed=3)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=2048)
+
+    def fit(fc):
+        be = HipBackend(spec, n, tc, device=dev)
+        w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+        if not graph:
+            be.fit(w, o, f, data, fc, seed=0)
+        else:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                be.fit(w, o, f, data, fc, seed=0)
+                s.synchronize()
+                w.copy_(be.new_weights(w0))
+                f.zero_()
+                g = Graph()
+                g.capture_begin(s)
+                try:
+                    be.fit(w, o, f, data, fc, seed=0)
+                finally:
+                    g.capture_end()
+                g.replay(s)
+                s.synchronize()
+        torch.cuda.synchronize()
+        return current_weights(spec, w), f.cpu().numpy()
+
+    fc_s = FitConfig(epochs=40, optimizer="lm", early_stopping=False, lm_stop_tol=0.02, lm_stop_min=3)
+    w_s, f_s = fit(fc_s)
+    k = int(f_s[L.F_EPOCH]) - 1
+    assert 3 <= k < 40, k
+    cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
+    tb = TorchBackend(spec, n, tc)
+    tb.fit(tb.new_weights(w0), tb.new_opt(), tb.new_fit(), cd, fc_s, seed=0)
+    assert len(tb.lm_last["hist"]) - 1 == k
+    w_f, f_f = fit(FitConfig(epochs=k, optimizer="lm", early_stopping=False))
+    np.testing.assert_array_equal(w_s, w_f)
+    np.testing.assert_array_equal(f_s[L.F_HIST:L.F_HIST + k + 1], f_f[L.F_HIST:L.F_HIST + k + 1])
+    assert f_s[L.F_EPOCH] == f_f[L.F_EPOCH] and f_s[L.F_BEST] == f_f[L.F_BEST]
+
+
 def test_lm_unsupported_shape_rejected_cleanly():
-    """The 6-asset net (P = 191) has no LM solver (its system does not fit one
-    workgroup's LDS): lm_supported() is False, an LM fit raises ValueError
-    before any launch, and the runtime is left without a pending HIP error."""
+    """The 32-unit nets (P = 1,153) have no LM solver (the system does not fit
+    one workgroup's LDS; every 8-unit net up to the 6-asset P = 191 does):
+    lm_supported() is False, an LM fit raises ValueError before any launch,
+    and the runtime is left without a pending HIP error."""
     from rphedge.engine import FitConfig, HipBackend, TrainConfig
 
     dev = torch.device("cuda", 0)
     n = 1 << 12
-    spec, feats, pr, y, data, w0 = _setup((6, 8, 7, 0), n, dev)
+    spec, feats, pr, y, data, w0 = _setup((1, 32, 2, 0), n, dev)
     be = HipBackend(spec, n, TrainConfig(batch_size=n), device=dev)
     assert not be.lm_supported()
     with pytest.raises(ValueError):

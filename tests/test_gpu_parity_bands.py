@@ -52,6 +52,15 @@ def test_mts_notebook_headline_seed_band():
     _band(v0, PUB["V0"], max_rel_scatter=0.04)
     _band(phi, PUB["phi0"], max_rel_scatter=0.08)
     _band(psi, PUB["psi0"], max_rel_scatter=0.15)
+    # the total t = 0 hedge value phi0 + psi0 is far tighter than its split
+    _band(np.add(phi, psi), PUB["phi0"] + PUB["psi0"], max_rel_scatter=0.02)
+    # overall residual VaR 98.5 / 99 / 99.5 % (":954-956"; EUR, near zero, so
+    # the scatter bound is absolute: 0.1 % of N P = 1,000 EUR)
+    var = np.asarray([r["VaR"] for r in runs], dtype=np.float64)
+    for k, pub in enumerate(PUB["VaR"]):
+        mean, sd = float(var[:, k].mean()), float(var[:, k].std(ddof=1))
+        assert sd <= 1_000.0, (k, mean, sd)
+        assert abs(mean - pub) <= 3.0 * sd + 50.0, (k, mean, sd, pub)
 
 
 def test_pension_rp_module_seed_band():

@@ -40,6 +40,40 @@ def test_lm_recovers_teacher_network(shape):
     assert float(f[2048 + 12]) == pytest.approx(min(hist), rel=1e-6)   # F_LAST_LOSS = best loss
 
 
+def test_lm_adaptive_budget_stops_early_and_equals_fixed_budget():
+    """lm_stop_tol: from pass lm_stop_min on, the first pass that lowers the
+    best loss by less than the tolerance (a rejection lowers it by 0) ends
+    the fit.  The stopped fit is the fixed-budget fit of that many passes
+    (same weights, same history)."""
+    from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops import layout as L
+
+    spec = NetSpec(1, 8, 2, 0)
+    n = 1 << 11
+    feats, pr, y = _teacher_problem(spec, n)
+    data = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr)
+    w0 = init_weights(spec, [0.5] * spec.nout, seed=1)
+
+    def run(**kw):
+        be = TorchBackend(spec, n, TrainConfig(batch_size=n, shuffle=False, lm_gram_paths=1024))
+        w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, FitConfig(optimizer="lm", early_stopping=False, **kw), seed=0)
+        return w.clone(), f.clone(), be.lm_last["hist"]
+
+    w_s, f_s, h_s = run(epochs=60, lm_stop_tol=0.05, lm_stop_min=3)
+    k = len(h_s) - 1                      # passes run
+    assert 3 <= k < 60
+    # the stopping pass gained < 5 %; every earlier pass from lm_stop_min on gained more
+    best = np.minimum.accumulate(h_s)
+    assert not (best[k - 1] - best[k] > 0.05 * best[k])
+    assert all(best[j - 1] - best[j] > np.float32(0.05) * best[j] for j in range(3, k))
+    w_f, f_f, h_f = run(epochs=k)
+    assert h_f == h_s
+    assert torch.equal(w_s, w_f)
+    assert int(f_s[L.F_EPOCH]) == k + 1
+
+
 def test_lm_pinball_rejected():
     from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig
     from rphedge.models.hedge_mlp import NetSpec, init_weights

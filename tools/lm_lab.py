@@ -141,6 +141,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
         if "varpro" in flags:
             trial, gt, Lt = project(trial, Gt, gt, Lt)
         hist.append(Lt)
+        Lb_prev = Lb
         if Lt == Lt and Lt < Lb:
             nacc += 1
             lam = max(lam * t.lm_lam_down, t.lm_lam_min)
@@ -150,6 +151,10 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
             w_best, G, g, Lb = trial, Gt, gt, Lt
         else:
             lam = min(lam * t.lm_lam_up, t.lm_lam_max)
+        if "adapt" in kv and not first and k >= int(kv.get("kmin", 2)):
+            # adaptive budget: stop once a pass improves the best loss by less than tol
+            if (Lb_prev - Lb) / max(Lb, 1e-300) < float(kv["adapt"]):
+                break
     if os.environ.get("LAB_DEBUG"): print("HIST", json.dumps([float("%.4g" % h) for h in hist]), file=sys.stderr)
     bi = E._lm_bias_index(spec, t)
     if bi >= 0 and float(G[bi, bi]) > 0.0:
@@ -167,7 +172,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
     fit[L.F_STOPPED] = 1.0
     fit[L.F_HASBEST] = 1.0
     VARIANT["lam_end"] = lam
-    VARIANT["log"].append({"passes": len(hist) - 1, "acc": nacc, "L0": hist[0], "L": Lb, "lam": lam})
+    VARIANT["log"].append({"passes": len(hist) - 1, "acc": nacc, "L0": hist[0], "L": Lb, "lam": lam, "hist": hist})
 
 
 
@@ -193,10 +198,14 @@ def main():
         res = json.loads(buf.getvalue().strip().splitlines()[-1])
         q = res["quality"]
         log = VARIANT["log"]
+        if os.environ.get("LAB_HIST"):
+            with open(os.environ["LAB_HIST"], "w") as fh:
+                json.dump(log, fh)
         print(json.dumps({"variant": v, "extra": a.extra, "pnl_std": round(q["terminal_pnl_std"], 4),
                           "resid_std": round(q["terminal_residual_std"], 4), "V0": round(q["V0"], 4),
                           "first": log[0] if log else None,
-                          "acc_rest": sum(x["acc"] for x in log[1:]), "fits": len(log)}), flush=True)
+                          "acc_rest": sum(x["acc"] for x in log[1:]), "fits": len(log),
+                          "passes_rest": sum(x["passes"] for x in log[1:])}), flush=True)
 
 
 if __name__ == "__main__":

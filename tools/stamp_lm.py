@@ -14,6 +14,9 @@ from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig  # noqa:
 from rphedge.models.hedge_mlp import NetSpec, init_weights  # noqa: E402
 
 
+TILE_SOLVER = True  # csrc/lm_chol.h (False: the RPH_LM_CHOL_V1 panel stamps)
+
+
 def run(n_log2=20, nin=1, passes=40):
     dev = torch.device("cuda", 0)
     nout = 2 if nin <= 4 else nin + 1
@@ -41,7 +44,16 @@ def run(n_log2=20, nin=1, passes=40):
     order = [k for k in (0, 1, 2, 6, 7, 3, 4, 5) if st[k]]
     ph = {f"solve_phase_{a}_{b}_us": (st[b] - st[a]) / 100.0 for a, b in zip(order, order[1:])}
     s1 = be.stamps[1].cpu().tolist()
-    if s1[0] and s1[1] and s1[2]:
+    if TILE_SOLVER and all(s1[k] for k in range(6)) and st[2]:
+        # csrc/lm_chol.h: row 1 = panel wave stamps (0/1 panel 0 wait passed / done, 2/3 panel 1, 4/5 last)
+        ph["tile_solver_us"] = {"setup_to_panel0_ready": (s1[0] - st[2]) / 100.0,
+                                "panel0": (s1[1] - s1[0]) / 100.0, "wait_panel1": (s1[2] - s1[1]) / 100.0,
+                                "panel1": (s1[3] - s1[2]) / 100.0, "wait_last": (s1[4] - s1[3]) / 100.0,
+                                "last_panel": (s1[5] - s1[4]) / 100.0,
+                                "factor_total": (s1[5] - s1[0]) / 100.0,
+                                "backward": (st[7] - st[6]) / 100.0 if st[6] and st[7] else None,
+                                "total_kernel": (st[5] - st[0]) / 100.0 if st[5] else None}
+    elif s1[0] and s1[1] and s1[2]:
         ph["panel6_phase1_us"] = (s1[1] - s1[0]) / 100.0
         ph["panel6_phase2_us"] = (s1[2] - s1[1]) / 100.0
     if s1[4] and st[7]:
