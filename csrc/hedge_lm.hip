@@ -676,6 +676,12 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     if (m == 0) RPH_STAMP(k);       \
   } while (0)
   RPH_STAMPS(0);
+#ifdef RPH_LDS_POISON
+  // diagnostic build: every dynamic-LDS double starts as NaN (a read before
+  // any write then shows in the result instead of an earlier kernel's data)
+  for (int i = tid; i < TileGrid<P>::LDS_BYTES / 8; i += 256) lds[i] = __builtin_nan("");
+  __syncthreads();
+#endif
   double* st = lm.state;
   double* best_red = st + LMS_RED;  // the best point's reduced block
   const double* sin = st + LMS_SLOTS + LM_SLOT * (pass & 1);  // read by every workgroup
@@ -849,10 +855,20 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   __syncthreads();  // the damped diagonal is in place
   switch (wid) {
     case 0:
-      lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail,
-                    (m == 0 && d.stamps != nullptr) ? reinterpret_cast<unsigned long long*>(d.stamps) + 8 : nullptr);
+    {
+      unsigned long long* stp = (m == 0 && d.stamps != nullptr) ? reinterpret_cast<unsigned long long*>(d.stamps) + 8 : nullptr;
+#ifdef RPH_PANEL_V2
+      lmc_panels_v2<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail, stp);
+#else
+      lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail, stp);
+#endif
+    }
       RPH_STAMPS(6);
+#ifdef RPH_BACKWARD_V2
+      lmc_backward_v2<P>(T, lds + TG::OFF_RDG, vec);
+#else
       lmc_backward<P>(T, lds + TG::OFF_RDG, vec);
+#endif
       RPH_STAMPS(7);
       break;
     case 1: LmcOwner<P, 0>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
@@ -861,6 +877,11 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   __syncthreads();
   RPH_STAMPS(3);
+#ifdef RPH_DUMP_T
+  // diagnostic build: the factored tile store -> d.stamps (as doubles)
+  if (m == 0 && d.stamps != nullptr)
+    for (int i = tid; i < TG::NTILE * 256 + 2 * TG::PT; i += 256) reinterpret_cast<double*>(d.stamps)[i] = lds[i];
+#endif
 #else
   using SY = LmSys<P>;
   double* A = lds;                          // system matrix, lower triangle (LmSys layout)

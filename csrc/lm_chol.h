@@ -39,14 +39,14 @@ struct TileGrid {
   static constexpr int NOWN = 3;                // owner waves
   static constexpr int TPW = (NTILE + NOWN - 1) / NOWN;
   static constexpr int NBG = (P + 31) / 32;     // 32 x 32 Gram blocks per row (k_lm_reduce layout)
-  // dynamic LDS (doubles): tile store | d [PT] | 1/L_kk [PT] | column broadcast [16]; the damped
+  // dynamic LDS (doubles): tile store | d [PT] | 1/L_kk [PT] | column broadcast [2][16]; the damped
   // diagonal shares d's slot (read by the owners' initial loads only, d written by the backward
   // solve after the last panel), so the 6-asset net (P = 191, 78 tiles) fits the 160 KB
   static constexpr int OFF_D = NTILE * 256;
   static constexpr int OFF_DIAG = OFF_D;
   static constexpr int OFF_RDG = OFF_D + PT;
   static constexpr int OFF_BC = OFF_RDG + PT;
-  static constexpr int OFF_FLAGS = OFF_BC + 16;  // (as unsigned) pub[NT + 1], fac[NT + 1]
+  static constexpr int OFF_FLAGS = OFF_BC + 32;  // (as unsigned) pub[NT + 1], fac[NT + 1]
   static constexpr int LDS_BYTES = OFF_FLAGS * 8 + 2 * (NT + 1) * 4 + 16;
   // lower tile t (column-major) <-> (row block, column block)
   static constexpr int tidx(int ib, int jb) { return jb * NT - jb * (jb - 1) / 2 + (ib - jb); }
@@ -93,6 +93,13 @@ RPH_INLINE double lmc_gram(const double* src, int i, int j) {
 RPH_INLINE void lmc_signal(unsigned* flag) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+// LDS hand-off between the lanes of ONE wave (a lane reads what other lanes
+// just stored): no instruction is needed (a wave's LDS operations complete in
+// order), but the compiler must not forward a value loaded before the stores
+// to a load after them - for the lanes that did not store, its single-thread
+// view says the memory is unchanged.  A wavefront-scope fence forbids that.
+RPH_INLINE void lmc_wave_sync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 
 // bounded wait for *flag >= target (one wave); false on timeout
 RPH_INLINE bool lmc_wait(const unsigned* flag, unsigned target) {
@@ -201,6 +208,104 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
                            unsigned long long* stamps) {
 #pragma clang fp contract(off)
   using TG = TileGrid<P>;
+  const int lane = threadIdx.x & 63;
+  bool ok = true, alive = true;
+  // every panel is its own straight-line code (static column count, static
+  // row slots): the column chain of one panel is a single basic block, so the
+  // next column's pivot chain overlaps this column's trailing updates
+  lm_static_for<TG::NK>([&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    constexpr int NC = P - 16 * K < 16 ? P - 16 * K : 16;  // factored columns
+    constexpr int ROWS = TG::PT - 16 * K;                  // rows of the panel (tile rows K..NT-1)
+    constexpr int NS = (ROWS + 63) / 64;                   // row slots per lane
+    if (!alive) return;
+    if (!lmc_wait(&pub[K], 3u)) {
+      *s_fail = 2;
+      alive = false;
+      return;
+    }
+    if constexpr (K < 2) LMC_STAMP(2 * K);
+    else if constexpr (K == TG::NK - 1) LMC_STAMP(4);
+    double a[NS][16];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int row = 16 * K + lane + 64 * s;
+      if (s + 1 < NS || lane + 64 * s < ROWS) {
+        const double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
+        const int sw = ((row & 15) >> 1) << 1;
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(tr + (c ^ sw));
+          a[s][c] = v.x;
+          a[s][c + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
+      }
+    }
+    // the lane's own diagonal entry (lanes 0..15: row 16K + lane of the diagonal
+    // tile), updated with its OWN L entries - the same fma sequence the column
+    // updates apply to it - so the pivot chain never waits for a broadcast
+    double dg = lane < 16 ? T[TG::tidx(K, K) * 256 + tg_off(lane, lane)] : 1.0;
+    lm_static_for<NC>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      const double piv = lmc_readlane(dg, c);
+      ok = ok && piv > 0.0;
+      const double rl = lmc_rsq(piv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) a[s][c] *= rl;
+      if (lane == c) rdg[16 * K + c] = rl;
+      // look-ahead: the next column first (its L entry by v_readlane), so the
+      // next pivot and scale wait for nothing but this column's arithmetic
+      if constexpr (c + 1 < NC) {
+        const double l1 = lmc_readlane(a[0][c], c + 1);  // L[16K + c + 1][16K + c]
+#pragma unroll
+        for (int s = 0; s < NS; ++s) a[s][c + 1] = __builtin_fma(-a[s][c], l1, a[s][c + 1]);
+      }
+      dg = __builtin_fma(-a[0][c], a[0][c], dg);  // lanes > c: their diagonal's column-c update
+      // the remaining columns: L[16K + j][16K + c] through an LDS broadcast
+      // (double-buffered by column parity: no write-after-read wait)
+      if constexpr (c + 2 < NC) {
+        double* b = bc + 16 * (c & 1);
+        if (lane < 16) b[lane] = a[0][c];
+        lmc_wave_sync();  // the other lanes' stores: no load may be forwarded across
+#pragma unroll
+        for (int j = c + 2; j < NC; ++j) {
+          const double lj = b[j];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
+        }
+      }
+    });
+    // write L back (the diagonal tile's upper triangle as zeros)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int row = 16 * K + lane + 64 * s;
+      if (s + 1 < NS || lane + 64 * s < ROWS) {
+        double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
+        const int sw = ((row & 15) >> 1) << 1;
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) {
+          double2 v;
+          v.x = (s == 0 && c > lane) ? 0.0 : a[s][c];
+          v.y = (s == 0 && c + 1 > lane) ? 0.0 : a[s][c + 1];
+          *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
+        }
+      }
+    }
+    lmc_signal(&fac[K]);
+    if constexpr (K < 2) LMC_STAMP(2 * K + 1);
+    else if constexpr (K == TG::NK - 1) LMC_STAMP(5);
+  });
+  if (!ok && lane == 0) *s_fail = 1;
+}
+// A/B: the round-3 runtime-loop panel and backward solve (bisecting)
+template <int P>
+RPH_INLINE void lmc_panels_v2(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail,
+                           unsigned long long* stamps) {
+#pragma clang fp contract(off)
+  using TG = TileGrid<P>;
   constexpr int NS = TG::NSLOT;
   const int lane = threadIdx.x & 63;
   bool ok = true;
@@ -245,6 +350,7 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
         for (int s = 0; s < NS; ++s) a[s][c] *= rl;
         dg = __builtin_fma(-a[0][c], a[0][c], dg);  // lanes > c: their diagonal's column-c update
         if (lane < 16) bc[lane] = a[0][c];
+        lmc_wave_sync();
         if (lane == c) rdg[16 * K + c] = rl;
 #pragma unroll
         for (int j = c + 1; j < 16; ++j) {
@@ -284,6 +390,51 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
 // triangular block by a readlane chain.  d -> dv[0, P).
 template <int P>
 RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv) {
+#pragma clang fp contract(off)
+  using TG = TileGrid<P>;
+  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+  // static blocks (last first): every load of a block is issued before its sums
+  lm_static_for<TG::NK>([&](auto kc) {
+    constexpr int K = TG::NK - 1 - decltype(kc)::value;
+    constexpr int NC = P - 16 * K < 16 ? P - 16 * K : 16;
+    constexpr int I0 = 16 * (K + 1);
+    constexpr int NI = P > I0 ? (P - I0 + 3) / 4 : 0;  // rows i = I0 + q + 4 t of this lane
+    const int col = 16 * K + c;
+    double z0 = 0.0, z1 = 0.0;  // two chains: half the fma latency
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int i = I0 + q + 4 * t;
+      if (i < P) {
+        const double l = T[TG::tidx(i >> 4, K) * 256 + tg_off(i & 15, c)];
+        if (t & 1) z1 = __builtin_fma(l, dv[i], z1);
+        else z0 = __builtin_fma(l, dv[i], z0);
+      }
+    }
+    double z = z0 + z1;
+    z += __shfl_xor(z, 16, 64);
+    z += __shfl_xor(z, 32, 64);
+    const double y = col < P ? T[TG::tidx(P >> 4, K) * 256 + tg_off(P & 15, c)] : 0.0;
+    z = y - z;
+    // column c of the diagonal tile: L[16K + j][16K + c], j = 0..15
+    double lc[16];
+    const double* td = T + TG::tidx(K, K) * 256;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) lc[j] = td[tg_off(j, c)];
+    const double rd = col < P ? rdg[col] : 0.0;
+    double dk = 0.0;
+#pragma unroll
+    for (int j = NC - 1; j >= 0; --j) {
+      const double dj = lmc_readlane(z * rd, j);  // d[16K + j] (final in lane j)
+      if (c == j) dk = dj;
+      z = __builtin_fma(-lc[j], dj, z);  // lanes c < j
+    }
+    if (q == 0 && col < P) dv[col] = dk;
+    lmc_wave_sync();
+  });
+}
+
+template <int P>
+RPH_INLINE void lmc_backward_v2(const double* T, const double* rdg, double* dv) {
 #pragma clang fp contract(off)
   using TG = TileGrid<P>;
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
