@@ -128,9 +128,12 @@ def parse(argv=None):
     ap.add_argument("--lm-stop-tol", type=float, default=None,
                     help="later dates: adaptive LM pass budget (relative best-loss gain that ends a fit; 0: off)")
     ap.add_argument("--lm-stop-min", type=int, default=None)
+    ap.add_argument("--lm-lam0-rest", type=float, default=None, help="later dates' initial LM damping (0: --lm-lam0)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--seed", type=int, default=1234, help="weight-init seed (the reference's 1234)")
+    ap.add_argument("--init", default=None, choices=["reference", "spread"], help="weight init (default: preset)")
     a = ap.parse_args(argv)
     pre = PRESETS[a.preset]
     for k in ("paths_log2", "dates", "substeps", "epochs_first", "epochs_rest", "batch_log2", "lr", "lr_rest"):
@@ -144,9 +147,11 @@ def parse(argv=None):
         a.feature_norm = pre.get("feature_norm", "date")
     if a.optimizer is None:
         a.optimizer = pre.get("optimizer", "adam")
+    if a.init is None:
+        a.init = pre.get("init", "reference")
     for k, dflt in (("lm_passes_first", 80), ("lm_passes_rest", 3), ("lm_gram_paths", 4096),
                     ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0),
-                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2)):
+                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -161,12 +166,12 @@ def build_run(a, world: int):
     tr = TrainingParams(batch_size=(1 << a.batch_log2) * world, epochs_first=a.epochs_first,
                         epochs_rest=a.epochs_rest, patience_first=10 ** 6, patience_rest=10 ** 6,
                         lr=a.lr, lr_rest=a.lr_rest, lr_decay=a.lr_decay, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
-                        chunk_log2=6, seed=1234, hidden=a.hidden, mfma_precision=a.mfma_precision,
+                        chunk_log2=6, seed=a.seed, hidden=a.hidden, mfma_precision=a.mfma_precision,
                         variant=a.variant, max_wgs=a.max_wgs, feature_norm=a.feature_norm,
                         optimizer=a.optimizer, lm_passes_first=a.lm_passes_first, lm_passes_rest=a.lm_passes_rest,
                         lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping, lm_lam0=a.lm_lam0,
                         lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down, lm_stop_tol=a.lm_stop_tol,
-                        lm_stop_min=a.lm_stop_min)
+                        lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, init=a.init)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -264,8 +269,14 @@ def lm_fit_stats(ind) -> dict:
         passes.append(max(len(h) - 1, 0))
         acc.append(n)
     tot = max(sum(passes), 1)
+    first = {"passes": passes[0] if passes else 0, "accepted": acc[0] if acc else 0}
+    if ind.dates:  # best-so-far loss of the first fit at a few passes (convergence record)
+        h = [x for x in ind.dates[0].fit_mse["history"] if x == x]
+        best = [min(h[:k + 1]) for k in range(len(h))]
+        first["best_loss_at"] = {str(k): best[k] for k in (0, 10, 20, 40, 60, 80, 120, 160, 240) if k < len(best)}
+        first["best_loss"] = best[-1] if best else None
     return {"passes_per_date": passes, "accepted_per_date": acc, "acceptance_rate": sum(acc) / tot,
-            "first_date": {"passes": passes[0] if passes else 0, "accepted": acc[0] if acc else 0}}
+            "first_date": first}
 
 
 def main(argv=None):
@@ -385,6 +396,7 @@ def main(argv=None):
                    "lm_gram_paths": a.lm_gram_paths if lm else None,
                    "lm_damping": a.lm_damping if lm else None,
                    "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
+                   "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None, "init": a.init,
                    "lm_stop": [a.lm_stop_tol, a.lm_stop_min] if (lm and a.lm_stop_tol > 0) else None,
                    "steps_per_epoch": None if lm else run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,

@@ -90,7 +90,12 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   const int trial = pass == 0 ? 0 : 1 - (int)sl[LSS_BEST];
   const Perm perm = make_perm(1u, 0u, 0u, false);
   typename B::Pre pre;
+#ifdef RPH_LM_PASS_V1
   B::load(d, 0, perm, B::first(wid), lane, pre);
+#else
+  const typename B::Sched sc = B::sched(d, lm.gram_wgs, lm.gram_skip);
+  B::load(d, 0, perm, sc.b0 * 128, lane, pre);
+#endif
   for (int i = tid; i < P; i += 256) {
     const float w = pass == 0 ? d.wts->w[0][i] : (float)st[LMS_W + trial * LM_NPMAX + i];
     wl[i] = w;
@@ -126,7 +131,11 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   typename B::Frags fr;
   B::make_frags(wl + S::OW2, fr);
   float val[NR];
+#ifdef RPH_LM_PASS_V1
   B::partial(d, 0, perm, wl, fr, scratch, pre, val);
+#else
+  B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc);
+#endif
 #pragma unroll
   for (int j = 0; j < NR; ++j)
     if (tid + 256 * j < R) lm.slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
@@ -991,8 +1000,19 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
 template <int NIN, int H, int NO, int HEAD>
 struct LmKernels {
   // the 1-3 input nets run two workgroups per CU (variant 5 body), the others one
+#ifndef RPH_LM_PAIR_WPS
+#define RPH_LM_PAIR_WPS 1
+#endif
+#ifdef RPH_LM_PASS_V1
   static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
+#else
+  static constexpr bool TWO = RPH_LM_PAIR_WPS == 2 && NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
+#endif
+#ifdef RPH_LM_PASS_V1
   using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
+#else
+  using Body = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1>;  // two paths per lane, packed fp32
+#endif
   using S = NetShape<NIN, H, NO, HEAD>;
 #ifndef RPH_LM_CHOL_V1
   // the tile store + vectors + hand-off counters (lm_chol.h)

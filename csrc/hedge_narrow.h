@@ -166,4 +166,194 @@ struct NarrowBody {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Full-batch MSE pass body of the Levenberg-Marquardt fits (k_lm_pass): TWO
+// paths per lane per iteration (lane l: paths j0 + l and j0 + 64 + l, both
+// coalesced), carried as float2 so the forward and backward matrix-vector
+// products issue as packed fp32 (v_pk_fma_f32: two paths per instruction)
+// and every weight read from LDS serves both paths.  The per-lane gradient
+// sums stay scalar (two fmas per entry and pair: a packed accumulator would
+// double the 128 accumulator registers past the 2-waves-per-SIMD budget).
+// Same packet layout and in-wave reduce-scatter as NarrowBody.
+// ---------------------------------------------------------------------------
+typedef float nb_f2 __attribute__((ext_vector_type(2)));
+
+RPH_INLINE nb_f2 nb_s(float w) { return nb_f2{w, w}; }
+RPH_INLINE nb_f2 nb_fma(nb_f2 a, nb_f2 b, nb_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+RPH_INLINE nb_f2 nb_lrelu(nb_f2 z, float alpha) { return __builtin_elementwise_max(z, z * alpha); }
+// d(lrelu)/dz * da (a = lrelu(z): a > 0 <=> z > 0 for 0 <= alpha)
+RPH_INLINE nb_f2 nb_lrelu_bwd(nb_f2 a, nb_f2 da, float alpha) {
+  const nb_f2 t = da * alpha;
+  return nb_f2{a.x > 0.f ? da.x : t.x, a.y > 0.f ? da.y : t.y};
+}
+// g += a.x * b.x + a.y * b.y (the pair's contribution to one gradient entry)
+RPH_INLINE float nb_acc(float g, nb_f2 a, nb_f2 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, g)); }
+
+template <int NIN, int H, int NO, int HEAD, int WPS = 2>
+struct NarrowPairBody {
+  static constexpr int WAVES_PER_SIMD = WPS;  // 2: two workgroups per CU (the 512-workgroup LM pass grid)
+  static constexpr int NIN_ = NIN, H_ = H, NO_ = NO, HEAD_ = HEAD;
+  using S = NetShape<NIN, H, NO, HEAD>;
+  static constexpr int P = S::P;
+  static constexpr int R = S::R;
+  static constexpr int NR = (R + 255) / 256;
+  static constexpr int NHOLD = S::NHOLD;
+  static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
+  static_assert(R <= 256, "one packet entry per thread");
+  struct Frags {};
+  struct Pre {
+    nb_f2 x[NIN], pr[NHOLD], y;
+    nb_f2 m;  // 1: a path of the shard, 0: past its end
+  };
+
+  RPH_INLINE static void make_frags(const float*, Frags&) {}
+  RPH_INLINE static long long first(int wid) { return (long long)(blockIdx.x * 4 + wid) * 128; }
+
+  // the 128-path blocks of this wave: b0, b0 + bstep, ... < bend.  The waves
+  // of the first gram_wgs workgroups (which also build a Gram tile after the
+  // paths) take gram_skip blocks fewer than an even split; the others share
+  // the rest (gram_skip = 0: every wave cyclic over all blocks)
+  struct Sched {
+    long long b0, bstep, bend;
+  };
+  RPH_INLINE static Sched sched(const TrainDesc& d, int gram_wgs, int gram_skip) {
+    const long long nblk = (d.batch + 127) / 128;
+    const int TW = (int)gridDim.x * 4, w = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int GW = (gram_wgs < (int)gridDim.x ? gram_wgs : (int)gridDim.x) * 4;
+    const long long per = nblk / TW;
+    if (gram_skip <= 0 || GW >= TW || per <= 0) return {w, TW, nblk};
+    const long long gb = per > gram_skip ? per - gram_skip : 0;
+    if (w < GW) return {w, GW, GW * gb};
+    return {GW * gb + (w - GW), TW - GW, nblk};
+  }
+
+  RPH_INLINE static void load(const TrainDesc& d, int, const Perm&, long long j0, int lane, Pre& p) {
+    const long long ja = j0 + lane, jb = ja + 64;
+    const bool va = ja < d.batch, vb = jb < d.batch;
+    const long long qa = va ? ja : 0, qb = vb ? jb : 0;
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) p.x[f] = nb_f2{d.feat[f][qa], d.feat[f][qb]};
+#pragma unroll
+    for (int k = 0; k < NHOLD - 1; ++k) p.pr[k] = nb_f2{d.price[k][qa], d.price[k][qb]};
+    p.pr[NHOLD - 1] = nb_s(d.bond);
+    p.y = nb_f2{d.target[qa], d.target[qb]};
+    p.m = nb_f2{va ? 1.f : 0.f, vb ? 1.f : 0.f};
+  }
+
+  RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
+                                 const Frags&, float* lds, Pre& pre, float (&val)[NR], const Sched& sc) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const long long stride = sc.bstep * 128;
+    const long long jend = sc.bend * 128 < d.batch ? sc.bend * 128 : d.batch;
+    float g[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) g[i] = 0.f;
+    const float alpha = d.alpha;
+    const float two_inv = 2.f * d.inv_batch;
+    Pre cur = pre;
+    for (long long j0 = sc.b0 * 128; j0 < jend; j0 += stride) {
+      // opaque 16-byte-aligned weight base: every weight use is an LDS
+      // broadcast read off one address register (register budget)
+      uint32_t z = 0;
+      asm volatile("" : "+v"(z));
+      const float* __restrict__ Wi = (const float*)__builtin_assume_aligned(W + (z & ~3u), 16);
+      nb_f2 x[NIN], pr[NHOLD];
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) x[f] = (cur.x[f] - d.fmu[f]) * d.fisd[f];
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) pr[k] = cur.pr[k];
+      const nb_f2 y = cur.y, m = cur.m;
+      if (j0 + stride < jend) load(d, step, perm, j0 + stride, lane, cur);  // the next pair, in flight
+
+      // forward
+      nb_f2 a1[H], a2[H], o[NO];
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        nb_f2 acc = nb_s(Wi[S::OB1 + j]);
+#pragma unroll
+        for (int f = 0; f < NIN; ++f) acc = nb_fma(x[f], nb_s(Wi[S::OW1 + f * H + j]), acc);
+        a1[j] = nb_lrelu(acc, alpha);
+      }
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        nb_f2 acc = nb_s(Wi[S::OB2 + j]);
+#pragma unroll
+        for (int i = 0; i < H; ++i) acc = nb_fma(a1[i], nb_s(Wi[S::OW2 + i * H + j]), acc);
+        a2[j] = nb_lrelu(acc, alpha);
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        nb_f2 acc = nb_s(Wi[S::OB3 + k]);
+#pragma unroll
+        for (int j = 0; j < H; ++j) acc = nb_fma(a2[j], nb_s(Wi[S::OW3 + j * NO + k]), acc);
+        o[k] = acc;
+      }
+      nb_f2 V;
+      if (HEAD == HEAD_COMPLEMENT) {  // psi = 1 - phi
+        V = nb_fma(o[0], pr[0] - pr[1], pr[1]);
+      } else {
+        V = o[0] * pr[0];
+#pragma unroll
+        for (int k = 1; k < NO; ++k) V = nb_fma(o[k], pr[k], V);
+      }
+      // MSE loss statistics and dL/dV (mean over the global batch)
+      const nb_f2 e = V - y;
+      const nb_f2 le = e * e * m;
+      const nb_f2 ae = nb_f2{fabsf(e.x), fabsf(e.y)} * m;
+      const nb_f2 ape = ae * nb_f2{__builtin_amdgcn_rcpf(fmaxf(fabsf(y.x), 1e-7f)),
+                                   __builtin_amdgcn_rcpf(fmaxf(fabsf(y.y), 1e-7f))};
+      g[P + 0] += le.x + le.y;
+      g[P + 1] += ae.x + ae.y;
+      g[P + 2] += ape.x + ape.y;
+      g[P + 3] += m.x + m.y;
+      const nb_f2 dV = e * m * two_inv;
+
+      // backward
+      nb_f2 dout[NO];
+      if (HEAD == HEAD_COMPLEMENT) {
+        dout[0] = dV * (pr[0] - pr[1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k].x + dout[k].y;
+      nb_f2 dz2[H];
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        nb_f2 da = nb_s(0.f);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          g[S::OW3 + j * NO + k] = nb_acc(g[S::OW3 + j * NO + k], a2[j], dout[k]);
+          da = nb_fma(nb_s(Wi[S::OW3 + j * NO + k]), dout[k], da);
+        }
+        dz2[j] = nb_lrelu_bwd(a2[j], da, alpha);
+        g[S::OB2 + j] += dz2[j].x + dz2[j].y;
+      }
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        nb_f2 da = nb_s(0.f);
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          g[S::OW2 + i * H + j] = nb_acc(g[S::OW2 + i * H + j], a1[i], dz2[j]);
+          da = nb_fma(nb_s(Wi[S::OW2 + i * H + j]), dz2[j], da);
+        }
+        const nb_f2 dz1 = nb_lrelu_bwd(a1[i], da, alpha);
+        g[S::OB1 + i] += dz1.x + dz1.y;
+#pragma unroll
+        for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = nb_acc(g[S::OW1 + f * H + i], x[f], dz1);
+      }
+    }
+    RPH_STAMP(5);  // path loop done
+    wave_reduce_scatter<R>(g, lane);
+    constexpr int PER = R / 64;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
+    __syncthreads();
+    const int t = threadIdx.x;
+    val[0] = (t < R) ? (lds[t] + lds[R + t]) + (lds[2 * R + t] + lds[3 * R + t]) : 0.f;
+    __syncthreads();
+  }
+};
+
 }  // namespace rph

@@ -247,7 +247,9 @@ struct LmDesc {
   // remaining launches of the fit return at once (stop_tol = 0: off)
   int stop_min;
   float stop_tol;
-  int pad2;
+  // pass kernel: the waves of the gram_wgs Gram workgroups take gram_skip
+  // path blocks fewer than an even split (their Gram tile follows the paths)
+  int gram_skip;
 };
 
 // Data-parallel exchange of the LM reduced block over IPC-mapped peer

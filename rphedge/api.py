@@ -220,7 +220,8 @@ class HedgeRun:
             bias = [p_itm, stats["E_payoff"] - p_itm] + [0.0] * (spec.nout - 2)
             if self.kind == "basket":
                 bias = [p_itm / c.n_assets] * c.n_assets + [stats["E_payoff"] - p_itm]
-        return hm.init_weights(spec, bias[: spec.nout], seed=c.train.seed)
+        return hm.init_weights(spec, bias[: spec.nout], seed=c.train.seed,
+                               spread=str(getattr(c.train, "init", "reference")) == "spread")
 
     def build(self, w0: np.ndarray | None = None):
         c = self.cfg
@@ -266,7 +267,7 @@ class HedgeRun:
                                feature_norm="none" if pf.raw_features else tr.feature_norm,
                                optimizer=str(tr.optimizer).lower(), lm_passes_first=int(tr.lm_passes_first),
                                lm_passes_rest=int(tr.lm_passes_rest), lm_stop_tol=float(tr.lm_stop_tol),
-                               lm_stop_min=int(tr.lm_stop_min),
+                               lm_stop_min=int(tr.lm_stop_min), lm_lam0_rest=float(tr.lm_lam0_rest),
                                mean_refit=bool(tr.mean_refit) and not pf.keras_fit_only)
         backend_q = None
         if (self.backend_kind == "hip" and self.di.world == 1 and icfg.q99 and not icfg.shared_q99_model

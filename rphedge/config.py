@@ -92,6 +92,10 @@ class TrainingParams:
     lm_stop_tol: float = 0.0         # later dates: adaptive pass budget, lm_passes_rest = the cap; a pass that
                                      # lowers the best loss by < lm_stop_tol (relative) ends the fit (0: off)
     lm_stop_min: int = 2             # ... never before this pass
+    init: str = "reference"          # weight init: reference (N(0, 0.1) kernels, zero hidden biases) | spread
+                                     # (first-layer breakpoints spread over the standardised inputs)
+    lm_lam0_rest: float = 0.0        # later dates' initial LM damping (0: lm_lam0; warm starts take smaller steps
+                                     # with a larger value)
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
     lm_damping: str = "simple"       # LM damping update: simple (x1/3 / x4) | nielsen (gain ratio)
     lm_lam0: float = 1e-3            # LM initial damping of every fit

@@ -61,6 +61,7 @@ class InductionConfig:
     lm_passes_rest: int = 3
     lm_stop_tol: float = 0.0             # later dates: adaptive LM pass budget (engine.FitConfig)
     lm_stop_min: int = 2
+    lm_lam0_rest: float = 0.0            # later dates' initial LM damping (0: TrainConfig.lm_lam0)
     # after each Adam MSE fit: exact refit of the bond holding's output bias
     # (engine bias_refit; LM fits do it in their last solve)
     mean_refit: bool = False
@@ -186,7 +187,8 @@ class BackwardInduction:
         if c.optimizer == "lm" and loss == L.LOSS_MSE:
             return FitConfig(epochs=c.lm_passes_first if first else c.lm_passes_rest, loss=loss,
                              optimizer="lm", early_stopping=False, lm_stop_tol=0.0 if first else c.lm_stop_tol,
-                             lm_stop_min=c.lm_stop_min)
+                             lm_stop_min=c.lm_stop_min,
+                             lm_lam0=None if (first or c.lm_lam0_rest <= 0) else c.lm_lam0_rest)
         return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
                          patience=c.patience_first if first else c.patience_rest,
                          loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else self.lr_rest,

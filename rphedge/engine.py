@@ -91,6 +91,7 @@ class FitConfig:
     # ``epochs`` stays the cap)
     lm_stop_tol: float = 0.0
     lm_stop_min: int = 2
+    lm_lam0: float | None = None          # initial LM damping of this fit (None: TrainConfig.lm_lam0)
 
     def key(self):
         return (self.epochs, self.patience if self.early_stopping else 1 << 30, self.restore_best,
@@ -133,6 +134,9 @@ class TrainConfig:
     # (free heads), so the fitted values' mean over all paths equals the
     # target's and no mean error drifts down the backward induction
     lm_bias_fix: bool = True
+    # pass kernel load balance: the Gram workgroups' waves take this many
+    # 128-path blocks fewer than an even split (their Gram tile follows)
+    lm_gram_skip: int = 3
     # run the data-parallel LM sequence (pass + reduce -> all-reduce of the
     # reduced block -> solve, one launch each) even on one rank: the test hook
     # that exercises the RCCL / mailbox exchange path at world size 1
@@ -532,6 +536,7 @@ class HipBackend:
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
             lm.bias_index = _lm_bias_index(self.spec, t)
             lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
+            lm.gram_skip = int(os.environ.get("RPH_LM_GRAM_SKIP", t.lm_gram_skip))  # (env: tuning sweeps)
             bufs["desc"] = lm
             return bufs
         return self._cache.get(("lm",), make)
@@ -547,6 +552,7 @@ class HipBackend:
         lm = b["desc"]
         lm.passes = int(fcfg.epochs)
         lm.stop_tol, lm.stop_min = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
+        lm.lam0 = float(self.tcfg.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
         d = self._train_desc(wts, opt, fit, data, fcfg, 0, None)
         d.batch, d.steps_per_epoch, d.shuffle = self.n_local, 1, 0
         d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
@@ -854,7 +860,7 @@ class TorchBackend:
 
         cur = int(wts[L.W_CUR].item())
         w_best = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
-        lam, nu = float(t.lm_lam0), 2.0
+        lam, nu = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0), 2.0
         nielsen = str(t.lm_damping).lower() == "nielsen"
         hist = []
         G, g, stb = evaluate(w_best)

@@ -131,10 +131,17 @@ def philox_normal(n: int, seed: int, stream: int = 0) -> np.ndarray:
     return ndtri_u30_f64(x)
 
 
-def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1) -> np.ndarray:
+def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1,
+                 spread: bool = False) -> np.ndarray:
     """Reference initialisation: kernels ~ N(0, 0.1) (seed 1234), hidden biases 0,
     output bias data-dependent (Q11: ``[1-p_oom, p_oom]`` pension,
-    ``mean(payoff)/S0`` European)."""
+    ``mean(payoff)/S0`` European).
+
+    ``spread``: the first layer's breakpoints are spread over the
+    standardised input range instead of all sitting at 0 (b1_j = -c_j |W1_j|,
+    c_j evenly spaced in [-1.5, 1.5]), so a kinked target has hidden units
+    near its kink from the start (an LM-mode option; the reference keeps
+    zero biases)."""
     o = spec.offsets
     w = np.zeros(spec.nparams, dtype=np.float32)
     for k, (name, shp) in enumerate(spec.shapes()):
@@ -142,6 +149,10 @@ def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1)
             n = int(np.prod(shp))
             start = {0: o["W1"], 2: o["W2"], 4: o["W3"]}[k]
             w[start:start + n] = (stddev * philox_normal(n, seed, stream=k)).astype(np.float32)
+    if spread and spec.hidden > 1:
+        W1 = w[o["W1"]:o["b1"]].reshape(spec.nin, spec.hidden).astype(np.float64)
+        c = np.linspace(-1.5, 1.5, spec.hidden)
+        w[o["b1"]:o["W2"]] = (-c * np.linalg.norm(W1, axis=0)).astype(np.float32)
     ob = np.broadcast_to(np.asarray(out_bias, dtype=np.float32), (spec.nout,))
     w[o["b3"]:o["b3"] + spec.nout] = ob
     return w

@@ -88,7 +88,7 @@ class LmDesc(C.Structure):
         ("gram_blk", C.c_int), ("gram_blk_stride", C.c_int), ("inv_ns", C.c_float), ("inv_n", C.c_float),
         ("lam0", C.c_float), ("lam_up", C.c_float), ("lam_down", C.c_float), ("lam_min", C.c_float),
         ("lam_max", C.c_float), ("ridge", C.c_float), ("bias_index", C.c_int), ("weights_only", C.c_int),
-        ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("pad2", C.c_int),
+        ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("gram_skip", C.c_int),
     ]
 
 
@@ -137,7 +137,7 @@ def _expected_layout() -> list[int]:
         PnlDesc.alpha.offset, PnlDesc.has_b.offset, PnlDesc.n_dates.offset, PnlDesc.head.offset,
         C.sizeof(LmDesc), LmDesc.slab_b.offset, LmDesc.slab_g.offset, LmDesc.num_wgs.offset,
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
-        LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset,
+        LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         L.LM_SPEC, L.LMS_SPEC_W, L.LMS_SLOTS, L.LM_SLOT, L.LSS_LBEST, L.LSS_STOP,
