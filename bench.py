@@ -129,6 +129,11 @@ def parse(argv=None):
                     help="later dates: adaptive LM pass budget (relative best-loss gain that ends a fit; 0: off)")
     ap.add_argument("--lm-stop-min", type=int, default=None)
     ap.add_argument("--lm-lam0-rest", type=float, default=None, help="later dates' initial LM damping (0: --lm-lam0)")
+    ap.add_argument("--lm-lam-carry", type=float, default=None,
+                    help="later dates start at the previous fit's final LM damping x this (0: off)")
+    ap.add_argument("--lm-starts", type=int, default=None, help="first date: multi-start LM exploration (1: off)")
+    ap.add_argument("--lm-explore-passes", type=int, default=None, help="trial points of every exploration fit")
+    ap.add_argument("--lm-explore-log2", type=int, default=None, help="exploration fits on 2^this local paths")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -151,7 +156,8 @@ def parse(argv=None):
         a.init = pre.get("init", "reference")
     for k, dflt in (("lm_passes_first", 80), ("lm_passes_rest", 3), ("lm_gram_paths", 4096),
                     ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0),
-                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0)):
+                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam_carry", 0.0),
+                    ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -171,7 +177,9 @@ def build_run(a, world: int):
                         optimizer=a.optimizer, lm_passes_first=a.lm_passes_first, lm_passes_rest=a.lm_passes_rest,
                         lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping, lm_lam0=a.lm_lam0,
                         lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down, lm_stop_tol=a.lm_stop_tol,
-                        lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, init=a.init)
+                        lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, init=a.init,
+                        lm_lam_carry=a.lm_lam_carry, lm_starts=a.lm_starts, lm_explore_passes=a.lm_explore_passes,
+                        lm_explore_log2=a.lm_explore_log2)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -279,6 +287,32 @@ def lm_fit_stats(ind) -> dict:
             "first_date": first}
 
 
+def multistart_record(run, a, world: int) -> dict:
+    """First-date multi-start exploration: every candidate's final best loss on
+    its exploration prefix (all ranks), the pick, and the exploration's work
+    in full passes over the local paths."""
+    from rphedge.ops import layout as L
+
+    be = run.backend
+    x = getattr(be, "lm_explore_last", None)
+    rec = {"starts": a.lm_starts * world, "explore_passes": a.lm_explore_passes}
+    nsub = min(run.n_local, 1 << a.lm_explore_log2)
+    rec["explore_paths_per_rank"] = nsub
+    rec["full_pass_equivalents"] = a.lm_starts * (a.lm_explore_passes + 1) * nsub / run.n_local
+    if isinstance(x, dict) and "sel" in x:
+        sel = x["sel"].double().cpu().numpy()
+        losses = [float(sel[c * L.LM_SEL_W]) for c in range(a.lm_starts * world)]
+    elif isinstance(x, dict):
+        losses = [float(v) for v in x["losses"]]
+    else:
+        return rec
+    import numpy as _np
+    ls = _np.where(_np.isnan(losses), _np.inf, losses)
+    rec["losses"] = losses
+    rec["pick"] = int(_np.argmin(ls))
+    return rec
+
+
 def main(argv=None):
     a = parse(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -342,6 +376,8 @@ def main(argv=None):
     res = run.collect()
     ms = 1000.0 * dt / max(a.steps, 1)
     lm_stats = lm_fit_stats(res.induction) if a.optimizer == "lm" else None
+    if lm_stats is not None and a.lm_starts > 1:
+        lm_stats["multistart"] = multistart_record(run, a, world)
     memory = None
     if gpu:
         # HBM footprint of this rank (every buffer is a torch allocation): the
@@ -361,6 +397,8 @@ def main(argv=None):
         (a.epochs_first + (n_dates - 1) * a.epochs_rest)
     if lm and lm_stats and a.lm_stop_tol > 0:  # adaptive budget: the evaluations actually run
         passes = sum(p + 1 for p in lm_stats["passes_per_date"])
+    if lm and lm_stats and lm_stats.get("multistart"):  # + the exploration, in full-pass equivalents
+        passes += lm_stats["multistart"]["full_pass_equivalents"]
     path_samples = float(n_total) * passes / (ms / 1000.0)
     value = float(n_total) / (ms / 1000.0)
     out = {
@@ -398,6 +436,10 @@ def main(argv=None):
                    "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
                    "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None, "init": a.init,
                    "lm_stop": [a.lm_stop_tol, a.lm_stop_min] if (lm and a.lm_stop_tol > 0) else None,
+                   "lm_lam_carry": (a.lm_lam_carry or None) if lm else None,
+                   "lm_multistart": ({"starts_per_rank": a.lm_starts, "explore_passes": a.lm_explore_passes,
+                                      "explore_paths_per_rank": 1 << a.lm_explore_log2}
+                                     if (lm and a.lm_starts > 1) else None),
                    "steps_per_epoch": None if lm else run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,
                    "step_schedule": None if lm else (run.backend.step_mode() if hasattr(run.backend, "step_mode")

@@ -77,13 +77,18 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   prefetch_kernarg_end(kat);
   // diagnostic phase stamps of every workgroup but 0 and 1 (tools/stamp_lm.py;
   // rows 0 and 1 belong to k_lm_solve)
-  const bool stamp_wg = blockIdx.x >= 2;
+  const bool stamp_wg = blockIdx.x >= 2 && blockIdx.y == 0;
 #define RPH_STAMPP(k)                 \
   do {                                \
     if (stamp_wg) RPH_STAMP(k);       \
   } while (0)
   RPH_STAMPP(0);
-  double* st = lm.state;
+  // instance (multi-start exploration: grid y) -> its state, slabs, reduced block
+  const int inst = blockIdx.y;
+  double* st = lm.state + (size_t)inst * LMS_FLOATS;
+  red_new += (size_t)inst * LM_RED;
+  float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
+  float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NBLK * 1024;
   double* sl = st + LMS_SLOTS + LM_SLOT * (pass & 1);  // this pass's scalars (written by the last solve)
   // trial point: pass 0 = the start point (canonical weights, published as
   // slot 0); later passes = the slot k_lm_solve wrote
@@ -97,7 +102,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   B::load(d, 0, perm, sc.b0 * 128, lane, pre);
 #endif
   for (int i = tid; i < P; i += 256) {
-    const float w = pass == 0 ? d.wts->w[0][i] : (float)st[LMS_W + trial * LM_NPMAX + i];
+    const float w = pass == 0 ? (lm.w0 != nullptr ? lm.w0[inst * LM_NPMAX + i] : d.wts->w[0][i])
+                              : (float)st[LMS_W + trial * LM_NPMAX + i];
     wl[i] = w;
     if (pass == 0 && blockIdx.x == 0) st[LMS_W + i] = (double)w;
   }
@@ -115,7 +121,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   if (pass > 0 && sl[LSS_STOP] != 0.0) return;  // adaptive budget spent: nothing to evaluate
   if (pass == 0 && blockIdx.x == 0 && tid == 0) {
     sl[LSS_BEST] = 1.0;
-    sl[LSS_LAM] = lm.lam0;
+    // (state[LMS_LAM] = the previous fit's final damping on this state)
+    sl[LSS_LAM] = lm.lam_carry > 0.f ? fmax(st[LMS_LAM] * (double)lm.lam_carry, (double)lm.lam_min) : (double)lm.lam0;
     sl[LSS_NU] = 2.0;
     sl[LSS_PRED] = 0.0;
     sl[LSS_COPY] = 0.0;
@@ -124,6 +131,10 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     sl[LSS_STOP] = 0.0;
     st[LMS_NACC] = 0.0;
     st[LMS_FAIL] = 0.0;
+  }
+  if (pass == 0 && blockIdx.x == 0 && inst == 0 && !lm.weights_only && !lm.explore) {
+    // the loss history: passes an adaptive budget skips stay NaN
+    for (int k = tid; k < MAXHIST; k += 256) d.fit->hist[k] = __builtin_nanf("");
   }
   __syncthreads();
   RPH_STAMPP(1);
@@ -138,7 +149,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 #endif
 #pragma unroll
   for (int j = 0; j < NR; ++j)
-    if (tid + 256 * j < R) lm.slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
+    if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
   RPH_STAMPP(2);
   if ((int)blockIdx.x >= lm.gram_wgs) return;
   // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
       const float* row = jt + (2 * s + h) * JP;
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(row[mb * 32 + r], row[nb * 32 + r], acc, 0, 0, 0);
     }
-    float* out = lm.slab_g + ((size_t)blockIdx.x * NBLK + b) * 1024;
+    float* out = slab_g + ((size_t)blockIdx.x * NBLK + b) * 1024;
 #pragma unroll
     for (int q = 0; q < 16; ++q) out[q * 64 + lane] = acc[q];
   }
@@ -223,14 +234,18 @@ __global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __re
   using LS = LmShape<P>;
   constexpr int NG = LS::NBLK * 1024;
   __shared__ double part[256];
-  if (pass > 0 && lm.state[LMS_SLOTS + LM_SLOT * (pass & 1) + LSS_STOP] != 0.0) return;
+  const int inst = blockIdx.y;  // multi-start instance
+  if (pass > 0 && lm.state[(size_t)inst * LMS_FLOATS + LMS_SLOTS + LM_SLOT * (pass & 1) + LSS_STOP] != 0.0) return;
+  red += (size_t)inst * LM_RED;
+  const float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NG;
+  const float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
   if ((int)blockIdx.x < NG / 64) {
     // Gram: workgroup handles entries [64 b, 64 b + 64), thread (g, l) sums
     // the slabs g, g + 4, ... of entry 64 b + l (16 loads in flight per
     // thread for 64 slabs), the 4 partial sums combined in LDS in fixed order
     const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + l;
-    const float* col = lm.slab_g + e;
+    const float* col = slab_g + e;
     double s0 = 0.0, s1 = 0.0;
     int w = g;
 #pragma unroll 4
@@ -253,10 +268,10 @@ __global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __re
   double s0 = 0.0, s1 = 0.0;
   int w = grp;
   for (; w + 64 < lm.num_wgs; w += 128) {
-    s0 += (double)lm.slab_b[(size_t)w * R + i];
-    s1 += (double)lm.slab_b[(size_t)(w + 64) * R + i];
+    s0 += (double)slab_b[(size_t)w * R + i];
+    s1 += (double)slab_b[(size_t)(w + 64) * R + i];
   }
-  if (w < lm.num_wgs) s0 += (double)lm.slab_b[(size_t)w * R + i];
+  if (w < lm.num_wgs) s0 += (double)slab_b[(size_t)w * R + i];
   part[threadIdx.x] = s0 + s1;
   __syncthreads();
 #pragma unroll
@@ -680,9 +695,9 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   __shared__ double s_diag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m = blockIdx.x;
-#define RPH_STAMPS(k)               \
-  do {                              \
-    if (m == 0) RPH_STAMP(k);       \
+#define RPH_STAMPS(k)                             \
+  do {                                            \
+    if (m == 0 && blockIdx.y == 0) RPH_STAMP(k);  \
   } while (0)
   RPH_STAMPS(0);
 #ifdef RPH_LDS_POISON
@@ -691,7 +706,9 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   for (int i = tid; i < TileGrid<P>::LDS_BYTES / 8; i += 256) lds[i] = __builtin_nan("");
   __syncthreads();
 #endif
-  double* st = lm.state;
+  const int inst = blockIdx.y;  // multi-start instance
+  double* st = lm.state + (size_t)inst * LMS_FLOATS;
+  red_new += (size_t)inst * LM_RED;
   double* best_red = st + LMS_RED;  // the best point's reduced block
   const double* sin = st + LMS_SLOTS + LM_SLOT * (pass & 1);  // read by every workgroup
   double* sout = st + LMS_SLOTS + LM_SLOT * ((pass + 1) & 1);  // written by workgroup 0
@@ -764,7 +781,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       st[LMS_BEST] = (double)best;  // host mirrors
       st[LMS_LAM] = lam_out;
       if (accept && pass > 0) st[LMS_NACC] += 1.0;
-      if (pass < MAXHIST && !lm.weights_only) d.fit->hist[pass] = (float)Lt;
+      if (pass < MAXHIST && !lm.weights_only && !lm.explore) d.fit->hist[pass] = (float)Lt;
     }
   };
   if (stopped && !final_pass) {  // carry the scalars to the next pass (no copy of the stale block)
@@ -784,6 +801,8 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     } else {
       publish(lam, pred_prev, (double)LM_SPEC);
     }
+    if (tid == 0) st[LMS_LFIN] = accept ? Lt : Lb;
+    if (lm.explore) return;  // exploration: k_lm_select publishes the chosen start point
     for (int i = tid; i < P; i += 256) {
       double wd = st[LMS_W + best * LM_NPMAX + i];
       if (i == lm.bias_index) {
@@ -865,7 +884,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   switch (wid) {
     case 0:
     {
-      unsigned long long* stp = (m == 0 && d.stamps != nullptr) ? reinterpret_cast<unsigned long long*>(d.stamps) + 8 : nullptr;
+      unsigned long long* stp = (m == 0 && blockIdx.y == 0 && d.stamps != nullptr) ? reinterpret_cast<unsigned long long*>(d.stamps) + 8 : nullptr;
 #ifdef RPH_PANEL_V2
       lmc_panels_v2<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail, stp);
 #else
@@ -1042,6 +1061,9 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   }
   if (lm->red_wgs != nblk * 1024 / 64 + R / 4) return rph_report("rph_lm", "bad red_wgs");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
+  if (lm->inst < 1 || lm->inst > LM_SEL_MAX) return rph_report("rph_lm", "bad instance count");
+  if (lm->inst > 1 && !lm->explore) return rph_report("rph_lm", "several instances are exploration fits only");
+  if (lm->explore && lm->weights_only) return rph_report("rph_lm", "exploration fits publish nothing");
   (void)P;
   return 0;
 }
@@ -1049,7 +1071,8 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
 template <int A, int B, int C, int E>
 static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const double* red_new, hipStream_t s) {
   using K = LmKernels<A, B, C, E>;
-  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs), dim3(256), 0, s, *d, *lm, pass, red_new);
+  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs, lm->inst), dim3(256), 0, s, *d, *lm, pass,
+                     red_new);
   return (int)hipGetLastError();
 }
 
@@ -1122,9 +1145,72 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange(const LmDpDesc x, double
   }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-start selection of a first date (one workgroup).  The exploration
+// fits (LmDesc.inst instances on a path prefix of every rank, LmDesc.explore)
+// leave their final best loss, damping and best weights in their states.
+//  phase 0 (pack): selection block of every candidate c = rank x inst + k:
+//    this rank's instances from their states, zeros in the other ranks'
+//    segments (summed over the ranks by the LM exchange = an all-gather);
+//  phase 1 (pick): the candidate with the lowest final best loss (NaN counts
+//    as +inf, ties go to the lowest index; every rank picks the same one):
+//    its weights -> the canonical NetWeights (the polish fit's start point),
+//    its damping -> main_state[LMS_LAM] (the polish fit carries it).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_lm_select(const TrainDesc d, const LmDesc lm, double* __restrict__ sel,
+                                                   double* __restrict__ main_state, const int world, const int rank,
+                                                   const int P, const int phase) {
+  const int tid = threadIdx.x;
+  const int K = lm.inst, NC = world * K;
+  if (phase == 0) {
+    for (int e = tid; e < NC * LM_SEL_W; e += 256) {
+      const int c = e / LM_SEL_W, j = e % LM_SEL_W;
+      double v = 0.0;
+      if (c / K == rank) {
+        const double* st = lm.state + (size_t)(c % K) * LMS_FLOATS;
+        const int best = (int)st[LMS_BEST];
+        v = j == 0 ? st[LMS_LFIN] : (j == 1 ? st[LMS_LAM] : (j - 2 < P ? st[LMS_W + best * LM_NPMAX + j - 2] : 0.0));
+      }
+      sel[e] = v;
+    }
+    return;
+  }
+  __shared__ int s_pick;
+  if (tid < 64) {
+    double l = tid < NC ? sel[(size_t)tid * LM_SEL_W] : INFINITY;
+    if (!(l == l)) l = INFINITY;
+    int idx = tid;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double l2 = __shfl_xor(l, o, 64);
+      const int i2 = __shfl_xor(idx, o, 64);
+      if (l2 < l || (l2 == l && i2 < idx)) {
+        l = l2;
+        idx = i2;
+      }
+    }
+    if (tid == 0) s_pick = idx < NC ? idx : 0;
+  }
+  __syncthreads();
+  const double* c = sel + (size_t)s_pick * LM_SEL_W;
+  for (int i = tid; i < P; i += 256) d.wts->w[0][i] = (float)c[2 + i];
+  if (tid == 0) main_state[LMS_LAM] = c[1];
+}
+
 }  // namespace rph
 
 using namespace rph;
+
+extern "C" int rph_lm_select(const TrainDesc* d, const LmDesc* lm, double* sel, double* main_state, int world,
+                             int rank, int P, int phase, void* stream) {
+  if (!d || !lm || !sel || !main_state || !lm->state || !d->wts) return rph_report("rph_lm_select", "null pointer");
+  if (world < 1 || rank < 0 || rank >= world || lm->inst < 1 || world * lm->inst > LM_SEL_MAX)
+    return rph_report("rph_lm_select", "bad world / rank / instance count");
+  if (P < 1 || P > LM_NPMAX || (phase != 0 && phase != 1)) return rph_report("rph_lm_select", "bad P / phase");
+  hipLaunchKernelGGL(k_lm_select, dim3(1), dim3(256), 0, (hipStream_t)stream, *d, *lm, sel, main_state, world, rank,
+                     P, phase);
+  return (int)hipGetLastError();
+}
 
 extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p, void* stream) {
   if (!x || !red || x->world < 2 || x->world > 8 || x->rank < 0 || x->rank >= x->world)
@@ -1180,7 +1266,8 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK)) return rc;      \
     if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs), dim3(256), 0, s, *lm, red_new, pass); \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs, lm->inst), dim3(256), 0, s, *lm, red_new, \
+                       pass);                                                                   \
     return (int)hipGetLastError();                                                              \
   }
   RPH_LM_SHAPES(X)
@@ -1204,7 +1291,8 @@ extern "C" int rph_lm_solve(const TrainDesc* d, const LmDesc* lm, const double* 
       }                                                                                                \
       attr = true;                                                                                     \
     }                                                                                                  \
-    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(LM_SPEC), dim3(256), bytes, s, *d, *lm, red_new, pass); \
+    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(LM_SPEC, lm->inst), dim3(256), bytes, s, *d, *lm, \
+                       red_new, pass);                                                                 \
     return (int)hipGetLastError();                                                                     \
   }
   RPH_LM_SHAPES(X)

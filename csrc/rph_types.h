@@ -195,6 +195,7 @@ enum LmState : int {
   LMS_LAM,                           // host mirror: damping after the last solve
   LMS_NACC,                          // accepted steps of the current fit
   LMS_FAIL,                          // Cholesky failures (non-positive pivot)
+  LMS_LFIN,                          // the fit's final best loss (written by the last solve)
   LMS_SPEC_LAM = LMS_FAIL + 8,       // [LM_SPEC] damping of precomputed reject-branch step m
   LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC,  // [LM_SPEC] its predicted reduction
   LMS_SPEC_OK = LMS_SPEC_PRED + LM_SPEC,   // [LM_SPEC] 1: positive definite (step valid)
@@ -250,7 +251,26 @@ struct LmDesc {
   // pass kernel: the waves of the gram_wgs Gram workgroups take gram_skip
   // path blocks fewer than an even split (their Gram tile follows the paths)
   int gram_skip;
+  // independent fits in one launch (grid y = instance k; k's state at
+  // state + k LMS_FLOATS, reduced block at red + k LM_RED, slabs at k x one
+  // instance's slab size): the multi-start exploration of a first date
+  int inst;
+  // 1: exploration fits - the last solve publishes nothing to the NetWeights /
+  // FitState (k_lm_select picks the start point of the polish fit)
+  int explore;
+  // > 0: the fit's initial damping is max(state[LMS_LAM] x lam_carry, lam_min)
+  // (the previous fit's final damping on this state), else lam0
+  float lam_carry;
+  int pad0;
+  const float* w0;               // [inst][LM_NPMAX] start weights (nullptr: the canonical NetWeights)
 };
+
+// Multi-start selection block (k_lm_select): candidate c = (rank, instance)
+// holds [final best loss, final damping, weights (LM_NPMAX)] at c * LM_SEL_W;
+// packed by every rank into its own segment, summed over the ranks (the LM
+// exchange), then every rank picks the same candidate.
+constexpr int LM_SEL_W = LM_NPMAX + 2;
+constexpr int LM_SEL_MAX = 64;          // candidates (world x instances)
 
 // Data-parallel exchange of the LM reduced block over IPC-mapped peer
 // mailboxes (k_lm_dp_exchange): LM_DP_WGS workgroups, each owning a chunk of

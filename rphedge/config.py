@@ -96,6 +96,12 @@ class TrainingParams:
                                      # (first-layer breakpoints spread over the standardised inputs)
     lm_lam0_rest: float = 0.0        # later dates' initial LM damping (0: lm_lam0; warm starts take smaller steps
                                      # with a larger value)
+    lm_lam_carry: float = 0.0        # later dates: initial LM damping = the previous fit's final one x this
+                                     # (0: off, lm_lam0 / lm_lam0_rest)
+    lm_starts: int = 1               # first date: multi-start LM exploration, starts per rank (1: off)
+    lm_explore_passes: int = 45      # ... trial points of every exploration fit
+    lm_explore_log2: int = 16        # ... on the first 2^this local paths; the best start over all ranks is
+                                     # then polished for lm_passes_first passes on every path
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
     lm_damping: str = "simple"       # LM damping update: simple (x1/3 / x4) | nielsen (gain ratio)
     lm_lam0: float = 1e-3            # LM initial damping of every fit

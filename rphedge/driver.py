@@ -62,6 +62,14 @@ class InductionConfig:
     lm_stop_tol: float = 0.0             # later dates: adaptive LM pass budget (engine.FitConfig)
     lm_stop_min: int = 2
     lm_lam0_rest: float = 0.0            # later dates' initial LM damping (0: TrainConfig.lm_lam0)
+    lm_lam_carry: float = 0.0            # later dates: start at the previous fit's final damping x this (0: off)
+    # first date: multi-start exploration (engine.FitConfig.lm_starts): lm_starts
+    # LM fits per rank of lm_explore_passes trial points on the first
+    # 2^lm_explore_log2 local paths, the best over all ranks polished for
+    # lm_passes_first passes on every path (1: off)
+    lm_starts: int = 1
+    lm_explore_passes: int = 45
+    lm_explore_log2: int = 16
     # after each Adam MSE fit: exact refit of the bond holding's output bias
     # (engine bias_refit; LM fits do it in their last solve)
     mean_refit: bool = False
@@ -148,6 +156,17 @@ class BackwardInduction:
             self.w_q = self.w_mse if icfg.shared_q99_model else backend.new_weights(w0)
             self.opt_q = backend.new_opt()
         self.w_init = backend.new_weights(w0)
+        # multi-start start points of the first LM fit: candidate 0 = the run's
+        # initial weights, the others the reference initialiser at seeds
+        # seed + 1000 c (same data-dependent output bias); every rank holds all
+        self.lm_w0s = None
+        if icfg.optimizer == "lm" and icfg.lm_starts > 1:
+            from .models import hedge_mlp as hm
+            o = spec.offsets
+            b3 = np.asarray(w0, np.float32)[o["b3"]:o["P"]]
+            rows = [np.asarray(w0, np.float32)] + [hm.init_weights(spec, b3, seed=icfg.seed + 1000 * c)
+                                                   for c in range(1, icfg.lm_starts * max(world, 1))]
+            self.lm_w0s = np.stack(rows)
         self.opt_init = backend.new_opt()
         self.fits = [[backend.new_fit(), backend.new_fit()] for _ in range(self.n_dates)]
         self.stats = [[backend.new_stats(), backend.new_stats()] for _ in range(self.n_dates)]
@@ -185,10 +204,16 @@ class BackwardInduction:
     def _fcfg(self, first: bool, loss: int) -> FitConfig:
         c = self.cfg
         if c.optimizer == "lm" and loss == L.LOSS_MSE:
+            ms = first and c.lm_starts > 1
             return FitConfig(epochs=c.lm_passes_first if first else c.lm_passes_rest, loss=loss,
                              optimizer="lm", early_stopping=False, lm_stop_tol=0.0 if first else c.lm_stop_tol,
                              lm_stop_min=c.lm_stop_min,
-                             lm_lam0=None if (first or c.lm_lam0_rest <= 0) else c.lm_lam0_rest)
+                             lm_lam0=None if (first or c.lm_lam0_rest <= 0) else c.lm_lam0_rest,
+                             lm_lam_carry=0.0 if first else c.lm_lam_carry,
+                             lm_starts=c.lm_starts if ms else 1,
+                             lm_explore_passes=c.lm_explore_passes if ms else 0,
+                             lm_explore_paths=(1 << int(c.lm_explore_log2)) if ms else 0,
+                             lm_w0s=self.lm_w0s if ms else None)
         return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
                          patience=c.patience_first if first else c.patience_rest,
                          loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else self.lr_rest,

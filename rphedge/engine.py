@@ -92,6 +92,19 @@ class FitConfig:
     lm_stop_tol: float = 0.0
     lm_stop_min: int = 2
     lm_lam0: float | None = None          # initial LM damping of this fit (None: TrainConfig.lm_lam0)
+    # > 0: the fit starts at the previous LM fit's final damping x lm_lam_carry
+    # (later dates: a warm start's curvature scale is the last fit's)
+    lm_lam_carry: float = 0.0
+    # multi-start exploration (first date): lm_starts fits per rank from the
+    # start points lm_w0s[rank * lm_starts + k] ([world x starts, P]; row 0 =
+    # the run's initial weights), lm_explore_passes trial points each on the
+    # first lm_explore_paths local paths (rank-local: no exchange), then every
+    # rank takes the candidate with the lowest final loss over all ranks and
+    # ``epochs`` polish passes on every path start there (at its damping)
+    lm_starts: int = 1
+    lm_explore_passes: int = 0
+    lm_explore_paths: int = 0
+    lm_w0s: object = None
 
     def key(self):
         return (self.epochs, self.patience if self.early_stopping else 1 << 30, self.restore_best,
@@ -558,6 +571,10 @@ class HipBackend:
         d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
         d.loss = L.LOSS_MSE
         n = self.native
+        lm.lam_carry = float(fcfg.lm_lam_carry)
+        if int(fcfg.lm_starts) > 1 and int(fcfg.lm_explore_passes) > 0:
+            self._lm_explore(d, fcfg)
+            lm.lam_carry = 1.0  # the polish starts at the chosen exploration's damping
         if self.world <= 1 and not self.tcfg.lm_split:
             n.lm_fit(d, lm, b["red"], self.stream)
             return
@@ -565,6 +582,70 @@ class HipBackend:
             n.lm_eval(d, lm, b["red"], k, self.stream)
             self._lm_allreduce(b["red"])
             n.lm_solve(d, lm, b["red"], k, self.stream)
+
+    def lm_explore_paths(self, fcfg: FitConfig) -> int:
+        """Local paths of a multi-start exploration: a prefix of the shard, a
+        multiple of 256 (one pass workgroup per 256 paths)."""
+        want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else self.n_local
+        return int(max(256, min(self.n_local, want) // 256 * 256))
+
+    def _lm_explore(self, d_main, fcfg: FitConfig):
+        """Multi-start exploration of a first date (graph-capturable): K
+        independent LM fits in ONE launch per kernel (grid y = instance) on the
+        first lm_explore_paths local paths, rank-local; k_lm_select packs the
+        candidates, the LM exchange all-gathers them (data parallel) and every
+        rank writes the same winner into the NetWeights and its damping into
+        the main LM state (the polish fit carries it)."""
+        b = self._lm_buffers()
+        K = int(fcfg.lm_starts)
+        nsub = self.lm_explore_paths(fcfg)
+        if K * max(self.world, 1) > L.LM_SEL_MAX:
+            raise ValueError(f"{K} starts x {self.world} ranks exceed the {L.LM_SEL_MAX} selection candidates")
+        if fcfg.lm_w0s is None or len(fcfg.lm_w0s) < K * max(self.world, 1):
+            raise ValueError("multi-start exploration needs lm_w0s (one start point per rank and instance)")
+        P = self.P
+
+        def make():
+            _, R, nblk, two = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+            t, dev = self.tcfg, self.device
+            nw = lm_pass_wgs(nsub, bool(two))
+            gw = int(max(1, min(max(L.LM_TILE, min(int(t.lm_gram_paths), nsub)) // L.LM_TILE, nw)))
+            w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
+            rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)[self.rank * K:(self.rank + 1) * K, :P]
+            w0[:, :P] = torch.from_numpy(np.ascontiguousarray(rows))
+            bufs = dict(state=torch.zeros(K, L.LMS_FLOATS, dtype=torch.float64, device=dev),
+                        red=torch.zeros(K, L.LM_RED, dtype=torch.float64, device=dev),
+                        slab_b=torch.zeros(K, nw, R, dtype=torch.float32, device=dev),
+                        slab_g=torch.zeros(K, gw, nblk * 1024, dtype=torch.float32, device=dev),
+                        w0=w0.to(dev), sel=torch.zeros(L.LM_RED, dtype=torch.float64, device=dev))
+            lm = type(b["desc"]).from_buffer_copy(b["desc"])
+            lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
+            lm.w0 = bufs["w0"].data_ptr()
+            lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol = K, 1, 0.0, 0, 0.0
+            lm.num_wgs, lm.gram_wgs = nw, gw
+            lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
+            lm.inv_ns, lm.inv_n = 1.0 / float(gw * L.LM_TILE), 1.0 / float(nsub)
+            bufs["desc"] = lm
+            return bufs
+        x = self._cache.get(("lm_explore", K, nsub), make)
+        lm = x["desc"]
+        lm.passes = int(fcfg.lm_explore_passes)
+        lm.lam0 = float(self.tcfg.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
+        d = type(d_main).from_buffer_copy(d_main)
+        d.n_local = d.batch = nsub
+        d.inv_batch = 1.0 / float(nsub)
+        n, W = self.native, max(self.world, 1)
+        n.lm_fit(d, lm, x["red"], self.stream)
+        n.lm_select(d, lm, x["sel"], b["state"], W, self.rank, P, 0, self.stream)
+        if W > 1:
+            ng = W * K * L.LM_SEL_W
+            if self.lm_mailbox is not None:
+                xd = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
+                n.lm_dp_exchange(xd, x["sel"], ng, 1, self.stream)
+            else:
+                self._lm_comm().allreduce_(x["sel"][:ng], self.stream)
+        n.lm_select(d, lm, x["sel"], b["state"], W, self.rank, P, 1, self.stream)
+        self.lm_explore_last = x
 
     def _lm_allreduce(self, red: torch.Tensor):
         """Sum the reduced LM block over the ranks: in-kernel exchange over the
@@ -785,6 +866,7 @@ class TorchBackend:
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
         self.eval_wgs = 1
         self._order_cache = {}
+        self._lm_lam_last = 0.0  # the last LM fit's final damping (FitConfig.lm_lam_carry)
 
     new_weights = HipBackend.new_weights
     new_opt = HipBackend.new_opt
@@ -818,7 +900,8 @@ class TorchBackend:
     def _lm_fit(self, wts, fit, data: DateData, fcfg: FitConfig):
         """Reference semantics of the HIP Levenberg-Marquardt fit (hedge_lm.hip):
         same trial sequence, damping rule, Gram subsample (the first
-        lm_gram_paths / world local paths) and bookkeeping, in float64."""
+        lm_gram_paths / world local paths) and bookkeeping, in float64; the
+        multi-start exploration (k_lm_select) and the damping carry included."""
         from torch.func import jacrev, vmap
 
         spec, t = self.spec, self.tcfg
@@ -829,79 +912,112 @@ class TorchBackend:
                          [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
         y = data.target.to(dt)
         W = max(self.world, 1)
-        n_glob = float(self.n_local * W)
-        nw = lm_pass_wgs(self.n_local, lm_two_per_cu(spec))
-        ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // W, self.n_local))
-        gw = max(1, min(ns_local // L.LM_TILE, nw))
-        ns = gw * L.LM_TILE
-        inv_ns = 1.0 / float(ns * W)
-        blk, bstride = lm_gram_geometry(self.n_local, ns, self.world)
-        sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
 
         def v_one(w, x, p):
             return (torch_forward(spec, w, x[None])[0] * p).sum()
 
-        def evaluate(w):
-            wg = w.detach().clone().requires_grad_(True)
-            e = (torch_forward(spec, wg, X) * pr).sum(1) - y
-            lsum = (e * e).sum()
-            (lsum / n_glob).backward()
-            J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X[sub], pr[sub])
-            red = torch.cat([(J.T @ J).reshape(-1) * inv_ns, wg.grad.detach(),
-                             torch.stack([lsum.detach(), e.detach().abs().sum(),
-                                          (e.detach().abs() / y.abs().clamp_min(1e-7)).sum(),
-                                          torch.tensor(float(len(y)), dtype=dt)])])
-            if self.world > 1:
-                self._allreduce(red)
-            G = red[: P * P].reshape(P, P)
-            g = red[P * P: P * P + P]
-            st = red[P * P + P:]
-            return G, g, st
+        def make_eval(n_loc: int, world: int):
+            """evaluate(w) -> (G, g, stats) over the first n_loc local paths
+            (all-reduced over the ranks when world > 1)."""
+            Xn, prn, yn = X[:n_loc], pr[:n_loc], y[:n_loc]
+            nw = lm_pass_wgs(n_loc, lm_two_per_cu(spec))
+            ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // world, n_loc))
+            gw = max(1, min(ns_local // L.LM_TILE, nw))
+            ns = gw * L.LM_TILE
+            inv_ns = 1.0 / float(ns * world)
+            blk, bstride = lm_gram_geometry(n_loc, ns, world)
+            sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
+            n_glob = float(n_loc * world)
+
+            def evaluate(w):
+                wg = w.detach().clone().requires_grad_(True)
+                e = (torch_forward(spec, wg, Xn) * prn).sum(1) - yn
+                lsum = (e * e).sum()
+                (lsum / n_glob).backward()
+                J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), Xn[sub], prn[sub])
+                red = torch.cat([(J.T @ J).reshape(-1) * inv_ns, wg.grad.detach(),
+                                 torch.stack([lsum.detach(), e.detach().abs().sum(),
+                                              (e.detach().abs() / yn.abs().clamp_min(1e-7)).sum(),
+                                              torch.tensor(float(len(yn)), dtype=dt)])])
+                if world > 1:
+                    self._allreduce(red)
+                return red[: P * P].reshape(P, P), red[P * P: P * P + P], red[P * P + P:]
+            return evaluate
+
+        nielsen = str(t.lm_damping).lower() == "nielsen"
+
+        def run(w_best, evaluate, passes, lam, tol=0.0, kmin=1):
+            """The solve kernel's sequence: returns (w, G, g, stats, loss, lam, hist)."""
+            nu = 2.0
+            G, g, stb = evaluate(w_best)
+            Lb = float(stb[0] / stb[3].clamp_min(1.0))
+            hist = [Lb]
+            for k in range(1, int(passes) + 1):
+                Lb_old = Lb
+                A = 2.0 * G
+                dg = torch.diagonal(A).clone()
+                dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
+                A = A + torch.diag(dmp)
+                Lc, info = torch.linalg.cholesky_ex(A)
+                pred = 0.0
+                if int(info) != 0:
+                    trial = w_best.clone()
+                    lam = min(lam * t.lm_lam_up * t.lm_lam_up, t.lm_lam_max)
+                else:
+                    dlt = torch.cholesky_solve(-g[:, None], Lc)[:, 0]
+                    trial = w_best + dlt
+                    pred = float(0.5 * ((dmp * dlt * dlt).sum() - (g * dlt).sum()))
+                Gt, gt, stt = evaluate(trial)
+                Lt = float(stt[0] / stt[3].clamp_min(1.0))
+                hist.append(Lt)
+                if Lt == Lt and Lt < Lb:
+                    if nielsen:
+                        rho = (Lb - Lt) / pred if pred > 0.0 else 1.0
+                        lam = max(lam * max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3), t.lm_lam_min)
+                        nu = 2.0
+                    else:
+                        lam = max(lam * t.lm_lam_down, t.lm_lam_min)
+                    w_best, G, g, stb, Lb = trial, Gt, gt, stt, Lt
+                elif nielsen:
+                    lam = min(lam * nu, t.lm_lam_max)
+                    nu *= 2.0
+                else:
+                    lam = min(lam * t.lm_lam_up, t.lm_lam_max)
+                # adaptive budget (the solve kernel's LSS_STOP rule; fp32 tolerance)
+                if tol > 0.0 and k >= kmin and not (Lb_old - Lb > float(np.float32(tol)) * Lb):
+                    break
+            return w_best, G, g, stb, Lb, lam, hist
 
         cur = int(wts[L.W_CUR].item())
         w_best = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
-        lam, nu = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0), 2.0
-        nielsen = str(t.lm_damping).lower() == "nielsen"
-        hist = []
-        G, g, stb = evaluate(w_best)
-        Lb = float(stb[0] / stb[3].clamp_min(1.0))
-        hist.append(Lb)
-        trial = None
+        lam = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
+        if float(fcfg.lm_lam_carry) > 0.0:
+            lam = max(self._lm_lam_last * float(np.float32(fcfg.lm_lam_carry)), float(np.float32(t.lm_lam_min)))
+        K = int(fcfg.lm_starts)
+        if K > 1 and int(fcfg.lm_explore_passes) > 0:
+            # multi-start exploration (k_lm_select): rank-local fits on a path prefix
+            want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else self.n_local
+            nsub = int(max(256, min(self.n_local, want) // 256 * 256))
+            ev = make_eval(nsub, 1)
+            rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)
+            lam_x = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
+            sel = torch.zeros(W * K, 2 + P, dtype=dt)
+            for k in range(K):
+                c = self.rank * K + k
+                wk = torch.from_numpy(rows[c, :P].copy()).to(dt)
+                wb, _, _, _, lb, lk, _ = run(wk, ev, int(fcfg.lm_explore_passes), lam_x)
+                sel[c, 0], sel[c, 1], sel[c, 2:] = lb, lk, wb
+            if self.world > 1:
+                self._allreduce(sel)
+            ls = sel[:, 0].clone()
+            ls[torch.isnan(ls)] = float("inf")
+            pick = int(torch.argmin(ls))  # (first index of the minimum)
+            w_best = sel[pick, 2:].to(torch.float32).to(dt)
+            lam = max(float(sel[pick, 1]), t.lm_lam_min)
+            self.lm_explore_last = {"losses": sel[:, 0].tolist(), "pick": pick}
         tol, kmin = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
-        for k in range(1, int(fcfg.epochs) + 1):
-            Lb_old = Lb
-            A = 2.0 * G
-            dg = torch.diagonal(A).clone()
-            dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
-            A = A + torch.diag(dmp)
-            Lc, info = torch.linalg.cholesky_ex(A)
-            pred = 0.0
-            if int(info) != 0:
-                trial = w_best.clone()
-                lam = min(lam * t.lm_lam_up * t.lm_lam_up, t.lm_lam_max)
-            else:
-                dlt = torch.cholesky_solve(-g[:, None], Lc)[:, 0]
-                trial = w_best + dlt
-                pred = float(0.5 * ((dmp * dlt * dlt).sum() - (g * dlt).sum()))
-            Gt, gt, stt = evaluate(trial)
-            Lt = float(stt[0] / stt[3].clamp_min(1.0))
-            hist.append(Lt)
-            if Lt == Lt and Lt < Lb:
-                if nielsen:
-                    rho = (Lb - Lt) / pred if pred > 0.0 else 1.0
-                    lam = max(lam * max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3), t.lm_lam_min)
-                    nu = 2.0
-                else:
-                    lam = max(lam * t.lm_lam_down, t.lm_lam_min)
-                w_best, G, g, stb, Lb = trial, Gt, gt, stt, Lt
-            elif nielsen:
-                lam = min(lam * nu, t.lm_lam_max)
-                nu *= 2.0
-            else:
-                lam = min(lam * t.lm_lam_up, t.lm_lam_max)
-            # adaptive budget (the solve kernel's LSS_STOP rule; fp32 tolerance)
-            if tol > 0.0 and k >= kmin and not (Lb_old - Lb > float(np.float32(tol)) * Lb):
-                break
+        w_best, G, g, stb, Lb, lam, hist = run(w_best, make_eval(self.n_local, W), int(fcfg.epochs), lam, tol, kmin)
+        self._lm_lam_last = lam
         bi = _lm_bias_index(spec, t)
         if bi >= 0 and float(G[bi, bi]) > 0.0:
             w_best = w_best.clone()
@@ -911,6 +1027,7 @@ class TorchBackend:
         wts[L.PMAX:L.PMAX + P] = w32
         wts[L.W_CUR] = 0.0
         fit.zero_()
+        fit[L.F_HIST:] = float("nan")  # (as k_lm_pass: passes never run stay NaN)
         fit[L.F_WBEST:L.F_WBEST + P] = w32
         c = max(float(stb[3]), 1.0)
         fit[L.F_BEST] = Lb

@@ -70,6 +70,9 @@ LMS_BEST = LMS_RED + 2 * LM_RED      # host mirrors of the last solve
 LMS_LAM = LMS_BEST + 1
 LMS_NACC = LMS_BEST + 2
 LMS_FAIL = LMS_BEST + 3
+LMS_LFIN = LMS_BEST + 4             # the fit's final best loss (last solve)
+LM_SEL_W = LM_NPMAX + 2             # multi-start selection block: [loss, damping, weights] per candidate
+LM_SEL_MAX = 64
 LM_DP_WGS = 16
 LM_SPEC = 4
 LMS_SPEC_LAM = LMS_FAIL + 8

@@ -89,7 +89,12 @@ class LmDesc(C.Structure):
         ("lam0", C.c_float), ("lam_up", C.c_float), ("lam_down", C.c_float), ("lam_min", C.c_float),
         ("lam_max", C.c_float), ("ridge", C.c_float), ("bias_index", C.c_int), ("weights_only", C.c_int),
         ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("gram_skip", C.c_int),
+        ("inst", C.c_int), ("explore", C.c_int), ("lam_carry", C.c_float), ("pad0", C.c_int), ("w0", VP),
     ]
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.inst = 1  # one fit per launch unless a multi-start exploration sets more
 
 
 class LmDpDesc(C.Structure):
@@ -138,6 +143,7 @@ def _expected_layout() -> list[int]:
         C.sizeof(LmDesc), LmDesc.slab_b.offset, LmDesc.slab_g.offset, LmDesc.num_wgs.offset,
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
+        LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, L.LMS_LFIN, L.LM_SEL_W,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         L.LM_SPEC, L.LMS_SPEC_W, L.LMS_SLOTS, L.LM_SLOT, L.LSS_LBEST, L.LSS_STOP,
@@ -181,6 +187,8 @@ def _bind(lib):
         "rph_lm_solve": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_fit": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, VP]),
         "rph_lm_dp_exchange": (C.c_int, [C.POINTER(LmDpDesc), VP, C.c_int, C.c_int, VP]),
+        "rph_lm_select": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, VP, C.c_int, C.c_int, C.c_int,
+                                    C.c_int, VP]),
         "rph_sobol_normal": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_longlong, C.c_int, C.c_int, VP]),
         "rph_simulate": (C.c_int, [C.POINTER(SimDesc), VP]),
         "rph_payoff": (C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP, C.c_float, VP, VP, VP]),
@@ -345,6 +353,15 @@ def lm_fit(desc: TrainDesc, lm: LmDesc, red_new: torch.Tensor, stream=None):
     """Whole single-rank Levenberg-Marquardt fit (csrc/hedge_lm.hip), launched from C++."""
     load(required=True)
     _check(_lib.rph_lm_fit(C.byref(desc), C.byref(lm), ptr(red_new), stream_handle(stream)), "rph_lm_fit")
+
+
+def lm_select(desc: TrainDesc, lm: LmDesc, sel: torch.Tensor, main_state: torch.Tensor, world: int, rank: int,
+              p: int, phase: int, stream=None):
+    """Multi-start selection (k_lm_select): phase 0 packs this rank's exploration
+    results into ``sel``, phase 1 picks the best candidate into the NetWeights
+    and ``main_state``'s damping."""
+    _check(_lib.rph_lm_select(C.byref(desc), C.byref(lm), ptr(sel), ptr(main_state), int(world), int(rank), int(p),
+                              int(phase), stream_handle(stream)), "rph_lm_select")
 
 
 def lm_dp_exchange(x: LmDpDesc, red: torch.Tensor, ng: int, p: int, stream=None):

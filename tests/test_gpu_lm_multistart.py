@@ -1,0 +1,142 @@
+"""Multi-start first-date LM fits (LmDesc.inst / explore, k_lm_select) and the
+damping carry (LmDesc.lam_carry) on the GPU: every exploration instance of the
+one-launch-per-kernel grid is bitwise the single fit from its start point, the
+selection writes the lowest-loss candidate, the whole explore + polish fit
+graph-captures and replays bitwise, and it follows the fp64 torch oracle."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_lm import _setup
+
+pytestmark = pytest.mark.gpu
+
+
+def _starts(spec, w0, k):
+    from rphedge.models.hedge_mlp import init_weights
+
+    o = spec.offsets
+    return np.stack([w0] + [init_weights(spec, w0[o["b3"]:o["P"]], seed=77 + 13 * c) for c in range(1, k)])
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0)])
+def test_explore_instances_equal_single_fits_and_pick_the_best(shape):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    n, nsub, K, n1 = 1 << 14, 1 << 12, 3, 10
+    spec, feats, pr, y, data, w0 = _setup(shape, n, dev, seed=5)
+    w0s = _starts(spec, w0, K)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=1024)
+    be = HipBackend(spec, n, tc, device=dev)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    fc = FitConfig(epochs=0, optimizer="lm", early_stopping=False, lm_starts=K, lm_explore_passes=n1,
+                   lm_explore_paths=nsub, lm_w0s=w0s)
+    be.fit(w, o, f, data, fc, seed=0)
+    torch.cuda.synchronize()
+    x = be.lm_explore_last
+    st = x["state"].cpu().numpy()
+    sel = x["sel"].cpu().numpy()
+    # every instance == the single-instance fit of its start point on the prefix
+    sub = DateData(feats=[t[:nsub] for t in data.feats], prices_next=[t[:nsub] for t in data.prices_next],
+                   bond_next=data.bond_next, target=data.target[:nsub], prices_now=[t[:nsub] for t in data.prices_now],
+                   fmu=data.fmu, fisd=data.fisd)
+    losses = []
+    for k in range(K):
+        b1 = HipBackend(spec, nsub, TrainConfig(batch_size=nsub, lm_gram_paths=1024), device=dev)
+        w1, o1, f1 = b1.new_weights(w0s[k]), b1.new_opt(), b1.new_fit()
+        b1.fit(w1, o1, f1, sub, FitConfig(epochs=n1, optimizer="lm", early_stopping=False), seed=0)
+        torch.cuda.synchronize()
+        s1 = b1._lm_buffers()["state"].cpu().numpy()
+        best = int(s1[L.LMS_BEST])
+        assert int(st[k, L.LMS_BEST]) == best
+        np.testing.assert_array_equal(st[k, L.LMS_W + best * L.LM_NPMAX:][:spec.nparams],
+                                      s1[L.LMS_W + best * L.LM_NPMAX:][:spec.nparams])
+        assert st[k, L.LMS_LFIN] == s1[L.LMS_LFIN]
+        assert st[k, L.LMS_LAM] == s1[L.LMS_LAM]
+        losses.append(s1[L.LMS_LFIN])
+        # the packed selection block
+        assert sel[k * L.LM_SEL_W] == s1[L.LMS_LFIN] and sel[k * L.LM_SEL_W + 1] == s1[L.LMS_LAM]
+    pick = int(np.argmin(losses))
+    bp = int(st[pick, L.LMS_BEST])
+    want = st[pick, L.LMS_W + bp * L.LM_NPMAX:][:spec.nparams].astype(np.float32)
+    # epochs = 0 polish: the start point is published (+ the bias Newton step)
+    got = current_weights(spec, w)
+    bi = spec.nparams - 1 if spec.head == L.HEAD_FREE else -1
+    keep = [i for i in range(spec.nparams) if i != bi]
+    np.testing.assert_array_equal(got[keep], want[keep])
+    assert int(f[L.F_EPOCH]) == 1 and np.isnan(float(f[L.F_HIST + 1]))
+
+
+def test_multistart_fit_graph_replays_and_follows_torch():
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.ops import layout as L
+    from rphedge.ops.native import Graph
+
+    dev = torch.device("cuda", 0)
+    n, K = 1 << 14, 4
+    spec, feats, pr, y, data, w0 = _setup((1, 8, 2, 0), n, dev, seed=3)
+    w0s = _starts(spec, w0, K)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=1024)
+    fc = FitConfig(epochs=8, optimizer="lm", early_stopping=False, lm_starts=K, lm_explore_passes=12,
+                   lm_explore_paths=1 << 12, lm_w0s=w0s)
+    be = HipBackend(spec, n, tc, device=dev)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, fc, seed=0)
+    torch.cuda.synchronize()
+    w_e, f_e = current_weights(spec, w), f.cpu().numpy()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    outs = []
+    with torch.cuda.stream(s):
+        g = Graph()
+        g.capture_begin(s)
+        try:
+            # (the exploration reads its start points from LmDesc.w0 and the
+            # selection overwrites the NetWeights: nothing to reset per replay)
+            be.fit(w, o, f, data, fc, seed=0)
+        finally:
+            g.capture_end()
+        for _ in range(2):
+            g.replay(s)
+            s.synchronize()
+            outs.append((current_weights(spec, w), f.cpu().numpy()))
+    for wg, fg in outs:
+        np.testing.assert_array_equal(wg, w_e)
+        np.testing.assert_array_equal(fg[L.F_HIST:L.F_HIST + 9], f_e[L.F_HIST:L.F_HIST + 9])
+    # torch oracle: same candidates picked, polish best loss close
+    cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
+    tb = TorchBackend(spec, n, tc)
+    tb.fit(tb.new_weights(w0), tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
+    xs = be.lm_explore_last["sel"].cpu().numpy()
+    lg = [xs[c * L.LM_SEL_W] for c in range(K)]
+    lc = tb.lm_explore_last["losses"]
+    np.testing.assert_allclose(lg, lc, rtol=2e-2)
+    assert int(np.argmin(lg)) == tb.lm_explore_last["pick"]
+    hist_g = np.minimum.accumulate(f_e[L.F_HIST:L.F_HIST + 9])
+    hist_c = np.minimum.accumulate(tb.lm_last["hist"])
+    np.testing.assert_allclose(hist_g[:4], hist_c[:4], rtol=5e-3)
+
+
+def test_lam_carry_starts_at_the_previous_fit_damping():
+    """lam_carry: a fit's first trial uses max(previous final damping x carry,
+    lam_min): two consecutive fits == the torch oracle's carried sequence."""
+    from rphedge.engine import FitConfig, HipBackend, TrainConfig
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 13
+    spec, feats, pr, y, data, w0 = _setup((1, 8, 2, 0), n, dev, seed=4)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=1024)
+    be = HipBackend(spec, n, tc, device=dev)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, FitConfig(epochs=6, optimizer="lm", early_stopping=False), seed=0)
+    torch.cuda.synchronize()
+    lam1 = float(be._lm_buffers()["state"][L.LMS_LAM])
+    # second fit, carry x 3, 0 trial points: the damping after its (start-only)
+    # final solve is the carried start damping
+    be.fit(w, o, f, data, FitConfig(epochs=0, optimizer="lm", early_stopping=False, lm_lam_carry=3.0), seed=0)
+    torch.cuda.synchronize()
+    lam2 = float(be._lm_buffers()["state"][L.LMS_LAM])
+    assert lam2 == pytest.approx(max(lam1 * 3.0, tc.lm_lam_min), rel=1e-12)

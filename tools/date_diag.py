@@ -18,7 +18,8 @@ def main(argv):
     run = HedgeRun(cfg)
     run.build()
     run.enqueue()
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     res = run.collect()
     ind = res.induction
     nh = run.spec.nhold
