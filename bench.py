@@ -67,7 +67,7 @@ METRIC = "MC paths/sec training 30-step hedge-MLP + terminal P&L std-dev, 1/2/4/
 PRESETS = {
     "euro30": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                    batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="lm",
-                   lm_passes_first=80, lm_passes_rest=2,
+                   lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0,
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
     "euro30_adam": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="adam",
@@ -75,16 +75,16 @@ PRESETS = {
     "heston30": dict(model="heston", dates=30, substeps=10, paths_log2=20, epochs_first=1024, epochs_rest=16,
                      batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1,
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
-                     optimizer="lm", lm_passes_first=80, lm_passes_rest=2,
+                     optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
-                    optimizer="lm", lm_passes_first=120, lm_passes_rest=2,
+                    optimizer="lm", lm_passes_first=120, lm_passes_rest=2, lm_lam_carry=3.0,
                     label="European call, 252-step GBM, 2M paths per GPU (16M at 8 GPUs)"),
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
                     extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
-                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2,
+                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0,
                     label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
     "euro30_mfma": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-3, lr_rest=1e-3, lr_decay=0.1, hidden=32,
@@ -132,6 +132,8 @@ def parse(argv=None):
     ap.add_argument("--lm-lam-carry", type=float, default=None,
                     help="later dates start at the previous fit's final LM damping x this (0: off)")
     ap.add_argument("--lm-starts", type=int, default=None, help="first date: multi-start LM exploration (1: off)")
+    ap.add_argument("--lm-renorm", type=int, default=None, choices=[0, 1],
+                    help="later dates: warm start re-expressed for the date's input standardisation")
     ap.add_argument("--lm-explore-passes", type=int, default=None, help="trial points of every exploration fit")
     ap.add_argument("--lm-explore-log2", type=int, default=None, help="exploration fits on 2^this local paths")
     ap.add_argument("--no-graph", action="store_true")
@@ -157,7 +159,7 @@ def parse(argv=None):
     for k, dflt in (("lm_passes_first", 80), ("lm_passes_rest", 3), ("lm_gram_paths", 4096),
                     ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0),
                     ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam_carry", 0.0),
-                    ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16)):
+                    ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16), ("lm_renorm", 0)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -179,7 +181,7 @@ def build_run(a, world: int):
                         lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down, lm_stop_tol=a.lm_stop_tol,
                         lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, init=a.init,
                         lm_lam_carry=a.lm_lam_carry, lm_starts=a.lm_starts, lm_explore_passes=a.lm_explore_passes,
-                        lm_explore_log2=a.lm_explore_log2)
+                        lm_explore_log2=a.lm_explore_log2, lm_renorm=bool(a.lm_renorm))
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -437,6 +439,7 @@ def main(argv=None):
                    "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None, "init": a.init,
                    "lm_stop": [a.lm_stop_tol, a.lm_stop_min] if (lm and a.lm_stop_tol > 0) else None,
                    "lm_lam_carry": (a.lm_lam_carry or None) if lm else None,
+                   "lm_renorm": bool(a.lm_renorm) if lm else None,
                    "lm_multistart": ({"starts_per_rank": a.lm_starts, "explore_passes": a.lm_explore_passes,
                                       "explore_paths_per_rank": 1 << a.lm_explore_log2}
                                      if (lm and a.lm_starts > 1) else None),

@@ -102,8 +102,28 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   B::load(d, 0, perm, sc.b0 * 128, lane, pre);
 #endif
   for (int i = tid; i < P; i += 256) {
-    const float w = pass == 0 ? (lm.w0 != nullptr ? lm.w0[inst * LM_NPMAX + i] : d.wts->w[0][i])
-                              : (float)st[LMS_W + trial * LM_NPMAX + i];
+    float w;
+    if (pass == 0) {
+      const float* w0p = lm.w0 != nullptr ? lm.w0 + inst * LM_NPMAX : d.wts->w[0];
+      w = w0p[i];
+      if (lm.renorm) {
+        // x_old = x_new (isd_old / isd_new) + (mu_new - mu_old) isd_old: W1 rescaled,
+        // b1 absorbs the shift (fp64, rounded once)
+        if (i >= S::OW1 && i < S::OW1 + NIN * H) {
+          const int f = (i - S::OW1) / H;
+          w = (float)((double)w * ((double)lm.ren_isd[f] / (double)d.fisd[f]));
+        } else if (i >= S::OB1 && i < S::OB1 + H) {
+          double acc = (double)w;
+#pragma unroll
+          for (int f = 0; f < NIN; ++f)
+            acc += (double)w0p[S::OW1 + f * H + (i - S::OB1)] * (double)lm.ren_isd[f] *
+                   ((double)d.fmu[f] - (double)lm.ren_mu[f]);
+          w = (float)acc;
+        }
+      }
+    } else {
+      w = (float)st[LMS_W + trial * LM_NPMAX + i];
+    }
     wl[i] = w;
     if (pass == 0 && blockIdx.x == 0) st[LMS_W + i] = (double)w;
   }

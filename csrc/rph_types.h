@@ -263,6 +263,14 @@ struct LmDesc {
   float lam_carry;
   int pad0;
   const float* w0;               // [inst][LM_NPMAX] start weights (nullptr: the canonical NetWeights)
+  // 1: the start weights were fitted on inputs standardised with (ren_mu,
+  // ren_isd); the first layer is re-expressed for this fit's (fmu, fisd), so
+  // the warm start is the previous date's hedge as a function of the RAW state
+  // (the reference's warm start: raw features)
+  int renorm;
+  int pad1;
+  float ren_mu[MAXIN];
+  float ren_isd[MAXIN];
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)

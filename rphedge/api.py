@@ -269,6 +269,7 @@ class HedgeRun:
                                lm_passes_rest=int(tr.lm_passes_rest), lm_stop_tol=float(tr.lm_stop_tol),
                                lm_stop_min=int(tr.lm_stop_min), lm_lam0_rest=float(tr.lm_lam0_rest),
                                lm_lam_carry=float(tr.lm_lam_carry), lm_starts=int(tr.lm_starts),
+                               lm_renorm=bool(tr.lm_renorm),
                                lm_explore_passes=int(tr.lm_explore_passes), lm_explore_log2=int(tr.lm_explore_log2),
                                mean_refit=bool(tr.mean_refit) and not pf.keras_fit_only)
         backend_q = None

@@ -98,6 +98,8 @@ class TrainingParams:
                                      # with a larger value)
     lm_lam_carry: float = 0.0        # later dates: initial LM damping = the previous fit's final one x this
                                      # (0: off, lm_lam0 / lm_lam0_rest)
+    lm_renorm: bool = False          # later dates: the warm start's first layer re-expressed for the date's input
+                                     # standardisation (the previous hedge as a function of the raw state)
     lm_starts: int = 1               # first date: multi-start LM exploration, starts per rank (1: off)
     lm_explore_passes: int = 45      # ... trial points of every exploration fit
     lm_explore_log2: int = 16        # ... on the first 2^this local paths; the best start over all ranks is

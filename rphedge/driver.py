@@ -63,6 +63,7 @@ class InductionConfig:
     lm_stop_min: int = 2
     lm_lam0_rest: float = 0.0            # later dates' initial LM damping (0: TrainConfig.lm_lam0)
     lm_lam_carry: float = 0.0            # later dates: start at the previous fit's final damping x this (0: off)
+    lm_renorm: bool = False              # later dates: warm start re-expressed for the date's standardisation
     # first date: multi-start exploration (engine.FitConfig.lm_starts): lm_starts
     # LM fits per rank of lm_explore_passes trial points on the first
     # 2^lm_explore_log2 local paths, the best over all ranks polished for
@@ -201,10 +202,13 @@ class BackwardInduction:
         c = self.cfg
         return -c.cost_of_capital if c.holdings_blend_sign_rp else c.cost_of_capital
 
-    def _fcfg(self, first: bool, loss: int) -> FitConfig:
+    def _fcfg(self, first: bool, loss: int, t: int | None = None) -> FitConfig:
         c = self.cfg
         if c.optimizer == "lm" and loss == L.LOSS_MSE:
             ms = first and c.lm_starts > 1
+            # the warm start was fitted at date t + 1 (its standardisation)
+            ren = (self.norms[t + 1] if (c.lm_renorm and not first and c.warm_start and t is not None and self.norms
+                                         and t + 1 < len(self.norms)) else None)
             return FitConfig(epochs=c.lm_passes_first if first else c.lm_passes_rest, loss=loss,
                              optimizer="lm", early_stopping=False, lm_stop_tol=0.0 if first else c.lm_stop_tol,
                              lm_stop_min=c.lm_stop_min,
@@ -213,7 +217,7 @@ class BackwardInduction:
                              lm_starts=c.lm_starts if ms else 1,
                              lm_explore_passes=c.lm_explore_passes if ms else 0,
                              lm_explore_paths=(1 << int(c.lm_explore_log2)) if ms else 0,
-                             lm_w0s=self.lm_w0s if ms else None)
+                             lm_w0s=self.lm_w0s if ms else None, lm_renorm=ren)
         return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
                          patience=c.patience_first if first else c.patience_rest,
                          loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else self.lr_rest,
@@ -263,7 +267,7 @@ class BackwardInduction:
                                        seed=fit_seed(c.seed, t, 1), poll_every=0)
                     join = torch.cuda.Event()
                     join.record(self._side)
-            be.fit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE),
+            be.fit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE, t),
                    seed=fit_seed(c.seed, t, 0), poll_every=c.poll_every)
             if c.mean_refit and c.optimizer != "lm":
                 be.bias_refit(self.w_mse, self.opt_mse, f_m, data, self._fcfg(first, L.LOSS_MSE))

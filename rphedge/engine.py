@@ -101,6 +101,10 @@ class FitConfig:
     # first lm_explore_paths local paths (rank-local: no exchange), then every
     # rank takes the candidate with the lowest final loss over all ranks and
     # ``epochs`` polish passes on every path start there (at its damping)
+    # (mu, isd) of the inputs the start weights were fitted on (the previous
+    # date): the first layer is re-expressed for this fit's standardisation, so
+    # a warm start is the previous hedge as a function of the raw state
+    lm_renorm: tuple | None = None
     lm_starts: int = 1
     lm_explore_passes: int = 0
     lm_explore_paths: int = 0
@@ -572,6 +576,12 @@ class HipBackend:
         d.loss = L.LOSS_MSE
         n = self.native
         lm.lam_carry = float(fcfg.lm_lam_carry)
+        lm.renorm = 0
+        if fcfg.lm_renorm is not None and data.fmu:
+            mu, isd = fcfg.lm_renorm
+            for i in range(len(mu)):
+                lm.ren_mu[i], lm.ren_isd[i] = float(mu[i]), float(isd[i])
+            lm.renorm = 1
         if int(fcfg.lm_starts) > 1 and int(fcfg.lm_explore_passes) > 0:
             self._lm_explore(d, fcfg)
             lm.lam_carry = 1.0  # the polish starts at the chosen exploration's damping
@@ -621,7 +631,7 @@ class HipBackend:
             lm = type(b["desc"]).from_buffer_copy(b["desc"])
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
             lm.w0 = bufs["w0"].data_ptr()
-            lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol = K, 1, 0.0, 0, 0.0
+            lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
             lm.num_wgs, lm.gram_wgs = nw, gw
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
             lm.inv_ns, lm.inv_n = 1.0 / float(gw * L.LM_TILE), 1.0 / float(nsub)
@@ -990,6 +1000,21 @@ class TorchBackend:
 
         cur = int(wts[L.W_CUR].item())
         w_best = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt).clone()
+        if fcfg.lm_renorm is not None and data.fmu:
+            # the k_lm_pass start-point transform (fp64 from the fp32 weights, rounded once)
+            o = spec.offsets
+            f32 = lambda v: float(np.float32(v))  # noqa: E731
+            w32 = wts[cur * L.PMAX: cur * L.PMAX + P].to(dt)
+            mu_o, isd_o = fcfg.lm_renorm
+            for j in range(spec.hidden):
+                acc = float(w32[o["b1"] + j])
+                for f in range(spec.nin):
+                    acc += float(w32[o["W1"] + f * spec.hidden + j]) * f32(isd_o[f]) * (f32(data.fmu[f]) - f32(mu_o[f]))
+                w_best[o["b1"] + j] = f32(acc)
+            for f in range(spec.nin):
+                r = f32(isd_o[f]) / f32(data.fisd[f])
+                for j in range(spec.hidden):
+                    w_best[o["W1"] + f * spec.hidden + j] = f32(float(w32[o["W1"] + f * spec.hidden + j]) * r)
         lam = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
         if float(fcfg.lm_lam_carry) > 0.0:
             lam = max(self._lm_lam_last * float(np.float32(fcfg.lm_lam_carry)), float(np.float32(t.lm_lam_min)))

@@ -90,6 +90,7 @@ class LmDesc(C.Structure):
         ("lam_max", C.c_float), ("ridge", C.c_float), ("bias_index", C.c_int), ("weights_only", C.c_int),
         ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("gram_skip", C.c_int),
         ("inst", C.c_int), ("explore", C.c_int), ("lam_carry", C.c_float), ("pad0", C.c_int), ("w0", VP),
+        ("renorm", C.c_int), ("pad1", C.c_int), ("ren_mu", C.c_float * MAXIN), ("ren_isd", C.c_float * MAXIN),
     ]
 
     def __init__(self, *a, **kw):
@@ -143,7 +144,8 @@ def _expected_layout() -> list[int]:
         C.sizeof(LmDesc), LmDesc.slab_b.offset, LmDesc.slab_g.offset, LmDesc.num_wgs.offset,
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
-        LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, L.LMS_LFIN, L.LM_SEL_W,
+        LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, LmDesc.renorm.offset,
+        LmDesc.ren_isd.offset, C.sizeof(LmDesc), L.LMS_LFIN, L.LM_SEL_W,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         L.LM_SPEC, L.LMS_SPEC_W, L.LMS_SLOTS, L.LM_SLOT, L.LSS_LBEST, L.LSS_STOP,

@@ -140,3 +140,35 @@ def test_lam_carry_starts_at_the_previous_fit_damping():
     torch.cuda.synchronize()
     lam2 = float(be._lm_buffers()["state"][L.LMS_LAM])
     assert lam2 == pytest.approx(max(lam1 * 3.0, tc.lm_lam_min), rel=1e-12)
+
+
+def test_renorm_reexpresses_the_warm_start():
+    """lm_renorm: the start point's first layer is re-expressed for the new
+    standardisation, so the network is the same function of the raw state
+    (before any trial), and the HIP transform equals the torch oracle's."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import torch_forward
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 12
+    spec, feats, pr, y, data, w0 = _setup((2, 8, 2, 0), n, dev, seed=6)
+    old = ((0.3, -0.2), (0.8, 1.7))  # (mu, isd) the start weights were fitted with
+    tc = TrainConfig(batch_size=n, lm_gram_paths=1024)
+    fc = FitConfig(epochs=0, optimizer="lm", early_stopping=False, lm_renorm=old)
+    be = HipBackend(spec, n, tc, device=dev)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, fc, seed=0)
+    torch.cuda.synchronize()
+    got = current_weights(spec, w)
+    raw = torch.stack([t.double() for t in feats], 1)
+    x_old = (raw - torch.tensor(old[0], dtype=torch.float64)) * torch.tensor(old[1], dtype=torch.float64)
+    x_new = (raw - torch.tensor(data.fmu, dtype=torch.float64)) * torch.tensor(data.fisd, dtype=torch.float64)
+    h_old = torch_forward(spec, torch.tensor(w0, dtype=torch.float64), x_old)[:, 0]
+    h_new = torch_forward(spec, torch.tensor(got, dtype=torch.float64), x_new)[:, 0]
+    np.testing.assert_allclose(h_new.numpy(), h_old.numpy(), rtol=1e-5, atol=1e-6)
+    cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
+    tb = TorchBackend(spec, n, tc)
+    wc = tb.new_weights(w0)
+    tb.fit(wc, tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
+    o_ = spec.offsets
+    np.testing.assert_array_equal(got[o_["W1"]:o_["W2"]], current_weights(spec, wc)[o_["W1"]:o_["W2"]])
