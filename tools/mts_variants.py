@@ -20,6 +20,8 @@ VARIANTS = {
     "restore_end": {"parity_flags": {"restore_best_at_end": True}},
     "adam_reset": {"parity_flags": {"carry_optimizer": False}},
     "alpha02_restore_end": {"leaky_alpha": 0.2, "parity_flags": {"restore_best_at_end": True}},
+    "unshared_q99": {"parity_flags": {"shared_q99_model": False}},
+    "blend_sign_corrected": {"parity_flags": {"holdings_blend_sign_rp": False}},
 }
 
 
