@@ -231,3 +231,54 @@ def test_dp_lm_two_ranks_matches_single_process():
     assert dp["phi"] == pytest.approx(ref.phi, rel=1e-5)
     assert dp["v0"] == pytest.approx(ref.v0, rel=1e-5)
     assert dp["pnl"] == pytest.approx(ref.terminal_pnl["std"], rel=1e-4)
+
+
+def _ms_cfg():
+    c = _lm_cfg()
+    c.train.lm_starts, c.train.lm_explore_passes, c.train.lm_explore_log2 = 3, 6, 9
+    c.train.lm_passes_first, c.train.lm_lam_carry = 4, 3.0
+    return c
+
+
+def _ms_worker(rank, world, port, out):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from rphedge.api import HedgeRun
+    from rphedge.parallel import dist as D
+
+    di = D.init(device="cpu")
+    run = HedgeRun(_ms_cfg(), dist_info=di)
+    res = run.run()
+    x = run.backend.lm_explore_last
+    with open(out + f".{rank}", "w") as f:
+        json.dump({"phi": res.phi, "v0": res.v0, "losses": x["losses"], "pick": x["pick"]}, f)
+    D.shutdown()
+
+
+def test_dp_lm_multistart_two_ranks():
+    """Multi-start exploration data parallel: every rank explores its own
+    starts on its own path prefix (no exchange), the candidates are
+    all-gathered and every rank continues from the same winner.  Rank 0's
+    candidates are the 1-process candidates (same starts, same prefix)."""
+    world, port = 2, _free_port()
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "ms.json")
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=_ms_worker, args=(r, world, port, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(240)
+            assert p.exitcode == 0
+        r0, r1 = (json.load(open(out + f".{r}")) for r in range(world))
+    assert r0 == r1                                  # same candidates, same pick, same result on both ranks
+    assert len(r0["losses"]) == 2 * 3
+    ls = np.where(np.isnan(r0["losses"]), np.inf, r0["losses"])
+    assert r0["pick"] == int(np.argmin(ls))
+    from rphedge.api import HedgeRun
+    from rphedge.parallel import dist as D
+
+    run = HedgeRun(_ms_cfg(), dist_info=D.DistInfo(device=torch.device("cpu")))
+    run.run()
+    assert run.backend.lm_explore_last["losses"] == r0["losses"][:3]

@@ -137,20 +137,34 @@ def test_missing_peer_times_out_cleanly():
     assert status.startswith("error:") and "did not arrive" in status, status
 
 
-def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None):
+def _ms_starts(spec, k):
+    from rphedge.models.hedge_mlp import init_weights
+
+    return np.stack([init_weights(spec, [0.5, 0.0], seed=1234 + 1000 * c) for c in range(k)])
+
+
+def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0, n_total=None):
     from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
     from rphedge.models.hedge_mlp import NetSpec, init_weights
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
     per = n // world
-    f, p1, y = _data(n, dev, rank * per, per)
+    f, p1, y = _data(n if n_total is None else n_total, dev, rank * per, per)
     y = y + 0.02 * torch.sin(9 * f)
     be = HipBackend(spec, per, TrainConfig(batch_size=per, lm_gram_paths=2048), device=dev, world=world,
                     rank=rank, mailbox=mailbox, lm_mailbox=lm_mailbox)
     data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f])
     w, o, fs = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
-    be.fit(w, o, fs, data, FitConfig(epochs=passes, optimizer="lm", early_stopping=False), seed=3)
+    fc = FitConfig(epochs=passes, optimizer="lm", early_stopping=False)
+    if starts:  # multi-start exploration: rank-local starts on a 2^12-path prefix, candidates all-gathered
+        fc.lm_starts, fc.lm_explore_passes, fc.lm_explore_paths = starts, 6, 1 << 12
+        fc.lm_w0s = _ms_starts(spec, starts * world)
+    be.fit(w, o, fs, data, fc, seed=3)
     torch.cuda.synchronize()
+    if starts:
+        from rphedge.ops import layout as L
+        sel = be.lm_explore_last["sel"].cpu().numpy()
+        return current_weights(spec, w), [float(sel[c * L.LM_SEL_W]) for c in range(starts * world)]
     return current_weights(spec, w), be.lm_state()
 
 
@@ -202,3 +216,53 @@ def test_lm_mailbox_exchange_two_ranks_one_gpu():
     ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0))
     assert s0 == f"{st['accepted']} {st['chol_failures']}"
     np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
+
+
+def _worker_ms(rank, world, port, n, passes, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from torch.distributed import distributed_c10d as c10d
+
+    from rphedge.ops import layout as L
+    from rphedge.ops.native import IpcMailbox
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = c10d._get_default_store()
+    mb = IpcMailbox(rank, world, 128, store, dev, tag="t_ms_a")
+    lmb = IpcMailbox(rank, world, L.LM_RED + L.LM_DP_WGS, store, dev, tag="t_ms_b")
+    dist.barrier()
+    w, losses = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb, starts=3)
+    lmb.check()
+    np.save(out + f".{rank}.npy", w)
+    np.save(out + f".{rank}.losses.npy", np.asarray(losses))
+    dist.barrier()
+    mb.close()
+    lmb.close()
+    dist.destroy_process_group()
+
+
+def test_lm_multistart_two_ranks_one_gpu():
+    """Multi-start exploration over 2 ranks: each rank explores its own 3
+    starts on its own prefix (no exchange), k_lm_select's block is all-gathered
+    through the LM mailbox (k_lm_dp_exchange) and both ranks polish the same
+    winner: bitwise-identical replicas and candidate lists; rank 0's
+    candidates are bitwise the 1-rank exploration of the same starts."""
+    n, passes, world = 1 << 15, 4, 2
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "w")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_ms, args=(r, world, port, n, passes, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+        l0, l1 = np.load(out + ".0.losses.npy"), np.load(out + ".1.losses.npy")
+    assert np.array_equal(w0, w1) and np.array_equal(l0, l1) and len(l0) == 6
+    # 1 rank, the same global paths [0, n): its prefix is rank 0's, its 3 starts rank 0's
+    _, l_ref = _lm_fit(0, 1, n // 2, passes, torch.device("cuda", 0), starts=3, n_total=n)
+    np.testing.assert_array_equal(l0[:3], np.asarray(l_ref))
