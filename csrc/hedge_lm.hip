@@ -250,57 +250,67 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 // Reduce kernel: red[e] = fixed-order sums of the slabs.
 // ---------------------------------------------------------------------------
 template <int P, int R>
-__global__ __launch_bounds__(256) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
+__global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
   using LS = LmShape<P>;
   constexpr int NG = LS::NBLK * 1024;
-  __shared__ double part[256];
+  __shared__ double part[1024];
   const int inst = blockIdx.y;  // multi-start instance
   if (pass > 0 && lm.state[(size_t)inst * LMS_FLOATS + LMS_SLOTS + LM_SLOT * (pass & 1) + LSS_STOP] != 0.0) return;
   red += (size_t)inst * LM_RED;
   const float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NG;
   const float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
+  const int tid = threadIdx.x;
   if ((int)blockIdx.x < NG / 64) {
-    // Gram: workgroup handles entries [64 b, 64 b + 64), thread (g, l) sums
-    // the slabs g, g + 4, ... of entry 64 b + l (16 loads in flight per
-    // thread for 64 slabs), the 4 partial sums combined in LDS in fixed order
-    const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+    // Gram: workgroup handles entries [64 b, 64 b + 64); thread (g, l) sums
+    // the slabs g, g + 16, ... of entry 64 b + l (every load of a 64-slab
+    // reduction in flight at once: 4 per thread), the 16 partial sums
+    // combined in LDS in fixed order
+    const int l = tid & 63, g = tid >> 6;
     const int e = blockIdx.x * 64 + l;
     const float* col = slab_g + e;
     double s0 = 0.0, s1 = 0.0;
     int w = g;
-#pragma unroll 4
-    for (; w + 4 < lm.gram_wgs; w += 8) {
+    for (; w + 16 < lm.gram_wgs; w += 32) {
       s0 += (double)col[(size_t)w * NG];
-      s1 += (double)col[(size_t)(w + 4) * NG];
+      s1 += (double)col[(size_t)(w + 16) * NG];
     }
     if (w < lm.gram_wgs) s0 += (double)col[(size_t)w * NG];
-    part[threadIdx.x] = s0 + s1;
+    part[tid] = s0 + s1;
     __syncthreads();
-    if (g == 0) red[e] = ((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) * (double)lm.inv_ns;
+    if (g == 0) {
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        a += part[q * 64 + l];
+        b += part[(q + 1) * 64 + l];
+      }
+      red[e] = (a + b) * (double)lm.inv_ns;
+    }
     return;
   }
   // gradient packet: workgroup pw handles entries [4 pw, 4 pw + 4); thread
-  // (grp, k) sums rows grp, grp + 64, ... of entry 4 pw + k (8 rows in flight
-  // at 512 workgroups), then a fixed-order LDS tree over the 64 row groups
+  // (grp, k) sums rows grp, grp + 256, ... of entry 4 pw + k (one row per
+  // thread at 256 pass workgroups), then a fixed-order LDS tree over the 256
+  // row groups
   const int pw = blockIdx.x - NG / 64;
-  const int k = threadIdx.x & 3, grp = threadIdx.x >> 2;
+  const int k = tid & 3, grp = tid >> 2;
   const int i = pw * 4 + k;
   double s0 = 0.0, s1 = 0.0;
   int w = grp;
-  for (; w + 64 < lm.num_wgs; w += 128) {
+  for (; w + 256 < lm.num_wgs; w += 512) {
     s0 += (double)slab_b[(size_t)w * R + i];
-    s1 += (double)slab_b[(size_t)(w + 64) * R + i];
+    s1 += (double)slab_b[(size_t)(w + 256) * R + i];
   }
   if (w < lm.num_wgs) s0 += (double)slab_b[(size_t)w * R + i];
-  part[threadIdx.x] = s0 + s1;
+  part[tid] = s0 + s1;
   __syncthreads();
 #pragma unroll
-  for (int st = 32; st >= 1; st >>= 1) {
-    if (grp < st) part[threadIdx.x] += part[threadIdx.x + 4 * st];
+  for (int st = 128; st >= 1; st >>= 1) {
+    if (grp < st) part[tid] += part[tid + 4 * st];
     __syncthreads();
   }
-  if (threadIdx.x < 4) {
-    const double v = part[threadIdx.x];
+  if (tid < 4) {
+    const double v = part[tid];
     if (i < P) red[LM_GBLK_MAX + i] = v;
     else if (i < P + 4) red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
   }
@@ -1286,7 +1296,7 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK)) return rc;      \
     if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs, lm->inst), dim3(256), 0, s, *lm, red_new, \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs, lm->inst), dim3(1024), 0, s, *lm, red_new, \
                        pass);                                                                   \
     return (int)hipGetLastError();                                                              \
   }
