@@ -133,8 +133,10 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     // only by this pass's reduce kernel, which runs after this one
     constexpr int NG = LmShape<P>::NBLK * 1024;
     double* best_red = st + LMS_RED;
-    for (int e = blockIdx.x * 256 + tid; e < NG + P + 4; e += (int)gridDim.x * 256) {
-      const int o = e < NG ? e : (e < NG + P ? LM_GBLK_MAX + e - NG : LM_GBLK_MAX + LM_NPMAX + e - NG - P);
+    for (int e = blockIdx.x * 256 + tid; e < NG + P + 4 + LM_OUTM; e += (int)gridDim.x * 256) {
+      const int o = e < NG ? e
+                    : (e < NG + P ? LM_GBLK_MAX + e - NG
+                                  : (e < NG + P + 4 ? LM_GBLK_MAX + LM_NPMAX + e - NG - P : LM_RED_OUTM + e - NG - P - 4));
       best_red[o] = red_new[o];
     }
   }
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 #ifdef RPH_LM_PASS_V1
   B::partial(d, 0, perm, wl, fr, scratch, pre, val);
 #else
-  B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc);
+  B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_mean != 0);
 #endif
 #pragma unroll
   for (int j = 0; j < NR; ++j)
@@ -313,6 +315,7 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     const double v = part[tid];
     if (i < P) red[LM_GBLK_MAX + i] = v;
     else if (i < P + 4) red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
+    else if (i < P + 4 + LM_OUTM) red[LM_RED_OUTM + i - P - 4] = v;  // out-means (0 where unused)
   }
 }
 
@@ -701,6 +704,75 @@ RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsig
   RPH_STAMPB(12);
 }
 
+// Exact Newton step on the OUTPUT block at the best point (the value is
+// linear in the output layer's N = out_n parameters [P - N, P), so the loss
+// is quadratic in them): 2 G_oo d = -g_o with the subsample Gram block, the
+// full-batch gradient, a Marquardt damping out_mu (relative, on the diagonal)
+// and a ridge of lm.ridge x mean diagonal.  The N x N system goes to LDS, the
+// whole workgroup eliminates it (LDL^T, one barrier per column), wave 0 runs
+// both triangular solves by v_readlane (lane i owns entry i, N <= 64), d ->
+// out[0, N).  False (nothing to apply) when a pivot is not positive.  Called
+// by workgroup 0 of the final pass only.
+template <int P>
+RPH_INLINE bool lm_out_newton(const double* src, const double* g, const int N, const float ridge, const float mu,
+                              double* A, double* out) {
+#pragma clang fp contract(off)
+  constexpr int NBG = TileGrid<P>::NBG;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int o0 = P - N, LDA = 65;
+  __shared__ double s_rid;
+  for (int e = tid; e < N * N; e += 256) {
+    const int i = e / N, j = e % N;
+    A[i * LDA + j] = 2.0 * lmc_gram<NBG>(src, o0 + i, o0 + j);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    double dg = lane < N ? A[lane * LDA + lane] : 0.0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dg += __shfl_xor(dg, o, 64);
+    if (lane == 0) s_rid = (double)ridge * dg / (double)N;
+  }
+  __syncthreads();
+  if (tid < N) {
+    const double a = A[tid * LDA + tid];
+    A[tid * LDA + tid] = (a + a * (double)mu) + s_rid;
+  }
+  __syncthreads();
+  // LDL^T elimination over the whole workgroup (lower triangle): step k
+  // subtracts A_ik A_jk / A_kk from every (i, j), k < j <= i; D_k = A_kk
+  bool ok = true;
+  for (int k = 0; k < N; ++k) {
+    const double akk = A[k * LDA + k];
+    ok = ok && akk > 0.0;
+    const double inv = lm_rcp(akk);
+    const int m = N - k - 1;
+    for (int e = tid; e < m * m; e += 256) {
+      const int i = k + 1 + e / m, j = k + 1 + e % m;
+      if (j <= i) A[i * LDA + j] -= (A[i * LDA + k] * A[j * LDA + k]) * inv;
+    }
+    __syncthreads();
+  }
+  if (tid < 64) {
+    // L z = b (L_ik = A_ik / D_k), z / D, L^T d = z: lane i holds entry i and
+    // 1 / D_i (v_rcp_f64 + one Newton step, as lm_rcp)
+    const double di = lane < N ? A[lane * LDA + lane] : 1.0;
+    const double ri = lm_rcp(di);
+    double b = lane < N ? -g[o0 + lane] : 0.0;
+    for (int k = 0; k < N; ++k) {
+      const double zk = lmc_readlane(b, k) * lmc_readlane(ri, k);  // L_ik z_k = A_ik (z_k / D_k)
+      if (lane > k && lane < N) b -= A[lane * LDA + k] * zk;
+    }
+    b *= ri;
+    for (int k = N - 1; k >= 0; --k) {
+      const double dk = lmc_readlane(b, k);
+      if (lane < k) b -= (A[k * LDA + lane] * ri) * dk;
+    }
+    if (lane < N) out[lane] = b;
+  }
+  __syncthreads();
+  return ok;
+}
+
 // Solve kernel, LM_SPEC workgroups.  Every workgroup takes the same
 // accept / reject decision from the same inputs (the scalar slot of this
 // pass's parity, which no workgroup of this launch writes: workgroup 0
@@ -833,9 +905,26 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
     if (tid == 0) st[LMS_LFIN] = accept ? Lt : Lb;
     if (lm.explore) return;  // exploration: k_lm_select publishes the chosen start point
+    // exact Newton step on the whole (linear) output layer, else on the bond bias alone
+    const int on = lm.out_n;
+    const bool out_ok = on > 0 && on <= 64 && on <= P && lm_out_newton<P>(src, g, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65);
+    if (out_ok && lm.out_mean && tid < 64) {
+      // exact mean: the value is linear in the output layer, so after the step
+      // the full-batch mean residual is m + sum_j mu_j d_j (mu = the
+      // out-means / count, m = g_bias / (2 B)); the bond bias (J = B) absorbs it
+      const double* sb = src + LM_GBLK_MAX + LM_NPMAX;
+      const double cnt = fmax(sb[3], 1.0), B = (double)d.bond;
+      double t = tid < on ? (src[LM_RED_OUTM + tid] / cnt) * lds[64 * 65 + tid] : 0.0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (tid == 0) lds[64 * 65 + on - 1] -= (g[P - 1] / (2.0 * B) + t) / B;
+    }
+    __syncthreads();
     for (int i = tid; i < P; i += 256) {
       double wd = st[LMS_W + best * LM_NPMAX + i];
-      if (i == lm.bias_index) {
+      if (out_ok) {
+        if (i >= P - on) wd += lds[64 * 65 + i - (P - on)];
+      } else if (i == lm.bias_index) {
         // exact Newton step on this bias alone (the loss is quadratic in it):
         // d = -g_i / (2 G_ii), G_ii from the diagonal 32x32 Gram block
         const int kb = i >> 5, ri = i & 31;
@@ -1125,10 +1214,12 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange(const LmDpDesc x, double
   __syncthreads();
   const unsigned seq = s_seq;
   const int slot = (int)(seq % DP_SLOTS);
-  const int len = ng + p + 4, chunk = (len + LM_DP_WGS - 1) / LM_DP_WGS;
+  const int len = ng + p + 4 + LM_OUTM, chunk = (len + LM_DP_WGS - 1) / LM_DP_WGS;
   const int e0 = wg * chunk, e1 = min(len, e0 + chunk);
   auto off = [&](int e) {  // block entry -> offset in red
-    return e < ng ? e : (e < ng + p ? LM_GBLK_MAX + e - ng : LM_GBLK_MAX + LM_NPMAX + e - ng - p);
+    return e < ng ? e
+                  : (e < ng + p ? LM_GBLK_MAX + e - ng
+                                : (e < ng + p + 4 ? LM_GBLK_MAX + LM_NPMAX + e - ng - p : LM_RED_OUTM + e - ng - p - 4));
   };
   for (int e = e0 + tid; e < e1; e += 256) {
     const double v = red[off(e)];

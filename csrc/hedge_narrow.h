@@ -200,6 +200,11 @@ struct NarrowPairBody {
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
   static_assert(R <= 256, "one packet entry per thread");
+  // out-means (free heads whose packet has room): packet slots [P + 4, P + 4 +
+  // OUTN) accumulate sum_p dV/dtheta_o (= a2_j price_k, price_k) for the
+  // exact-mean output-layer step of the LM solve (LmDesc.out_n)
+  static constexpr int OUTN = HEAD == HEAD_FREE ? H * NO + NO : 0;
+  static constexpr bool OUTM = HEAD == HEAD_FREE && P + 4 + OUTN <= R;
   struct Frags {};
   struct Pre {
     nb_f2 x[NIN], pr[NHOLD], y;
@@ -241,7 +246,8 @@ struct NarrowPairBody {
   }
 
   RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
-                                 const Frags&, float* lds, Pre& pre, float (&val)[NR], const Sched& sc) {
+                                 const Frags&, float* lds, Pre& pre, float (&val)[NR], const Sched& sc,
+                                 const bool outm = false) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long long stride = sc.bstep * 128;
     const long long jend = sc.bend * 128 < d.batch ? sc.bend * 128 : d.batch;
@@ -306,6 +312,17 @@ struct NarrowPairBody {
       g[P + 1] += ae.x + ae.y;
       g[P + 2] += ape.x + ape.y;
       g[P + 3] += m.x + m.y;
+      if constexpr (OUTM) {
+        if (outm) {  // (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          const nb_f2 mp = m * pr[k];
+          g[P + 4 + H * NO + k] += mp.x + mp.y;
+#pragma unroll
+          for (int j = 0; j < H; ++j) g[P + 4 + j * NO + k] = nb_acc(g[P + 4 + j * NO + k], a2[j], mp);
+        }
+        }
+      }
       const nb_f2 dV = e * m * two_inv;
 
       // backward

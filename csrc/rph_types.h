@@ -182,7 +182,11 @@ constexpr int LM_TILE = 64;          // Gram subsample paths per gram workgroup 
 //   G: NB(NB+1)/2 upper-triangular 32x32 blocks in MFMA register order
 //   g: gradient of mean((V - y)^2) [LM_NPMAX]; stats: loss sum, |e| sum, ape sum, count
 constexpr int LM_GBLK_MAX = 21 * 1024;
-constexpr int LM_RED = LM_GBLK_MAX + LM_NPMAX + 8;
+// + out-means: the full-batch sums of the output-layer Jacobian (sum over
+// paths of dV/dtheta_o, free-head nets whose packet has room) at LM_RED_OUTM
+constexpr int LM_OUTM = 64;
+constexpr int LM_RED_OUTM = LM_GBLK_MAX + LM_NPMAX + 8;
+constexpr int LM_RED = LM_RED_OUTM + LM_OUTM;
 // k_lm_solve workgroups of a full solve: workgroup m factorises the system at
 // the damping that m consecutive rejections would reach, so a rejection's
 // solve only publishes a step computed ahead (speculative reject branch)
@@ -271,6 +275,15 @@ struct LmDesc {
   int pad1;
   float ren_mu[MAXIN];
   float ren_isd[MAXIN];
+  // > 0: after the last pass the output layer's out_n parameters (the last
+  // ones) take the exact Newton step 2 G_oo d = -g_o (the value is linear in
+  // them); 0: only the bond bias (bias_index) does
+  int out_n;
+  float out_mu;                  // its Marquardt damping: A_ii = 2 G_ii (1 + out_mu) + ridge x mean diagonal
+  // 1: the pass packet carries the out-means (NarrowPairBody::OUTM, free heads):
+  // the bond bias then absorbs the step's full-batch mean residual exactly
+  int out_mean;
+  int pad3;
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)

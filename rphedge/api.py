@@ -235,7 +235,7 @@ class HedgeRun:
                            mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode,
                            lm_gram_paths=int(tr.lm_gram_paths), lm_damping=str(tr.lm_damping),
                            lm_lam0=float(tr.lm_lam0), lm_lam_up=float(tr.lm_lam_up),
-                           lm_lam_down=float(tr.lm_lam_down))
+                           lm_lam_down=float(tr.lm_lam_down), lm_out_fix=bool(tr.lm_out_fix))
         if int(tr.variant) >= 0:
             tcfg.variant = int(tr.variant)
         kw = {}
@@ -393,7 +393,7 @@ class HedgeRun:
             ind.opt_q.copy_(ind.opt_init)
         # the first resumed date is NOT the reference's "first" date (no LR schedule)
         orig = ind._fcfg
-        ind._fcfg = lambda first, loss: orig(False, loss)
+        ind._fcfg = lambda first, loss, t=None: orig(False, loss, t)
         try:
             ind.enqueue(start=date - 1)
         finally:

@@ -98,6 +98,8 @@ class TrainingParams:
                                      # with a larger value)
     lm_lam_carry: float = 0.0        # later dates: initial LM damping = the previous fit's final one x this
                                      # (0: off, lm_lam0 / lm_lam0_rest)
+    lm_out_fix: bool = False         # LM fits end with the exact Newton step on the whole output layer (linear
+                                     # in the value) instead of the bond bias alone
     lm_renorm: bool = False          # later dates: the warm start's first layer re-expressed for the date's input
                                      # standardisation (the previous hedge as a function of the raw state)
     lm_starts: int = 1               # first date: multi-start LM exploration, starts per rank (1: off)

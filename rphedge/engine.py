@@ -154,6 +154,10 @@ class TrainConfig:
     # pass kernel load balance: the Gram workgroups' waves take this many
     # 128-path blocks fewer than an even split (their Gram tile follows)
     lm_gram_skip: int = 3
+    # after the last pass: exact Newton step on the whole output layer (the
+    # value is linear in it; 2 G_oo d = -g_o), subsuming the bias step
+    lm_out_fix: bool = False
+    lm_out_mu: float = 1e-6        # its relative Marquardt damping (near-collinear hidden units)
     # run the data-parallel LM sequence (pass + reduce -> all-reduce of the
     # reduced block -> solve, one launch each) even on one rank: the test hook
     # that exercises the RCCL / mailbox exchange path at world size 1
@@ -215,6 +219,19 @@ def _lm_bias_index(spec, t) -> int:
     """LmDesc.bias_index: the bond holding's output bias (the last parameter of
     a free-head net), -1 for the complement head or with lm_bias_fix off."""
     return spec.nparams - 1 if (t.lm_bias_fix and spec.head == L.HEAD_FREE) else -1
+
+
+def lm_out_means(spec) -> bool:
+    """csrc/hedge_narrow.h NarrowPairBody::OUTM: the pass packet has room for
+    the full-batch out-means (free heads with P + 4 + out_n <= R)."""
+    return spec.head == L.HEAD_FREE and spec.nparams + 4 + spec.hidden * spec.nout + spec.nout <= spec.red_width
+
+
+def _lm_out_n(spec, t) -> int:
+    """LmDesc.out_n: output-layer parameters of the final exact Newton step
+    (TrainConfig.lm_out_fix; only where the out-means keep the full-batch mean
+    residual exact), 0 = the bias step alone."""
+    return spec.hidden * spec.nout + spec.nout if (t.lm_out_fix and lm_out_means(spec)) else 0
 
 
 def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
@@ -552,6 +569,8 @@ class HipBackend:
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
             lm.bias_index = _lm_bias_index(self.spec, t)
+            lm.out_n, lm.out_mu = _lm_out_n(self.spec, t), float(t.lm_out_mu)
+            lm.out_mean = 1 if lm.out_n > 0 else 0
             lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
             lm.gram_skip = int(os.environ.get("RPH_LM_GRAM_SKIP", t.lm_gram_skip))  # (env: tuning sweeps)
             bufs["desc"] = lm
@@ -632,6 +651,7 @@ class HipBackend:
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
             lm.w0 = bufs["w0"].data_ptr()
             lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
+            lm.out_n, lm.out_mean = 0, 0
             lm.num_wgs, lm.gram_wgs = nw, gw
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
             lm.inv_ns, lm.inv_n = 1.0 / float(gw * L.LM_TILE), 1.0 / float(nsub)
@@ -707,7 +727,7 @@ class HipBackend:
         def make():
             src = b["desc"]
             lm = type(src).from_buffer_copy(src)
-            lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol = 0, 1, 1, 0.0
+            lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol, lm.out_n, lm.out_mean = 0, 1, 1, 0.0, 0, 0
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
             return lm
@@ -1044,7 +1064,34 @@ class TorchBackend:
         w_best, G, g, stb, Lb, lam, hist = run(w_best, make_eval(self.n_local, W), int(fcfg.epochs), lam, tol, kmin)
         self._lm_lam_last = lam
         bi = _lm_bias_index(spec, t)
-        if bi >= 0 and float(G[bi, bi]) > 0.0:
+        n_out, out_ok = _lm_out_n(spec, t), False
+        if n_out:  # the solve kernel's output-block Newton step (lm_out_newton)
+            A = 2.0 * G[P - n_out:, P - n_out:]
+            dgA = torch.diagonal(A).clone()
+            A = A + torch.diag(dgA * float(np.float32(t.lm_out_mu))) + \
+                torch.eye(n_out, dtype=dt) * (float(np.float32(t.lm_ridge)) * float(dgA.sum()) / n_out)
+            Lc, info = torch.linalg.cholesky_ex(A)
+            if int(info) == 0:
+                dlt = torch.cholesky_solve(-g[P - n_out:, None], Lc)[:, 0]
+                # exact mean (lm_out_means): the bond bias absorbs the step's
+                # full-batch mean residual m + mean(J_o) . d
+                h, no = spec.hidden, spec.nout
+                o = spec.offsets
+                W1 = w_best[o["W1"]:o["b1"]].view(spec.nin, h)
+                a1 = torch.nn.functional.leaky_relu(X @ W1 + w_best[o["b1"]:o["W2"]], spec.alpha)
+                a2 = torch.nn.functional.leaky_relu(a1 @ w_best[o["W2"]:o["b2"]].view(h, h) + w_best[o["b2"]:o["W3"]],
+                                                    spec.alpha)
+                mu = torch.cat([(a2[:, :, None] * pr[:, None, :]).mean(0).reshape(-1), pr.mean(0)])
+                if self.world > 1:
+                    mu = mu * float(self.n_local)
+                    self._allreduce(mu)
+                    mu = mu / float(self.n_local * self.world)
+                B = float(data.bond_next)
+                dlt[-1] -= (float(g[P - 1]) / (2.0 * B) + float(mu @ dlt)) / B
+                w_best = w_best.clone()
+                w_best[P - n_out:] += dlt
+                out_ok = True
+        if not out_ok and bi >= 0 and float(G[bi, bi]) > 0.0:
             w_best = w_best.clone()
             w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
         w32 = w_best.to(torch.float32)

@@ -63,7 +63,9 @@ HESTON_EULER, HESTON_QE = 0, 1   # SimDesc.scheme (csrc/rph_types.h HestonScheme
 LM_NPMAX = 192
 LM_TILE = 64
 LM_GBLK_MAX = 21 * 1024
-LM_RED = LM_GBLK_MAX + LM_NPMAX + 8
+LM_OUTM = 64                         # full-batch sums of the output-layer Jacobian (out-means)
+LM_RED_OUTM = LM_GBLK_MAX + LM_NPMAX + 8
+LM_RED = LM_RED_OUTM + LM_OUTM
 LMS_W = 0
 LMS_RED = 2 * LM_NPMAX
 LMS_BEST = LMS_RED + 2 * LM_RED      # host mirrors of the last solve

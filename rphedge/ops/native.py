@@ -91,6 +91,7 @@ class LmDesc(C.Structure):
         ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("gram_skip", C.c_int),
         ("inst", C.c_int), ("explore", C.c_int), ("lam_carry", C.c_float), ("pad0", C.c_int), ("w0", VP),
         ("renorm", C.c_int), ("pad1", C.c_int), ("ren_mu", C.c_float * MAXIN), ("ren_isd", C.c_float * MAXIN),
+        ("out_n", C.c_int), ("out_mu", C.c_float), ("out_mean", C.c_int), ("pad3", C.c_int),
     ]
 
     def __init__(self, *a, **kw):
@@ -145,7 +146,7 @@ def _expected_layout() -> list[int]:
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
         LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, LmDesc.renorm.offset,
-        LmDesc.ren_isd.offset, C.sizeof(LmDesc), L.LMS_LFIN, L.LM_SEL_W,
+        LmDesc.ren_isd.offset, LmDesc.out_n.offset, C.sizeof(LmDesc), L.LMS_LFIN, L.LM_SEL_W,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         L.LM_SPEC, L.LMS_SPEC_W, L.LMS_SLOTS, L.LM_SLOT, L.LSS_LBEST, L.LSS_STOP,

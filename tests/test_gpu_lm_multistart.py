@@ -172,3 +172,69 @@ def test_renorm_reexpresses_the_warm_start():
     tb.fit(wc, tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
     o_ = spec.offsets
     np.testing.assert_array_equal(got[o_["W1"]:o_["W2"]], current_weights(spec, wc)[o_["W1"]:o_["W2"]])
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (5, 8, 6, 0)])
+def test_output_newton_step_matches_torch(shape):
+    """lm_out_fix: the last solve's Newton step on the output layer
+    (2 G_oo (1 + mu I) d = -g_o, lm_out_newton in one wave) at a fitted point:
+    only the output layer moves, the full-batch loss drops, and by the same
+    amount as with the fp64 torch oracle's step."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.models.hedge_mlp import torch_forward
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 13
+    spec, feats, pr, y, data, w_init = _setup(shape, n, dev, seed=7)
+    # a fitted point (at the random init the output Gram is near-singular)
+    b0 = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=2048), device=dev)
+    w1 = b0.new_weights(w_init)
+    b0.fit(w1, b0.new_opt(), b0.new_fit(), data, FitConfig(epochs=20, optimizer="lm", early_stopping=False), seed=0)
+    torch.cuda.synchronize()
+    w0 = current_weights(spec, w1)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=2048, lm_out_fix=True)
+    fc = FitConfig(epochs=0, optimizer="lm", early_stopping=False)
+    be = HipBackend(spec, n, tc, device=dev)
+    w = be.new_weights(w0)
+    be.fit(w, be.new_opt(), be.new_fit(), data, fc, seed=0)
+    torch.cuda.synchronize()
+    got = current_weights(spec, w)
+    cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
+    tb = TorchBackend(spec, n, tc)
+    wc = tb.new_weights(w0)
+    tb.fit(wc, tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
+    want = current_weights(spec, wc)
+    n_out = spec.hidden * spec.nout + spec.nout
+    np.testing.assert_array_equal(got[:-n_out], w0[:-n_out])
+    assert not np.array_equal(got[-n_out:], w0[-n_out:])
+
+    def loss(wv):
+        X = (torch.stack([f.double() for f in feats], 1) - torch.tensor(data.fmu, dtype=torch.float64)) * \
+            torch.tensor(data.fisd, dtype=torch.float64)
+        P = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
+        return float((((torch_forward(spec, torch.tensor(wv, dtype=torch.float64), X) * P).sum(1) - y.double()) ** 2).mean())
+    # the fitted values (not the weights: near-collinear hidden units leave
+    # near-null directions that the fp32 Gram resolves differently) agree
+    l0, lg, lt = loss(w0), loss(got), loss(want)
+    assert lg < l0 and lt < l0
+    assert abs(lg - lt) <= 2e-2 * (l0 - lt), (l0, lg, lt)
+
+    def mean_res(wv):
+        X = (torch.stack([f.double() for f in feats], 1) - torch.tensor(data.fmu, dtype=torch.float64)) * \
+            torch.tensor(data.fisd, dtype=torch.float64)
+        P = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
+        return float(((torch_forward(spec, torch.tensor(wv, dtype=torch.float64), X) * P).sum(1) - y.double()).mean())
+    # the out-means keep the full-batch mean residual exact (as the bias step did)
+    assert abs(mean_res(got)) < 1e-4 * float(y.double().abs().mean()) + 1e-6, mean_res(got)
+
+
+def test_output_newton_step_needs_out_means():
+    """Nets whose pass packet has no room for the out-means (complement head,
+    the 2-4 input 8-unit nets) keep the bias step: lm_out_fix is off there."""
+    from rphedge.engine import TrainConfig, _lm_out_n, lm_out_means
+    from rphedge.models.hedge_mlp import NetSpec
+
+    tc = TrainConfig(lm_out_fix=True)
+    assert lm_out_means(NetSpec(1, 8, 2, 0)) and lm_out_means(NetSpec(5, 8, 6, 0))
+    for shp in [(1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0)]:
+        assert _lm_out_n(NetSpec(*shp), tc) == 0

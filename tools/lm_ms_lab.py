@@ -118,7 +118,19 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
         w_best, G, g, Lb, lam, hist, nacc = lm_core(spec, t, w0, X, pr, y, t.lm_gram_paths, int(fcfg.epochs), lam,
                                                     tol=0.0 if first else fl.get("adapt", 0.0))
     bi = E._lm_bias_index(spec, t)
-    if bi >= 0 and float(G[bi, bi]) > 0.0:
+    if "outfix" in fl:
+        # exact Newton step on the whole (linear) output layer at the final
+        # point: 2 G_oo d = -g_o (Gram of the subsample, full-batch gradient)
+        P_ = spec.nparams
+        n_out = spec.hidden * spec.nout + spec.nout
+        oi = torch.arange(P_ - n_out, P_)
+        Goo = G[oi][:, oi]
+        mu = fl.get("ofmu", 0.0)
+        A = 2.0 * Goo + torch.diag(2.0 * Goo.diagonal() * mu) + 1e-10 * torch.eye(n_out, dtype=G.dtype) * Goo.diagonal().mean()
+        dlt = torch.linalg.solve(A, -g[oi])
+        w_best = w_best.clone()
+        w_best[oi] += fl["outfix"] * dlt
+    elif bi >= 0 and float(G[bi, bi]) > 0.0:
         w_best = w_best.clone()
         w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
     w32 = w_best.to(torch.float32)
@@ -142,7 +154,7 @@ def parse_flags(v):
     for f in v.split("+"):
         if f == "base":
             continue
-        for key in ("ms_n1", "ms_n2", "ms_sub", "ms", "carry", "lf", "adapt"):
+        for key in ("ms_n1", "ms_n2", "ms_sub", "ms", "carry", "lf", "adapt", "outfix", "ofmu"):
             if f.startswith(key):
                 out[key] = float(f[len(key):].lstrip("="))
                 break
