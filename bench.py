@@ -67,7 +67,7 @@ METRIC = "MC paths/sec training 30-step hedge-MLP + terminal P&L std-dev, 1/2/4/
 PRESETS = {
     "euro30": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                    batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="lm",
-                   lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0,
+                   lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
     "euro30_adam": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="adam",
@@ -79,12 +79,12 @@ PRESETS = {
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
-                    optimizer="lm", lm_passes_first=120, lm_passes_rest=2, lm_lam_carry=3.0,
+                    optimizer="lm", lm_passes_first=120, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                     label="European call, 252-step GBM, 2M paths per GPU (16M at 8 GPUs)"),
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
                     extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
-                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0,
+                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                     label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
     "euro30_mfma": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-3, lr_rest=1e-3, lr_decay=0.1, hidden=32,

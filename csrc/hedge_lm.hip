@@ -907,7 +907,9 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     if (lm.explore) return;  // exploration: k_lm_select publishes the chosen start point
     // exact Newton step on the whole (linear) output layer, else on the bond bias alone
     const int on = lm.out_n;
-    const bool out_ok = on > 0 && on <= 64 && on <= P && lm_out_newton<P>(src, g, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65);
+    // (the best point was evaluated by an out-means pass: its bond entry = count x B > 0)
+    const bool have_om = on > 0 && on <= 64 && on <= P && (!lm.out_mean || src[LM_RED_OUTM + on - 1] > 0.0);
+    const bool out_ok = have_om && lm_out_newton<P>(src, g, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65);
     if (out_ok && lm.out_mean && tid < 64) {
       // exact mean: the value is linear in the output layer, so after the step
       // the full-batch mean residual is m + sum_j mu_j d_j (mu = the
@@ -1150,6 +1152,8 @@ struct LmKernels {
   using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
 #else
   using Body = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1>;  // two paths per lane, packed fp32
+  // the same body accumulating the out-means (the last passes of an lm_out_fix fit)
+  using BodyOM = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true>;
 #endif
   using S = NetShape<NIN, H, NO, HEAD>;
 #ifndef RPH_LM_CHOL_V1
@@ -1190,6 +1194,16 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
 template <int A, int B, int C, int E>
 static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const double* red_new, hipStream_t s) {
   using K = LmKernels<A, B, C, E>;
+#ifndef RPH_LM_PASS_V1
+  if constexpr (K::BodyOM::OUTM) {
+    // the last LM_OUTM_TAIL evaluations of an lm_out_fix fit carry the out-means
+    if (lm->out_mean && pass > lm->passes - LM_OUTM_TAIL) {
+      hipLaunchKernelGGL((k_lm_pass<typename K::BodyOM>), dim3(lm->num_wgs, lm->inst), dim3(256), 0, s, *d, *lm,
+                         pass, red_new);
+      return (int)hipGetLastError();
+    }
+  }
+#endif
   hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs, lm->inst), dim3(256), 0, s, *d, *lm, pass,
                      red_new);
   return (int)hipGetLastError();

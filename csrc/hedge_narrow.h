@@ -189,7 +189,7 @@ RPH_INLINE nb_f2 nb_lrelu_bwd(nb_f2 a, nb_f2 da, float alpha) {
 // g += a.x * b.x + a.y * b.y (the pair's contribution to one gradient entry)
 RPH_INLINE float nb_acc(float g, nb_f2 a, nb_f2 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, g)); }
 
-template <int NIN, int H, int NO, int HEAD, int WPS = 2>
+template <int NIN, int H, int NO, int HEAD, int WPS = 2, bool OM = false>
 struct NarrowPairBody {
   static constexpr int WAVES_PER_SIMD = WPS;  // 2: two workgroups per CU (the 512-workgroup LM pass grid)
   static constexpr int NIN_ = NIN, H_ = H, NO_ = NO, HEAD_ = HEAD;
@@ -204,7 +204,8 @@ struct NarrowPairBody {
   // OUTN) accumulate sum_p dV/dtheta_o (= a2_j price_k, price_k) for the
   // exact-mean output-layer step of the LM solve (LmDesc.out_n)
   static constexpr int OUTN = HEAD == HEAD_FREE ? H * NO + NO : 0;
-  static constexpr bool OUTM = HEAD == HEAD_FREE && P + 4 + OUTN <= R;
+  static constexpr bool FITS_OUTM = HEAD == HEAD_FREE && P + 4 + OUTN <= R;
+  static constexpr bool OUTM = OM && FITS_OUTM;  // (its own kernel: the extra sums cost registers)
   struct Frags {};
   struct Pre {
     nb_f2 x[NIN], pr[NHOLD], y;
@@ -313,7 +314,7 @@ struct NarrowPairBody {
       g[P + 2] += ape.x + ape.y;
       g[P + 3] += m.x + m.y;
       if constexpr (OUTM) {
-        if (outm) {  // (wave-uniform)
+        if (outm) {
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
           const nb_f2 mp = m * pr[k];

@@ -185,6 +185,7 @@ constexpr int LM_GBLK_MAX = 21 * 1024;
 // + out-means: the full-batch sums of the output-layer Jacobian (sum over
 // paths of dV/dtheta_o, free-head nets whose packet has room) at LM_RED_OUTM
 constexpr int LM_OUTM = 64;
+constexpr int LM_OUTM_TAIL = 3;  // evaluations of an lm_out_fix fit that carry them: passes - 2 .. passes
 constexpr int LM_RED_OUTM = LM_GBLK_MAX + LM_NPMAX + 8;
 constexpr int LM_RED = LM_RED_OUTM + LM_OUTM;
 // k_lm_solve workgroups of a full solve: workgroup m factorises the system at

@@ -982,6 +982,7 @@ class TorchBackend:
             G, g, stb = evaluate(w_best)
             Lb = float(stb[0] / stb[3].clamp_min(1.0))
             hist = [Lb]
+            self._lm_best_k = 0  # the evaluation the best point came from
             for k in range(1, int(passes) + 1):
                 Lb_old = Lb
                 A = 2.0 * G
@@ -1008,6 +1009,7 @@ class TorchBackend:
                     else:
                         lam = max(lam * t.lm_lam_down, t.lm_lam_min)
                     w_best, G, g, stb, Lb = trial, Gt, gt, stt, Lt
+                    self._lm_best_k = k
                 elif nielsen:
                     lam = min(lam * nu, t.lm_lam_max)
                     nu *= 2.0
@@ -1065,7 +1067,9 @@ class TorchBackend:
         self._lm_lam_last = lam
         bi = _lm_bias_index(spec, t)
         n_out, out_ok = _lm_out_n(spec, t), False
-        if n_out:  # the solve kernel's output-block Newton step (lm_out_newton)
+        # (only when the best point came from an out-means pass: the last
+        # LM_OUTM_TAIL evaluations, k_lm_pass<BodyOM>)
+        if n_out and self._lm_best_k > int(fcfg.epochs) - L.LM_OUTM_TAIL:  # the solve kernel's lm_out_newton
             A = 2.0 * G[P - n_out:, P - n_out:]
             dgA = torch.diagonal(A).clone()
             A = A + torch.diag(dgA * float(np.float32(t.lm_out_mu))) + \

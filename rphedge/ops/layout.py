@@ -64,6 +64,7 @@ LM_NPMAX = 192
 LM_TILE = 64
 LM_GBLK_MAX = 21 * 1024
 LM_OUTM = 64                         # full-batch sums of the output-layer Jacobian (out-means)
+LM_OUTM_TAIL = 3                     # the last evaluations of an lm_out_fix fit carry them
 LM_RED_OUTM = LM_GBLK_MAX + LM_NPMAX + 8
 LM_RED = LM_RED_OUTM + LM_OUTM
 LMS_W = 0
