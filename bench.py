@@ -62,12 +62,18 @@ BASELINE_PATHS_PER_S = 4096.0 / ((500 + 29 * (1404 - 500) / 51) * 8 * 0.006)
 METRIC = "MC paths/sec training 30-step hedge-MLP + terminal P&L std-dev, 1/2/4/8 MI355X"
 
 
+LAM0_FIRST = 16.384000778198242  # float32(1e-3) * 4**7 (exact in fp32)
+
 # BASELINE.json configs -> (model, dates, Euler substeps per date, paths per GPU log2, epochs first/rest,
 # per-GPU batch log2, lr first/rest, extra RunConfig fields)
 PRESETS = {
     "euro30": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                    batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="lm",
-                   lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                   # first date: start at the damping of the first trial the round-3 sequence
+                   # (lam0 1e-3, x4 per rejection) could accept, fp32(1e-3) x 4^7: its 7
+                   # rejected trials are skipped, the rest of the trajectory is unchanged
+                   lm_lam0_first=LAM0_FIRST, lm_passes_first=73,
+                   lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
     "euro30_adam": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="adam",
@@ -129,6 +135,7 @@ def parse(argv=None):
                     help="later dates: adaptive LM pass budget (relative best-loss gain that ends a fit; 0: off)")
     ap.add_argument("--lm-stop-min", type=int, default=None)
     ap.add_argument("--lm-lam0-rest", type=float, default=None, help="later dates' initial LM damping (0: --lm-lam0)")
+    ap.add_argument("--lm-lam0-first", type=float, default=None, help="first date's initial LM damping (0: --lm-lam0)")
     ap.add_argument("--lm-lam-carry", type=float, default=None,
                     help="later dates start at the previous fit's final LM damping x this (0: off)")
     ap.add_argument("--lm-starts", type=int, default=None, help="first date: multi-start LM exploration (1: off)")
@@ -160,7 +167,8 @@ def parse(argv=None):
         a.init = pre.get("init", "reference")
     for k, dflt in (("lm_passes_first", 80), ("lm_passes_rest", 3), ("lm_gram_paths", 4096),
                     ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0),
-                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam_carry", 0.0),
+                    ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam0_first", 0.0),
+                    ("lm_lam_carry", 0.0),
                     ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16), ("lm_renorm", 0), ("lm_out_fix", 0)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
@@ -181,7 +189,8 @@ def build_run(a, world: int):
                         optimizer=a.optimizer, lm_passes_first=a.lm_passes_first, lm_passes_rest=a.lm_passes_rest,
                         lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping, lm_lam0=a.lm_lam0,
                         lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down, lm_stop_tol=a.lm_stop_tol,
-                        lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, init=a.init,
+                        lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, lm_lam0_first=a.lm_lam0_first,
+                        init=a.init,
                         lm_lam_carry=a.lm_lam_carry, lm_starts=a.lm_starts, lm_explore_passes=a.lm_explore_passes,
                         lm_explore_log2=a.lm_explore_log2, lm_renorm=bool(a.lm_renorm), lm_out_fix=bool(a.lm_out_fix))
     model = pre["model"]
@@ -289,6 +298,17 @@ def lm_fit_stats(ind) -> dict:
         first["best_loss"] = best[-1] if best else None
     return {"passes_per_date": passes, "accepted_per_date": acc, "acceptance_rate": sum(acc) / tot,
             "first_date": first}
+
+
+def lm_exchange_record(run, passes: int, world: int) -> dict:
+    """Data-parallel LM exchange volume: every rank builds the same Gram
+    matrix from the simulated global subsample, so one pass pushes only the
+    gradient region [g | stats | out-means] to each peer."""
+    per_peer = int(run.backend.lm_exchange_bytes())
+    return {"bytes_per_pass_per_peer": per_peer, "peers": world - 1,
+            "bytes_per_pass_per_rank": per_peer * (world - 1),
+            "bytes_per_run_per_rank": per_peer * (world - 1) * int(passes),
+            "same_gram_every_rank": bool(run.backend._lm_same_gram)}
 
 
 def multistart_record(run, a, world: int) -> dict:
@@ -438,7 +458,8 @@ def main(argv=None):
                    "lm_gram_paths": a.lm_gram_paths if lm else None,
                    "lm_damping": a.lm_damping if lm else None,
                    "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
-                   "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None, "init": a.init,
+                   "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None,
+                   "lm_lam0_first": (a.lm_lam0_first or None) if lm else None, "init": a.init,
                    "lm_stop": [a.lm_stop_tol, a.lm_stop_min] if (lm and a.lm_stop_tol > 0) else None,
                    "lm_lam_carry": (a.lm_lam_carry or None) if lm else None,
                    "lm_renorm": bool(a.lm_renorm) if lm else None,
@@ -463,6 +484,7 @@ def main(argv=None):
                     "mc_discounted_payoff": res.summary["E_payoff"] * run.scale * math.exp(-cfg.r * cfg.T),
                     "reference_terminal_residual_std_52step": 1.7504, "reference_V0": 11.352},
         "lm": lm_stats,
+        "lm_exchange": lm_exchange_record(run, passes, world) if (lm and not a.cpu) else None,
         "memory": memory,
         "path_samples_per_s": path_samples, "full_passes_per_run": passes,
         "path_samples_vs_keras": path_samples / BASELINE_SAMPLES_PER_S,

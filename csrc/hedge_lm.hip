@@ -94,13 +94,12 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   // slot 0); later passes = the slot k_lm_solve wrote
   const int trial = pass == 0 ? 0 : 1 - (int)sl[LSS_BEST];
   const Perm perm = make_perm(1u, 0u, 0u, false);
+  // workgroups [num_wgs, grid) only add a Gram tile (a Gram subsample larger
+  // than 64 x the path grid: the subsample is the same at every world size)
+  const bool path_wg = (int)blockIdx.x < lm.num_wgs;
   typename B::Pre pre;
-#ifdef RPH_LM_PASS_V1
-  B::load(d, 0, perm, B::first(wid), lane, pre);
-#else
-  const typename B::Sched sc = B::sched(d, lm.gram_wgs, lm.gram_skip);
-  B::load(d, 0, perm, sc.b0 * 128, lane, pre);
-#endif
+  const typename B::Sched sc = B::sched(d, lm.num_wgs, lm.gram_wgs, lm.gram_skip);
+  if (path_wg) B::load(d, 0, perm, sc.b0 * 128, lane, pre);
   for (int i = tid; i < P; i += 256) {
     float w;
     if (pass == 0) {
@@ -161,30 +160,39 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   __syncthreads();
   RPH_STAMPP(1);
   // ---- loss + exact gradient over every local path (VALU) -------------------
-  typename B::Frags fr;
-  B::make_frags(wl + S::OW2, fr);
-  float val[NR];
-#ifdef RPH_LM_PASS_V1
-  B::partial(d, 0, perm, wl, fr, scratch, pre, val);
-#else
-  B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_mean != 0);
-#endif
+  if (path_wg) {
+    typename B::Frags fr;
+    B::make_frags(wl + S::OW2, fr);
+    float val[NR];
+    B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_mean != 0);
 #pragma unroll
-  for (int j = 0; j < NR; ++j)
-    if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
+    for (int j = 0; j < NR; ++j)
+      if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
+  }
   RPH_STAMPP(2);
   if ((int)blockIdx.x >= lm.gram_wgs) return;
   // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
   if (wid == 0) {
     const long long slot = (long long)blockIdx.x * LM_TILE + lane;
-    const long long p = (slot / lm.gram_blk) * lm.gram_blk_stride + slot % lm.gram_blk;
-    const bool ok = p < d.n_local;
-    const long long q = ok ? p : 0;
     float x[NIN], pr[NHOLD];
+    bool ok;
+    if (lm.gram_side) {
+      // the global subsample, simulated on this rank (slot order): every rank
+      // builds the same Gram matrix
+      ok = true;
 #pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = (d.feat[f][q] - d.fmu[f]) * d.fisd[f];
+      for (int f = 0; f < NIN; ++f) x[f] = (lm.gfeat[f][slot] - d.fmu[f]) * d.fisd[f];
 #pragma unroll
-    for (int k = 0; k < NHOLD - 1; ++k) pr[k] = d.price[k][q];
+      for (int k = 0; k < NHOLD - 1; ++k) pr[k] = lm.gprice[k][slot];
+    } else {
+      const long long p = (slot / lm.gram_blk) * lm.gram_blk_stride + slot % lm.gram_blk;
+      ok = p < d.n_local;
+      const long long q = ok ? p : 0;
+#pragma unroll
+      for (int f = 0; f < NIN; ++f) x[f] = (d.feat[f][q] - d.fmu[f]) * d.fisd[f];
+#pragma unroll
+      for (int k = 0; k < NHOLD - 1; ++k) pr[k] = d.price[k][q];
+    }
     pr[NHOLD - 1] = d.bond;
     float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
     net_forward<NIN, H, NO, HEAD>(wl, x, d.alpha, z1, a1, z2, a2, hold);
@@ -324,19 +332,6 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
 // red_new: the reduced block of the trial just evaluated (all-reduced when
 // data parallel); the state keeps the best point's block.
 // ---------------------------------------------------------------------------
-RPH_INLINE int lm_tri(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower triangle, j <= i
-
-// LDS storage of the fp64 system matrix (lower triangle used): dense with an
-// odd pitch up to 128 parameters (no index arithmetic in the inner loops),
-// packed lower-triangular above (the 160 KB LDS holds 191 x 192 / 2 doubles)
-template <int P>
-struct LmSys {
-  static constexpr bool DENSE = P <= 128;
-  static constexpr int LD = P + 1;
-  static constexpr int ELEMS = DENSE ? P * LD : P * (P + 1) / 2;
-  RPH_INLINE static int idx(int i, int j) { return DENSE ? i * LD + j : lm_tri(i, j); }
-};
-
 // fp64 reciprocal / reciprocal square root from the hardware approximations
 // (v_rcp_f64 / v_rsq_f64, max rel. error 4.6e-8 / 5.2e-8 on gfx950) + ONE
 // Newton step: 2.2e-15 / 4.0e-15 (tools/micro/rsq_prec.hip); the IEEE division
@@ -349,136 +344,6 @@ RPH_INLINE double lm_rsq(double x) {
   const double y = __builtin_amdgcn_rsq(x);
   return y * __builtin_fma(-0.5 * x * y, y, 1.5);
 }
-
-// Both triangular solves L y = b, L^T d = y of the LM system in ONE wave (no
-// barriers), blocked by 8 columns: lane l keeps the right-hand side of rows
-// l, l + 64, l + 128 in registers; per block the 8 current entries are
-// gathered to every lane with v_readlane, the 8 x 8 diagonal block is solved
-// redundantly on every lane (its L entries are LDS broadcasts), then every
-// lane applies the block to its own rows (8 independent products, tree sum).
-// rdg = reciprocal pivots.  The solution replaces vec.
-template <int P, class SY, bool FWD = true>
-RPH_INLINE void lm_tri_solve_wave(const double* A, double* vec, const double* rdg) {
-  static_assert(P <= 192, "three rows per lane");
-  constexpr int NS = (P + 63) / 64, NB = (P + 7) / 8;
-  const int lane = threadIdx.x & 63;
-  double b[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) b[s] = lane + 64 * s < P ? vec[lane + 64 * s] : 0.0;
-  auto bcast = [](double v, int l) -> double {
-    const unsigned long long u = __double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-  };
-  auto slot = [&](int sK) -> double {  // b[sK] for a wave-uniform sK
-    double v = b[0];
-#pragma unroll
-    for (int s = 1; s < NS; ++s) v = sK == s ? b[s] : v;
-    return v;
-  };
-  // ---- forward: L y = b --------------------------------------------------------
-  for (int K = 0; K < (FWD ? NB : 0); ++K) {
-    const int k0 = 8 * K, sK = k0 >> 6, l0 = k0 & 63;
-    double lr[NS][8];  // this lane's rows of the block's columns (independent of the chain)
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int row = lane + 64 * s;
-        lr[s][c] = (row >= k0 + 8 && row < P && k0 + c < P) ? A[SY::idx(row, k0 + c)] : 0.0;
-      }
-    const double bs = slot(sK);
-    double y[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      double v = bcast(bs, l0 + c);
-#pragma unroll
-      for (int q = 0; q < c; ++q) v = __builtin_fma(-A[SY::idx(k0 + c, k0 + q)], y[q], v);
-      y[c] = k0 + c < P ? v * rdg[k0 + c] : 0.0;
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const double t01 = __builtin_fma(lr[s][1], y[1], lr[s][0] * y[0]);
-      const double t23 = __builtin_fma(lr[s][3], y[3], lr[s][2] * y[2]);
-      const double t45 = __builtin_fma(lr[s][5], y[5], lr[s][4] * y[4]);
-      const double t67 = __builtin_fma(lr[s][7], y[7], lr[s][6] * y[6]);
-      b[s] -= (t01 + t23) + (t45 + t67);
-      if (s == sK) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) b[s] = lane == l0 + c ? y[c] : b[s];
-      }
-    }
-  }
-  // ---- backward: L^T d = y -----------------------------------------------------
-  for (int K = NB - 1; K >= 0; --K) {
-    const int k0 = 8 * K, sK = k0 >> 6, l0 = k0 & 63;
-    double lr[NS][8];  // L[k0 + c][row] for this lane's rows below k0
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int row = lane + 64 * s;
-        lr[s][c] = (row < k0 && k0 + c < P) ? A[SY::idx(k0 + c, row)] : 0.0;
-      }
-    const double bs = slot(sK);
-    double dv[8];
-#pragma unroll
-    for (int c = 7; c >= 0; --c) {
-      double v = bcast(bs, l0 + c);
-#pragma unroll
-      for (int q = 7; q > c; --q)
-        if (k0 + q < P) v = __builtin_fma(-A[SY::idx(k0 + q, k0 + c)], dv[q], v);
-      dv[c] = k0 + c < P ? v * rdg[k0 + c] : 0.0;
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const double t01 = __builtin_fma(lr[s][1], dv[1], lr[s][0] * dv[0]);
-      const double t23 = __builtin_fma(lr[s][3], dv[3], lr[s][2] * dv[2]);
-      const double t45 = __builtin_fma(lr[s][5], dv[5], lr[s][4] * dv[4]);
-      const double t67 = __builtin_fma(lr[s][7], dv[7], lr[s][6] * dv[6]);
-      b[s] -= (t01 + t23) + (t45 + t67);
-      if (s == sK) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) b[s] = lane == l0 + c ? dv[c] : b[s];
-      }
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-    if (lane + 64 * s < P) vec[lane + 64 * s] = b[s];
-}
-
-#define RPH_STAMPB(k)                                                                         \
-  do {                                                                                      \
-    if (stamps != nullptr && threadIdx.x == 0)                                              \
-      stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();              \
-  } while (0)
-
-// Tiles of the trailing-matrix register state of lm_chol_solve_blocked: the
-// lower triangle of the padded matrix in 16 x 16 tiles, ordered by column
-// block then row block, dealt round-robin to the 4 waves (the tiles still
-// active at panel K are a suffix of that order, so the waves stay balanced).
-template <int P>
-struct CholTiles {
-  static constexpr int PB = (P + 7) / 8 * 8;
-  static constexpr int NT = (PB + 15) / 16;
-  static constexpr int NTILE = NT * (NT + 1) / 2;
-  static constexpr int TPW = (NTILE + 3) / 4;
-  static constexpr int RWX = 16 * NT > PB ? 16 * NT : PB + 1;  // LDS rows: tile grid + the rhs row PB
-  static constexpr int col(int t) {
-    int b = 0;
-    while (t >= NT - b) t -= NT - b++;
-    return b;
-  }
-  static constexpr int row(int t) {
-    int b = 0;
-    while (t >= NT - b) t -= NT - b++;
-    return b + t;
-  }
-};
-
-typedef double lm_d4 __attribute__((ext_vector_type(4)));
 
 // compile-time unrolled loop: f(std::integral_constant<int, j>) for j in [0, N)
 template <class F, int... J>
@@ -493,216 +358,6 @@ RPH_INLINE void lm_static_for(F&& f) {
 }  // namespace rph
 #include "lm_chol.h"
 namespace rph {
-
-// Trailing-matrix tiles of wave W (tile ownership is a compile-time function
-// of W, so every tile and fragment index is a static register index):
-// load from A, rank-8 update on the fp64 matrix cores, publish of the next
-// panel's columns.  Entries left of / above the active trailing block get
-// updated with stale operands but are dead (L is already in A; phase 1 reads
-// only rows >= k0).
-template <int P, class SY, int W>
-struct CholWave {
-  using CT = CholTiles<P>;
-  static constexpr int TPW = CT::TPW;
-  RPH_INLINE static void load(lm_d4* C, const double* A, int lr, int lq) {
-    lm_static_for<TPW>([&](auto jc) {
-      constexpr int j = decltype(jc)::value, t = W + 4 * j;
-      if constexpr (t < CT::NTILE) {
-        constexpr int ib = CT::row(t), jb = CT::col(t);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = 16 * ib + lq + 4 * r, jj = 16 * jb + lr;
-          C[j][r] = (i < P && jj <= i) ? A[SY::idx(i, jj)] : ((i == jj && i < CT::PB) ? 1.0 : 0.0);
-        }
-      }
-    });
-  }
-  // C -= U U^T over the active tiles (column block >= bk), U = uL (two
-  // v_mfma_f64_16x16x4_f64 per tile: K = 8), then the owners of column block
-  // bk write the next panel's columns [off, off + 8) to cn
-  RPH_INLINE static void update(lm_d4* C, const double (*fu)[2], int bk, int off, double (*cn)[CT::RWX], int lr,
-                                int lq) {
-    lm_static_for<TPW>([&](auto jc) {
-      constexpr int j = decltype(jc)::value, t = W + 4 * j;
-      if constexpr (t < CT::NTILE) {
-        constexpr int ib = CT::row(t), jb = CT::col(t);
-        if (jb >= bk) {
-          C[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-fu[ib][0], fu[jb][0], C[j], 0, 0, 0);
-          C[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-fu[ib][1], fu[jb][1], C[j], 0, 0, 0);
-        }
-      }
-    });
-    lm_static_for<TPW>([&](auto jc) {
-      constexpr int j = decltype(jc)::value, t = W + 4 * j;
-      if constexpr (t < CT::NTILE) {
-        constexpr int ib = CT::row(t), jb = CT::col(t);
-        if (jb == bk && lr >= off && lr < off + 8) {
-          // rows >= PB are padding of the tile grid; row PB of the panel is the
-          // right-hand side, written by its own threads (rb): never from a tile
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (16 * ib + lq + 4 * r < CT::PB) cn[lr - off][16 * ib + lq + 4 * r] = C[j][r];
-        }
-      }
-    });
-  }
-};
-
-// Panel loop of the blocked Cholesky.  Per panel of 8 columns:
-//   phase 1: row threads t in [k0, PB) factor the 8 x 8 diagonal block
-//            (redundantly, from the LDS-broadcast panel) and solve their L21
-//            row -> uL (LDS) and A;
-//   phase 2: every wave's rank-8 trailing update on the matrix cores
-//            (CholWave), the next panel's columns published (colb,
-//            double-buffered).
-// Phase 1 is one copy of code for all waves; only the small tile code is
-// per-wave (one kernel body fits the instruction cache).
-template <int P, class SY>
-RPH_INLINE void lm_chol_factor(double* A, double* vec, int* s_fail, double (*colb)[CholTiles<P>::RWX],
-                               double (*uL)[9], unsigned long long* stamps) {
-  using CT = CholTiles<P>;
-  constexpr int PB = CT::PB, NK = PB / 8, NT = CT::NT, TPW = CT::TPW;
-  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
-  lm_d4 C[TPW];
-  switch (wid) {
-    case 0: CholWave<P, SY, 0>::load(C, A, lr, lq); break;
-    case 1: CholWave<P, SY, 1>::load(C, A, lr, lq); break;
-    case 2: CholWave<P, SY, 2>::load(C, A, lr, lq); break;
-    default: CholWave<P, SY, 3>::load(C, A, lr, lq); break;
-  }
-  // the right-hand side rides along as row PB of the factorization (its L21
-  // row is y = L^-1 b): thread j < PB keeps element (PB, j) in a register and
-  // applies the rank-8 updates on the VALU
-  double rb = tid < P ? vec[tid] : 0.0;
-  for (int K = 0; K < NK; ++K) {
-    const int k0 = 8 * K;
-    __syncthreads();
-    if (K == 6) RPH_STAMPB(8);
-    const double(*cb)[CT::RWX] = colb;  // single buffer: phase 2 overwrites it after the barrier
-    // ---- phase 1: row threads t in [k0, PB]: diagonal block + L21 row ----------
-    // (thread PB is the right-hand side: its "L21 row" is y = L^-1 b)
-    if (tid >= k0 && tid <= PB) {
-      double L[8][8], rl[8], u[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) u[c] = cb[c][tid];  // this row's panel entries (latency under the diag chain)
-      bool ok = true;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        double sc = cb[c][k0 + c];
-#pragma unroll
-        for (int p = 0; p < c; ++p) sc -= L[c][p] * L[c][p];
-        ok = ok && sc > 0.0;
-        rl[c] = lm_rsq(sc);  // 1 / L_cc
-        L[c][c] = sc * rl[c];
-#pragma unroll
-        for (int r = c + 1; r < 8; ++r) {
-          double v = cb[c][k0 + r];
-#pragma unroll
-          for (int p = 0; p < c; ++p) v -= L[r][p] * L[c][p];
-          L[r][c] = v * rl[c];
-        }
-      }
-      if (!ok && tid == k0) *s_fail = 1;
-      const int i = tid;
-      if (i >= k0 + 8) {
-        // the row's 8 panel entries are read BEFORE any store (the stores to
-        // uL / A may alias the panel for the compiler, which would otherwise
-        // wait out one LDS round trip per column)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          double v = u[c];
-#pragma unroll
-          for (int p = 0; p < c; ++p) v -= u[p] * L[c][p];
-          u[c] = v * rl[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 8; ++c) uL[i][c] = u[c];
-        if (i < P) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c)
-            if (k0 + c < P) A[SY::idx(i, k0 + c)] = u[c];
-        } else if (i == PB) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c)
-            if (k0 + c < P) vec[k0 + c] = u[c];  // forward solve, free
-        }
-      } else if (i < P) {
-        const int rr = i - k0;
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          if (r == rr) {
-#pragma unroll
-            for (int c = 0; c <= r; ++c)
-              if (k0 + c < P) A[SY::idx(i, k0 + c)] = L[r][c];
-          }
-      }
-    }
-    __syncthreads();
-    if (K == 6) RPH_STAMPB(9);
-    // (a non-positive pivot only poisons the rest with NaNs: checked once after
-    // the loop, not with an LDS round trip per panel)
-    // ---- phase 2: rank-8 update of the trailing tiles on the matrix cores -------
-    const int kn = k0 + 8;
-    if (kn >= PB) break;
-    const int bk = kn >> 4, off = kn & 15;
-    double fu[NT][2];  // lane (lr, lq): U[16 X + lr][4 s + lq]
-#pragma unroll
-    for (int X = 0; X < NT; ++X)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) fu[X][s2] = uL[16 * X + lr][4 * s2 + lq];
-    double(*cn)[CT::RWX] = colb;
-    switch (wid) {
-      case 0: CholWave<P, SY, 0>::update(C, fu, bk, off, cn, lr, lq); break;
-      case 1: CholWave<P, SY, 1>::update(C, fu, bk, off, cn, lr, lq); break;
-      case 2: CholWave<P, SY, 2>::update(C, fu, bk, off, cn, lr, lq); break;
-      default: CholWave<P, SY, 3>::update(C, fu, bk, off, cn, lr, lq); break;
-    }
-    if (tid >= kn && tid < PB) {
-      double pr[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pr[q] = __builtin_fma(uL[PB][q + 4], uL[tid][q + 4], uL[PB][q] * uL[tid][q]);
-      rb -= (pr[0] + pr[1]) + (pr[2] + pr[3]);
-      if (tid < kn + 8) cn[tid - kn][PB] = rb;
-    }
-    if (K == 6) RPH_STAMPB(10);
-  }
-}
-
-// Blocked (8-column panels) fp64 Cholesky + triangular solves of the LM
-// system for up to 128 parameters, one workgroup: the trailing matrix lives
-// in the waves' MFMA accumulator tiles (lm_chol_factor), P/8 panels with two
-// barriers each; then blocked triangular solves with the diagonal blocks'
-// inverses.  The matrix is padded to a multiple of 8 with identity rows.  L is
-// written over A (lower triangle, SY layout); the solution replaces vec.
-template <int P, class SY>
-RPH_INLINE void lm_chol_solve_blocked(double* A, double* vec, int* s_fail, unsigned long long* stamps) {
-  constexpr int PB = (P + 7) / 8 * 8;
-  constexpr int NK = PB / 8;
-  constexpr int RW = CholTiles<P>::RWX;  // rows of the tile grid + the right-hand side row PB
-  static_assert(PB <= 192, "blocked solver: up to 192 parameters");
-  __shared__ double colb[8][RW];
-  __shared__ double uL[RW][9];
-  const int tid = threadIdx.x, wid = tid >> 6;
-  for (int t = tid; t < RW * 9; t += 256) (&uL[0][0])[t] = 0.0;
-  for (int e = tid; e < 8 * RW; e += 256) {
-    const int c = e / RW, i = e % RW;
-    colb[c][i] = (i < P && c <= i) ? A[SY::idx(i, c)]
-                 : i == PB         ? (c < P ? vec[c] : 0.0)
-                                   : ((i == c && i < PB) ? 1.0 : 0.0);
-  }
-  lm_chol_factor<P, SY>(A, vec, s_fail, colb, uL, stamps);
-  __syncthreads();
-  if (*s_fail) return;
-  RPH_STAMPB(6);
-  // reciprocal pivots, then both triangular solves in one wave (lm_tri_solve_wave)
-  double* rdg = vec + 2 * P;
-  for (int k = tid; k < P; k += 256) rdg[k] = lm_rcp(A[SY::idx(k, k)]);
-  __syncthreads();
-  RPH_STAMPB(7);
-  if (wid == 0) lm_tri_solve_wave<P, SY, false>(A, vec, rdg);  // y = L^-1 b came out of the factorization
-  __syncthreads();
-  RPH_STAMPB(12);
-}
 
 // Exact Newton step on the OUTPUT block at the best point (the value is
 // linear in the output layer's N = out_n parameters [P - N, P), so the loss
@@ -972,7 +627,6 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   }
   // a precomputed step is used at the solve of pass + m (< passes): skip the rest
   if (m > 0 && pass + m > lm.passes - 1) return;
-#ifndef RPH_LM_CHOL_V1
   // ---- tile-store Cholesky (lm_chol.h): panel wave 0, owner waves 1..3 ------
   using TG = TileGrid<P>;
   double* T = lds;
@@ -997,7 +651,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   __syncthreads();
   double dmp = 0.0;  // this parameter's damping term lam 2G_ii + ridge (for the predicted reduction)
   if (tid < P) {
-    dmp = a_ii * lam_m + (double)lm.ridge * s_diag;
+    // Marquardt scaling with a floor: a parameter whose subsample curvature
+    // vanishes (a hidden unit dead on the Gram subsample, active elsewhere)
+    // still gets damped, so growing lam always shortens its step
+    dmp = fmax(a_ii, (double)lm.diag_floor * s_diag) * lam_m + (double)lm.ridge * s_diag;
     lds[TG::OFF_DIAG + tid] = a_ii + dmp;
   }
   RPH_STAMPS(2);
@@ -1006,18 +663,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     case 0:
     {
       unsigned long long* stp = (m == 0 && blockIdx.y == 0 && d.stamps != nullptr) ? reinterpret_cast<unsigned long long*>(d.stamps) + 8 : nullptr;
-#ifdef RPH_PANEL_V2
-      lmc_panels_v2<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail, stp);
-#else
       lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail, stp);
-#endif
     }
       RPH_STAMPS(6);
-#ifdef RPH_BACKWARD_V2
-      lmc_backward_v2<P>(T, lds + TG::OFF_RDG, vec);
-#else
       lmc_backward<P>(T, lds + TG::OFF_RDG, vec);
-#endif
       RPH_STAMPS(7);
       break;
     case 1: LmcOwner<P, 0>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
@@ -1030,69 +679,6 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   // diagnostic build: the factored tile store -> d.stamps (as doubles)
   if (m == 0 && d.stamps != nullptr)
     for (int i = tid; i < TG::NTILE * 256 + 2 * TG::PT; i += 256) reinterpret_cast<double*>(d.stamps)[i] = lds[i];
-#endif
-#else
-  using SY = LmSys<P>;
-  double* A = lds;                          // system matrix, lower triangle (LmSys layout)
-  double* vec = lds + SY::ELEMS;            // [P] rhs / solution, [P] pivots, [P] reciprocal pivots
-  // ---- A = 2 G + lam diag(2 G) + ridge * mean diag, packed lower triangle -----
-  // every block of this wave is loaded first (one round trip for the whole
-  // Gram matrix, not one per block), then scattered into the LDS triangle
-  const int h = lane >> 5, r = lane & 31;
-  constexpr int BPW = (NBLK + 3) / 4;
-  static_assert(P <= 256, "one parameter per thread");
-  const double gi = tid < P ? g[tid] : 0.0;                          // gradient (same round trip)
-  const double wbest = tid < P ? st[LMS_W + best * LM_NPMAX + tid] : 0.0;  // for the final update
-  double gv[BPW][16];
-#pragma unroll
-  for (int k = 0; k < BPW; ++k) {
-    const int b = wid + 4 * k;
-    if (b < NBLK) {
-      const double* blk = src + (size_t)b * 1024;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) gv[k][q] = blk[q * 64 + lane];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < BPW; ++k) {
-    const int b = wid + 4 * k;
-    if (b >= NBLK) continue;
-    int mb, nb;
-    lm_blk(b, NB, mb, nb);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = mb * 32 + lm_row(q, h), j = nb * 32 + r;  // i <= j when mb < nb
-      if (i < P && j < P && (mb < nb || i >= j)) {
-        const int hi = i > j ? i : j, lo = i > j ? j : i;
-        A[SY::idx(hi, lo)] = 2.0 * gv[k][q];
-      }
-    }
-  }
-  __syncthreads();
-  if (wid == 0) {
-    double s = 0.0;
-    for (int i = lane; i < P; i += 64) s += A[SY::idx(i, i)];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0) {
-      s_diag = s / P;
-      s_fail = 0;
-    }
-  }
-  __syncthreads();
-  double dmp = 0.0;  // this parameter's damping term lam 2G_ii + ridge (for the predicted reduction)
-  if (tid < P) {
-    double& a = A[SY::idx(tid, tid)];
-    dmp = a * lam_m + (double)lm.ridge * s_diag;
-    a = a + dmp;
-    vec[tid] = -gi;
-  }
-  RPH_STAMPS(2);
-  __syncthreads();  // the damped diagonal is in place
-  // blocked Cholesky (trailing update on the fp64 matrix cores) + one-wave
-  // triangular solves; dense LDS storage up to 128 parameters, packed above
-  lm_chol_solve_blocked<P, SY>(A, vec, &s_fail, m == 0 ? d.stamps : nullptr);
-  __syncthreads();
 #endif
   const bool failed = s_fail != 0;
   // predicted reduction of the quadratic model at the step d:
@@ -1139,34 +725,19 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
 // ---------------------------------------------------------------------------
 template <int NIN, int H, int NO, int HEAD>
 struct LmKernels {
-  // the 1-3 input nets run two workgroups per CU (variant 5 body), the others one
+  // the 1-3 input nets could run two pass workgroups per CU (measured slower:
+  // one wave per SIMD with the packed two-path body is the default)
 #ifndef RPH_LM_PAIR_WPS
 #define RPH_LM_PAIR_WPS 1
 #endif
-#ifdef RPH_LM_PASS_V1
-  static constexpr bool TWO = NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
-#else
   static constexpr bool TWO = RPH_LM_PAIR_WPS == 2 && NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
-#endif
-#ifdef RPH_LM_PASS_V1
-  using Body = NarrowBody<NIN, H, NO, HEAD, 1, 1, false, true>;
-#else
   using Body = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1>;  // two paths per lane, packed fp32
   // the same body accumulating the out-means (the last passes of an lm_out_fix fit)
   using BodyOM = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true>;
-#endif
   using S = NetShape<NIN, H, NO, HEAD>;
-#ifndef RPH_LM_CHOL_V1
   // the tile store + vectors + hand-off counters (lm_chol.h)
   static constexpr int smem() { return TileGrid<S::P>::LDS_BYTES; }
   static_assert(smem() + 128 <= 160 * 1024, "LM solve exceeds the LDS of one workgroup");
-#else
-  static constexpr int smem() { return (int)((LmSys<S::P>::ELEMS + 3 * S::P) * sizeof(double)); }
-  // the solve's dynamic LDS (system matrix + vectors) and its static panel
-  // buffers (colb, uL of lm_chol_solve_blocked) share the CU's 160 KB
-  static_assert(smem() + (8 + 9) * CholTiles<S::P>::RWX * (int)sizeof(double) + 64 <= 160 * 1024,
-                "LM solve exceeds the LDS of one workgroup");
-#endif
 };
 
 static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {
@@ -1175,9 +746,17 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (d->batch != d->n_local || d->steps_per_epoch != 1) return rph_report("rph_lm", "LM fits are full batch");
   if (lm->num_wgs < 1 || lm->num_wgs > 65535 || lm->passes < 0 || lm->passes >= MAXHIST)
     return rph_report("rph_lm", "bad num_wgs / passes");
-  if (lm->gram_wgs < 1 || lm->gram_wgs > lm->num_wgs || lm->gram_blk < 1 || lm->gram_blk > lm->gram_blk_stride)
-    return rph_report("rph_lm", "bad Gram subsample geometry");
-  {
+  if (lm->gram_wgs < 1 || lm->gram_wgs > 65535) return rph_report("rph_lm", "bad Gram workgroup count");
+  if (lm->gram_side) {
+    // the subsample comes from gfeat / gprice ([gram_wgs x 64] each)
+    const int nhold = d->head == HEAD_COMPLEMENT ? 2 : d->nout;
+    for (int f = 0; f < d->nin; ++f)
+      if (!lm->gfeat[f]) return rph_report("rph_lm", "null Gram subsample feature");
+    for (int k = 0; k < nhold - 1; ++k)
+      if (!lm->gprice[k]) return rph_report("rph_lm", "null Gram subsample price");
+  } else {
+    if (lm->gram_wgs > lm->num_wgs || lm->gram_blk < 1 || lm->gram_blk > lm->gram_blk_stride)
+      return rph_report("rph_lm", "bad Gram subsample geometry");
     const long long ns = (long long)lm->gram_wgs * LM_TILE;  // the last slot must stay inside the shard
     const long long last = ((ns - 1) / lm->gram_blk) * lm->gram_blk_stride + (ns - 1) % lm->gram_blk;
     if (last >= d->n_local) return rph_report("rph_lm", "Gram subsample leaves the shard");
@@ -1194,18 +773,17 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
 template <int A, int B, int C, int E>
 static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const double* red_new, hipStream_t s) {
   using K = LmKernels<A, B, C, E>;
-#ifndef RPH_LM_PASS_V1
+  // path workgroups + Gram-only workgroups past them (Gram subsample > 64 x path grid)
+  const unsigned grid = (unsigned)(lm->gram_wgs > lm->num_wgs ? lm->gram_wgs : lm->num_wgs);
   if constexpr (K::BodyOM::OUTM) {
     // the last LM_OUTM_TAIL evaluations of an lm_out_fix fit carry the out-means
     if (lm->out_mean && pass > lm->passes - LM_OUTM_TAIL) {
-      hipLaunchKernelGGL((k_lm_pass<typename K::BodyOM>), dim3(lm->num_wgs, lm->inst), dim3(256), 0, s, *d, *lm,
-                         pass, red_new);
+      hipLaunchKernelGGL((k_lm_pass<typename K::BodyOM>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
+                         red_new);
       return (int)hipGetLastError();
     }
   }
-#endif
-  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(lm->num_wgs, lm->inst), dim3(256), 0, s, *d, *lm, pass,
-                     red_new);
+  hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass, red_new);
   return (int)hipGetLastError();
 }
 
@@ -1281,6 +859,76 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange(const LmDpDesc x, double
 }
 
 // ---------------------------------------------------------------------------
+// Data-parallel all-reduce of the gradient region [g | stats | out-means] =
+// red[LM_GBLK_MAX, LM_RED) (264 doubles, 2.1 KB) when every rank builds the
+// same Gram matrix from the simulated global subsample (LmDesc.gram_side):
+// ONE workgroup, 132 lanes each push one 16-byte pair to every peer with a
+// write-through (sc0 sc1: system scope) global_store_dwordx4, drain, one
+// flag per peer (system-scope release), bounded acquire waits, fixed-rank-
+// order sums (bitwise-identical replicas).  Same mailbox rows, flag slot and
+// exchange counter as k_lm_dp_exchange (the sequence tags stay monotonic).
+// ---------------------------------------------------------------------------
+constexpr int LM_GREG = LM_RED - LM_GBLK_MAX;  // doubles of the gradient region
+
+RPH_INLINE void lm_store_sys_b128(double* p, double a, double b) {
+  typedef unsigned lm_u4 __attribute__((ext_vector_type(4)));
+  const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+  const lm_u4 v = {(unsigned)ua, (unsigned)(ua >> 32), (unsigned)ub, (unsigned)(ub >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+__global__ __launch_bounds__(256) void k_lm_dp_exchange_g(const LmDpDesc x, double* __restrict__ red) {
+  __shared__ unsigned s_seq;
+  const int tid = threadIdx.x, W = x.world, me = x.rank;
+  if (tid == 0) s_seq = __hip_atomic_load(x.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const unsigned seq = s_seq;
+  const int slot = (int)(seq % DP_SLOTS);
+  double* const g = red + LM_GBLK_MAX;
+  double v0 = 0.0, v1 = 0.0;
+  if (2 * tid < LM_GREG) {
+    v0 = g[2 * tid];
+    v1 = g[2 * tid + 1];
+    for (int q = 0; q < W; ++q)
+      if (q != me) lm_store_sys_b128(x.mbox[q] + ((size_t)slot * W + me) * x.pitch + 2 * tid, v0, v1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its pushes
+  __syncthreads();
+  if (tid < W && tid != me) {
+    unsigned* fo = reinterpret_cast<unsigned*>(x.mbox[tid] + ((size_t)slot * W + me) * x.pitch + LM_RED);
+    __hip_atomic_store(fo, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* fi = reinterpret_cast<const unsigned*>(x.mbox[me] + ((size_t)slot * W + tid) * x.pitch + LM_RED);
+    unsigned it = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(fi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++it & 255u) == 0u && (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS ||
+                                  __hip_atomic_load(x.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+        __hip_atomic_store(x.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (2 * tid < LM_GREG) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int q = 0; q < W; ++q) {
+      if (q == me) {
+        s0 += v0;
+        s1 += v1;
+      } else {
+        const double* m = x.mbox[me] + ((size_t)slot * W + q) * x.pitch + 2 * tid;
+        s0 += __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s1 += __hip_atomic_load(m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    g[2 * tid] = s0;
+    g[2 * tid + 1] = s1;
+  }
+  if (tid == 0) __hip_atomic_store(x.counter, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
 // Multi-start selection of a first date (one workgroup).  The exploration
 // fits (LmDesc.inst instances on a path prefix of every rank, LmDesc.explore)
 // leave their final best loss, damping and best weights in their states.
@@ -1352,17 +1000,18 @@ extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p,
     return rph_report("rph_lm_dp_exchange", "bad world / rank");
   if (x->pitch < LM_RED + LM_DP_WGS || ng < 0 || ng > LM_GBLK_MAX || p < 1 || p > LM_NPMAX)
     return rph_report("rph_lm_dp_exchange", "bad mailbox pitch / block geometry");
+  if ((x->pitch % 2) != 0) return rph_report("rph_lm_dp_exchange", "mailbox rows must be 16-byte aligned");
   for (int q = 0; q < x->world; ++q)
     if (!x->mbox[q]) return rph_report("rph_lm_dp_exchange", "null peer mailbox");
+  if (ng == 0) {
+    // no Gram entries: the whole gradient region in one workgroup (16-byte pushes)
+    hipLaunchKernelGGL(k_lm_dp_exchange_g, dim3(1), dim3(256), 0, (hipStream_t)stream, *x, red);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(k_lm_dp_exchange, dim3(LM_DP_WGS), dim3(256), 0, (hipStream_t)stream, *x, red, ng, p);
   return (int)hipGetLastError();
 }
 
-#ifndef RPH_LM_CHOL_V1
-#define RPH_LM_SHAPE_191(X) X(6, 8, 7, HEAD_FREE)
-#else
-#define RPH_LM_SHAPE_191(X)
-#endif
 #define RPH_LM_SHAPES(X)         \
   X(1, 8, 1, HEAD_COMPLEMENT)    \
   X(1, 8, 2, HEAD_FREE)          \
@@ -1370,7 +1019,7 @@ extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p,
   X(3, 8, 2, HEAD_FREE)          \
   X(4, 8, 2, HEAD_FREE)          \
   X(5, 8, 6, HEAD_FREE)          \
-  RPH_LM_SHAPE_191(X)
+  X(6, 8, 7, HEAD_FREE)
 // (6, 8, 7): P = 191, 78 tiles of the tile store = 156 KB of the CU's 160 KB
 // (lm_chol.h); larger nets have no LM solver and fit with Adam
 // (HipBackend.lm_supported() is False)

@@ -222,10 +222,11 @@ struct NarrowPairBody {
   struct Sched {
     long long b0, bstep, bend;
   };
-  RPH_INLINE static Sched sched(const TrainDesc& d, int gram_wgs, int gram_skip) {
+  // (num_wgs: the path workgroups; a pass grid may carry Gram-only workgroups beyond them)
+  RPH_INLINE static Sched sched(const TrainDesc& d, int num_wgs, int gram_wgs, int gram_skip) {
     const long long nblk = (d.batch + 127) / 128;
-    const int TW = (int)gridDim.x * 4, w = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    const int GW = (gram_wgs < (int)gridDim.x ? gram_wgs : (int)gridDim.x) * 4;
+    const int TW = num_wgs * 4, w = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int GW = (gram_wgs < num_wgs ? gram_wgs : num_wgs) * 4;
     const long long per = nblk / TW;
     if (gram_skip <= 0 || GW >= TW || per <= 0) return {w, TW, nblk};
     const long long gb = per > gram_skip ? per - gram_skip : 0;

@@ -300,88 +300,6 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
   });
   if (!ok && lane == 0) *s_fail = 1;
 }
-// A/B: the round-3 runtime-loop panel and backward solve (bisecting)
-template <int P>
-RPH_INLINE void lmc_panels_v2(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail,
-                           unsigned long long* stamps) {
-#pragma clang fp contract(off)
-  using TG = TileGrid<P>;
-  constexpr int NS = TG::NSLOT;
-  const int lane = threadIdx.x & 63;
-  bool ok = true;
-  for (int K = 0; K < TG::NK; ++K) {
-    if (!lmc_wait(&pub[K], 3u)) {
-      *s_fail = 2;
-      return;
-    }
-    if (K < 2) LMC_STAMP(2 * K);
-    else if (K == TG::NK - 1) LMC_STAMP(4);
-    const int nc = P - 16 * K < 16 ? P - 16 * K : 16;
-    double a[NS][16];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int row = 16 * K + lane + 64 * s;
-      if (row < TG::PT) {
-        const double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
-        const int sw = ((row & 15) >> 1) << 1;
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-          const double2 v = *reinterpret_cast<const double2*>(tr + (c ^ sw));
-          a[s][c] = v.x;
-          a[s][c + 1] = v.y;
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
-      }
-    }
-    // the lane's own diagonal entry (lanes 0..15: row 16K + lane of the diagonal
-    // tile), updated with its OWN L entries - the same fma sequence the
-    // broadcast update applies to it (bc[lane] is this lane's value), so the
-    // pivot chain never waits for the LDS broadcast round trip
-    double dg = lane < 16 ? T[TG::tidx(K, K) * 256 + tg_off(lane, lane)] : 1.0;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if (c < nc) {
-        const double piv = lmc_readlane(dg, c);
-        ok = ok && piv > 0.0;
-        const double rl = lmc_rsq(piv);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) a[s][c] *= rl;
-        dg = __builtin_fma(-a[0][c], a[0][c], dg);  // lanes > c: their diagonal's column-c update
-        if (lane < 16) bc[lane] = a[0][c];
-        lmc_wave_sync();
-        if (lane == c) rdg[16 * K + c] = rl;
-#pragma unroll
-        for (int j = c + 1; j < 16; ++j) {
-          const double lj = bc[j];  // L[16K + j][16K + c] (LDS broadcast)
-#pragma unroll
-          for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
-        }
-      }
-    }
-    // write L back (the diagonal tile's upper triangle as zeros)
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int row = 16 * K + lane + 64 * s;
-      if (row < TG::PT) {
-        double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
-        const int sw = ((row & 15) >> 1) << 1;
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-          double2 v;
-          v.x = (s == 0 && c > lane) ? 0.0 : a[s][c];
-          v.y = (s == 0 && c + 1 > lane) ? 0.0 : a[s][c + 1];
-          *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
-        }
-      }
-    }
-    lmc_signal(&fac[K]);
-    if (K < 2) LMC_STAMP(2 * K + 1);
-    else if (K == TG::NK - 1) LMC_STAMP(5);
-  }
-  if (!ok && lane == 0) *s_fail = 1;
-}
 #undef LMC_STAMP
 
 // Backward solve L^T d = y (y = row P of L) by the panel wave, blocks of 16
@@ -431,40 +349,6 @@ RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv) {
     if (q == 0 && col < P) dv[col] = dk;
     lmc_wave_sync();
   });
-}
-
-template <int P>
-RPH_INLINE void lmc_backward_v2(const double* T, const double* rdg, double* dv) {
-#pragma clang fp contract(off)
-  using TG = TileGrid<P>;
-  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-  for (int K = TG::NK - 1; K >= 0; --K) {
-    const int col = 16 * K + c;
-    double z = 0.0;
-    for (int i = 16 * (K + 1) + q; i < P; i += 4)
-      z = __builtin_fma(T[TG::tidx(i >> 4, K) * 256 + tg_off(i & 15, c)], dv[i], z);
-    z += __shfl_xor(z, 16, 64);
-    z += __shfl_xor(z, 32, 64);
-    const double y = col < P ? T[TG::tidx(P >> 4, K) * 256 + tg_off(P & 15, c)] : 0.0;
-    z = y - z;
-    // column c of the diagonal tile: L[16K + j][16K + c], j = 0..15
-    double lc[16];
-    const double* td = T + TG::tidx(K, K) * 256;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) lc[j] = td[tg_off(j, c)];
-    const double rd = col < P ? rdg[col] : 0.0;
-    const int nc = P - 16 * K < 16 ? P - 16 * K : 16;
-    double dk = 0.0;
-#pragma unroll
-    for (int j = 15; j >= 0; --j) {
-      if (j < nc) {
-        const double dj = lmc_readlane(z * rd, j);  // d[16K + j] (final in lane j)
-        if (c == j) dk = dj;
-        z = __builtin_fma(-lc[j], dj, z);  // lanes c < j
-      }
-    }
-    if (q == 0 && col < P) dv[col] = dk;
-  }
 }
 
 }  // namespace rph

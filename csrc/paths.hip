@@ -14,6 +14,10 @@
 #include "rph_types.h"
 
 namespace rph {
+int rph_report(const char* what, const char* msg);  // runtime.cpp
+}
+
+namespace rph {
 
 template <typename Real>
 RPH_INLINE Real ndtri_u30(uint32_t x);
@@ -45,6 +49,13 @@ __global__ __launch_bounds__(256) void k_sobol_normal(Real* __restrict__ out, in
   }
 }
 
+// global (Sobol / Philox) index of local path p (SimDesc.map_blk: the LM Gram
+// subsample, a few aligned blocks of the global range, simulated on every rank)
+RPH_INLINE long long sim_gidx(const SimDesc& d, int p) {
+  return d.map_blk > 0 ? d.path_offset + ((long long)p / d.map_blk) * d.map_stride + (long long)p % d.map_blk
+                       : d.path_offset + p;
+}
+
 // ---------------------------------------------------------------------------
 // Single-asset / SV / Heston / mortality scans.
 // ---------------------------------------------------------------------------
@@ -52,7 +63,8 @@ template <typename Real, bool ALIGNED, int MODEL>
 __global__ __launch_bounds__(256) void k_sim_scan(const SimDesc d) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (!ALIGNED && p >= d.n_local) return;
-  const uint32_t g = gray_code((uint64_t)(d.path_offset + p));
+  const long long gp = sim_gidx(d, p);
+  const uint32_t g = gray_code((uint64_t)gp);
   const Real dt = (Real)d.dt;
   const Real sdt = sqrt(dt);
   const Real mu = (Real)d.mu[0], sig = (Real)d.sigma[0];
@@ -172,7 +184,7 @@ __global__ __launch_bounds__(256) void k_sim_scan(const SimDesc d) {
       double q = 1.0 - exp(-(double)lam * (double)dt);
       q = q < 0.0 ? 0.0 : (q > 1.0 ? 1.0 : q);
       if (N > 0 && q > 0.0) {
-        const u32x4 r = philox4x32_10({(uint32_t)(d.path_offset + p), (uint32_t)((d.path_offset + p) >> 32),
+        const u32x4 r = philox4x32_10({(uint32_t)gp, (uint32_t)(gp >> 32),
                                        (uint32_t)t, 0xB1A0u},
                                       d.seed, 0x1234u);
         const double u = u01d(r.x, r.y);
@@ -221,7 +233,7 @@ template <int NA, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_sim_basket(const SimDesc d) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (!ALIGNED && p >= d.n_local) return;
-  const uint32_t g = gray_code((uint64_t)(d.path_offset + p));
+  const uint32_t g = gray_code((uint64_t)sim_gidx(d, p));
   const float dt = (float)d.dt, sdt = sqrtf(dt);
   float ly[NA], drift[NA], vol[NA], inv[NA], ch[NA * (NA + 1) / 2];
   const size_t n = (size_t)d.n_local;
@@ -369,7 +381,10 @@ static int launch_basket(const SimDesc* d, hipStream_t s) {
 
 extern "C" int rph_simulate(const SimDesc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const bool aligned = (d->n_local % 256 == 0) && (d->path_offset % 64 == 0);
+  if (d->map_blk < 0 || (d->map_blk > 0 && d->map_stride < d->map_blk)) return rph_report("rph_simulate", "bad path-index map");
+  // (aligned: every wave's 64 paths are one aligned range of global indices)
+  const bool aligned = (d->n_local % 256 == 0) && (d->path_offset % 64 == 0) &&
+                       (d->map_blk == 0 || (d->map_blk % 64 == 0 && d->map_stride % 64 == 0));
   if (d->model == SIM_BASKET) return aligned ? launch_basket<true>(d, s) : launch_basket<false>(d, s);
   if (d->fp64) return aligned ? launch_scan<double, true>(d, s) : launch_scan<double, false>(d, s);
   return aligned ? launch_scan<float, true>(d, s) : launch_scan<float, false>(d, s);

@@ -266,7 +266,7 @@ struct LmDesc {
   // > 0: the fit's initial damping is max(state[LMS_LAM] x lam_carry, lam_min)
   // (the previous fit's final damping on this state), else lam0
   float lam_carry;
-  int pad0;
+  float diag_floor;              // damping diagonal max(2 G_ii, diag_floor x mean 2 G_ii) (Marquardt scaling floor)
   const float* w0;               // [inst][LM_NPMAX] start weights (nullptr: the canonical NetWeights)
   // 1: the start weights were fitted on inputs standardised with (ren_mu,
   // ren_isd); the first layer is re-expressed for this fit's (fmu, fisd), so
@@ -285,6 +285,16 @@ struct LmDesc {
   // the bond bias then absorbs the step's full-batch mean residual exactly
   int out_mean;
   int pad3;
+  // 1: the Gram subsample is read from gfeat / gprice ([ns] per feature /
+  // traded asset, slot order = the global subsample, simulated identically on
+  // every rank), so every rank builds the same Gram matrix and the data-
+  // parallel exchange carries only [g | stats | out-means]; 0: slot j reads
+  // local path (j / gram_blk) * gram_blk_stride + j % gram_blk of the shard
+  // (this rank's part of the subsample; the Gram is then summed over ranks)
+  const float* gfeat[MAXIN];
+  const float* gprice[MAXIN];
+  int gram_side;
+  int pad4;
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)
@@ -347,6 +357,11 @@ struct SimDesc {
   double sv_tscale;
   int scheme;                    // HESTON: 0 full-truncation Euler, 1 Andersen QE (martingale-corrected)
   int pad0;
+  // path-index map (the LM Gram subsample simulated on every rank): local path
+  // p is global path path_offset + (p / map_blk) * map_stride + p % map_blk;
+  // map_blk = 0: contiguous (path_offset + p)
+  long long map_blk;
+  long long map_stride;
 };
 
 enum HestonScheme : int { HESTON_EULER = 0, HESTON_QE = 1 };

@@ -69,7 +69,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       // LmDesc + LM state layout
       (long long)sizeof(LmDesc), OFF(LmDesc, slab_b), OFF(LmDesc, slab_g), OFF(LmDesc, num_wgs),
       OFF(LmDesc, passes), OFF(LmDesc, gram_blk), OFF(LmDesc, inv_ns), OFF(LmDesc, lam0), OFF(LmDesc, ridge), OFF(LmDesc, bias_index), OFF(LmDesc, weights_only), OFF(LmDesc, damping), OFF(LmDesc, stop_tol), OFF(LmDesc, gram_skip),
-      OFF(LmDesc, inst), OFF(LmDesc, lam_carry), OFF(LmDesc, w0), OFF(LmDesc, renorm), OFF(LmDesc, ren_isd), OFF(LmDesc, out_n), (long long)sizeof(LmDesc), (long long)LMS_LFIN, (long long)LM_SEL_W,
+      OFF(LmDesc, inst), OFF(LmDesc, lam_carry), OFF(LmDesc, w0), OFF(LmDesc, renorm), OFF(LmDesc, ren_isd), OFF(LmDesc, out_n), OFF(LmDesc, gfeat), OFF(LmDesc, gprice), OFF(LmDesc, gram_side), (long long)sizeof(LmDesc), (long long)LMS_LFIN, (long long)LM_SEL_W,
       (long long)sizeof(LmDpDesc), OFF(LmDpDesc, counter), OFF(LmDpDesc, world), OFF(LmDpDesc, pitch),
       (long long)LM_NPMAX, (long long)LM_RED, (long long)LMS_BEST, (long long)LMS_FLOATS,
       (long long)LM_SPEC, (long long)LMS_SPEC_W, (long long)LMS_SLOTS, (long long)LM_SLOT, (long long)LSS_LBEST, (long long)LSS_STOP,
@@ -78,7 +78,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       OFF(SimDesc, sv2), OFF(SimDesc, dims2), OFF(SimDesc, s0), OFF(SimDesc, chol), OFF(SimDesc, dt),
       OFF(SimDesc, inv_norm), OFF(SimDesc, v0), OFF(SimDesc, rho), OFF(SimDesc, l0), OFF(SimDesc, n0),
       OFF(SimDesc, seed), OFF(SimDesc, out), OFF(SimDesc, final2_out), OFF(SimDesc, sv_tscale),
-      OFF(SimDesc, scheme),
+      OFF(SimDesc, scheme), OFF(SimDesc, map_blk), OFF(SimDesc, map_stride),
       (long long)LAG_SLOTS,
   };
   const int n = (int)(sizeof(v) / sizeof(v[0]));

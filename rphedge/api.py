@@ -22,7 +22,7 @@ import torch
 from . import risk
 from .config import RunConfig, parse_params
 from .driver import BackwardInduction, InductionConfig, InductionResult, error_history, expected_value_trajectory
-from .engine import TrainConfig, make_backend, set_weights
+from .engine import TrainConfig, gram_subsample, make_backend, set_weights
 from .models import hedge_mlp as hm
 from .ops import layout as L
 from .ops import paths as P
@@ -87,6 +87,7 @@ class HedgeRun:
         self.kind = self._kind()
         self.spec = self._spec()
         self.paths = None
+        self.gpaths = None  # LM Gram subsample paths (engine.gram_subsample), simulated on every rank
         self.induction = None
         self.graph = None
 
@@ -126,65 +127,76 @@ class HedgeRun:
 
         ``into``: re-simulate into the buffers of the existing paths and
         terminal value (no allocation, no host synchronisation), so the
-        simulation can be captured into the run's hipGraph."""
-        c, g, dev = self.cfg, self.grid, self.device
-        fp64 = c.dtype == "fp64"
-        kw = dict(device=dev, offset=self.offset, stream=self.stream, out=into)
+        simulation can be captured into the run's hipGraph.  LM fits also get
+        the global Gram subsample simulated on this rank (:meth:`gram_paths`)."""
+        c = self.cfg
         vt_out = self.v_terminal if into is not None else None
         with self.timer.phase("simulate"):
+            p = self._simulate_paths(self.n_local, self.offset, None, into)
             if self.kind == "european":
-                if c.model == "heston":
-                    p = P.simulate_sv(g, self.n_local, c.Y, c.r, c.v0, model="heston", kappa=c.kappa,
-                                      theta=c.theta, xi=c.xi, rho=c.rho, norm=c.Y, fp64=fp64,
-                                      scheme=c.heston_scheme, joint=not c.parity.paired_sobol, **kw)
-                else:
-                    scheme = "arith" if c.model == "gbm" else "log"
-                    p = P.simulate_gbm(g, self.n_local, c.Y, c.r, c.sigma, scheme=scheme, norm=c.Y, fp64=fp64,
-                                       **kw)
-                # EO normalises BOTH prices by S0 (cell 13: _B_t = B/S0, so psi counts
-                # unit bonds); the corrected default quotes the bond in S0 units.
-                p.bond = g.bond(c.r, norm=c.Y if c.parity.complement_head else 1.0)
                 v_t = P.payoff(c.option_type.lower(), p, c.K / c.Y, stream=self.stream, out=vt_out)
             elif self.kind == "basket":
-                na = c.n_assets
-                corr = np.full((na, na), c.basket_corr) + np.eye(na) * (1 - c.basket_corr)
-                s0 = [c.Y] * na
-                p = P.simulate_basket(g, self.n_local, s0, [c.r] * na, [c.sigma] * na, corr, norm=s0, **kw)
-                p.bond = g.bond(c.r)
-                w = c.basket_weights or tuple([1.0 / na] * na)
+                w = c.basket_weights or tuple([1.0 / c.n_assets] * c.n_assets)
                 v_t = P.payoff("basket_call", p, c.K / c.Y, weights=w, stream=self.stream, out=vt_out)
             else:
-                if c.model in ("sv_ref", "heston"):
-                    sv_c = c.sv_c
-                    p = P.simulate_sv(g, self.n_local, c.Y, c.mu, c.s0, model=c.model, a=c.a, b=c.b, c=sv_c,
-                                      kappa=c.kappa, theta=c.theta, xi=c.xi, rho=c.rho, fp64=fp64,
-                                      parity_nan=c.parity.sv_sqrt_nan, scheme=c.heston_scheme,
-                                      sv_tscale=0.0 if c.parity.sv_reference_dynamics else c.sv_days_per_year,
-                                      joint=not c.parity.paired_sobol, **kw)
-                else:
-                    p = P.simulate_gbm(g, self.n_local, c.Y, c.mu, c.sigma, scheme=("log" if c.model == "gbm_log"
-                                                                                   else "arith"),
-                                       fp64=fp64, **kw)
-                if c.mortality:
-                    if into is not None and c.parity.numpy_binomial:
-                        raise NotImplementedError("numpy binomial (Q20 parity) runs on the host: not graph-safe")
-                    P.simulate_mortality(p, c.l0, c.c, c.ita, c.N, lambda_fine_index=c.parity.lambda_fine_index,
-                                         fp64=fp64, numpy_binomial=c.parity.numpy_binomial,
-                                         stream=self.stream)
-                else:
-                    p.kind = "pension_nomort"
-                p.bond = g.bond(c.r)
-                if not c.parity.fine_terminal_payoff:
-                    if into is None:
-                        p.S_final = p.S[-1].clone()
-                    else:
-                        p.S_final.copy_(p.S[-1])
-                if p.nfrac is not None:
-                    # the coarse terminal survivors are what the liability is paid on (RP:184)
-                    p.nfrac_final = p.nfrac[-1]
                 v_t = P.payoff("guarantee", p, c.K, stream=self.stream, out=vt_out)
+            if str(c.train.optimizer).lower() == "lm":
+                ns, blk, stride = gram_subsample(self.n_total, c.train.lm_gram_paths)
+                self.gpaths = self._simulate_paths(ns, 0, (blk, stride), self.gpaths if into is not None else None)
         self.paths, self.v_terminal = p, v_t
         return p, v_t
+
+    def _simulate_paths(self, n: int, offset: int, index_map, into: P.Paths | None) -> P.Paths:
+        """One model's coarse-grid paths for ``n`` paths from global index
+        ``offset`` (``index_map``: the Gram subsample's global blocks)."""
+        c, g, dev = self.cfg, self.grid, self.device
+        fp64 = c.dtype == "fp64"
+        kw = dict(device=dev, offset=offset, stream=self.stream, out=into, index_map=index_map)
+        if self.kind == "european":
+            if c.model == "heston":
+                p = P.simulate_sv(g, n, c.Y, c.r, c.v0, model="heston", kappa=c.kappa, theta=c.theta, xi=c.xi,
+                                  rho=c.rho, norm=c.Y, fp64=fp64, scheme=c.heston_scheme,
+                                  joint=not c.parity.paired_sobol, **kw)
+            else:
+                scheme = "arith" if c.model == "gbm" else "log"
+                p = P.simulate_gbm(g, n, c.Y, c.r, c.sigma, scheme=scheme, norm=c.Y, fp64=fp64, **kw)
+            # EO normalises BOTH prices by S0 (cell 13: _B_t = B/S0, so psi counts
+            # unit bonds); the corrected default quotes the bond in S0 units.
+            p.bond = g.bond(c.r, norm=c.Y if c.parity.complement_head else 1.0)
+            return p
+        if self.kind == "basket":
+            na = c.n_assets
+            corr = np.full((na, na), c.basket_corr) + np.eye(na) * (1 - c.basket_corr)
+            s0 = [c.Y] * na
+            p = P.simulate_basket(g, n, s0, [c.r] * na, [c.sigma] * na, corr, norm=s0, **kw)
+            p.bond = g.bond(c.r)
+            return p
+        if c.model in ("sv_ref", "heston"):
+            p = P.simulate_sv(g, n, c.Y, c.mu, c.s0, model=c.model, a=c.a, b=c.b, c=c.sv_c, kappa=c.kappa,
+                              theta=c.theta, xi=c.xi, rho=c.rho, fp64=fp64, parity_nan=c.parity.sv_sqrt_nan,
+                              scheme=c.heston_scheme,
+                              sv_tscale=0.0 if c.parity.sv_reference_dynamics else c.sv_days_per_year,
+                              joint=not c.parity.paired_sobol, **kw)
+        else:
+            p = P.simulate_gbm(g, n, c.Y, c.mu, c.sigma, scheme=("log" if c.model == "gbm_log" else "arith"),
+                               fp64=fp64, **kw)
+        if c.mortality:
+            if into is not None and c.parity.numpy_binomial:
+                raise NotImplementedError("numpy binomial (Q20 parity) runs on the host: not graph-safe")
+            P.simulate_mortality(p, c.l0, c.c, c.ita, c.N, lambda_fine_index=c.parity.lambda_fine_index,
+                                 fp64=fp64, numpy_binomial=c.parity.numpy_binomial, stream=self.stream)
+        else:
+            p.kind = "pension_nomort"
+        p.bond = g.bond(c.r)
+        if not c.parity.fine_terminal_payoff:
+            if into is None:
+                p.S_final = p.S[-1].clone()
+            else:
+                p.S_final.copy_(p.S[-1])
+        if p.nfrac is not None:
+            # the coarse terminal survivors are what the liability is paid on (RP:184)
+            p.nfrac_final = p.nfrac[-1]
+        return p
 
     def summary_stats(self) -> dict:
         """E[N_T], P(out of the money), E[payoff] (C10; global over ranks)."""
@@ -235,7 +247,8 @@ class HedgeRun:
                            mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode,
                            lm_gram_paths=int(tr.lm_gram_paths), lm_damping=str(tr.lm_damping),
                            lm_lam0=float(tr.lm_lam0), lm_lam_up=float(tr.lm_lam_up),
-                           lm_lam_down=float(tr.lm_lam_down), lm_out_fix=bool(tr.lm_out_fix))
+                           lm_lam_down=float(tr.lm_lam_down), lm_out_fix=bool(tr.lm_out_fix),
+                           lm_diag_floor=float(tr.lm_diag_floor))
         if int(tr.variant) >= 0:
             tcfg.variant = int(tr.variant)
         kw = {}
@@ -268,6 +281,7 @@ class HedgeRun:
                                optimizer=str(tr.optimizer).lower(), lm_passes_first=int(tr.lm_passes_first),
                                lm_passes_rest=int(tr.lm_passes_rest), lm_stop_tol=float(tr.lm_stop_tol),
                                lm_stop_min=int(tr.lm_stop_min), lm_lam0_rest=float(tr.lm_lam0_rest),
+                               lm_lam0_first=float(tr.lm_lam0_first),
                                lm_lam_carry=float(tr.lm_lam_carry), lm_starts=int(tr.lm_starts),
                                lm_renorm=bool(tr.lm_renorm),
                                lm_explore_passes=int(tr.lm_explore_passes), lm_explore_log2=int(tr.lm_explore_log2),
@@ -282,7 +296,8 @@ class HedgeRun:
             if not backend_q.concurrent_with(self.backend):
                 backend_q = None
         self.induction = BackwardInduction(self.paths, self.v_terminal, self.spec, self.w0, self.backend, icfg,
-                                           world=self.di.world, rank=self.di.rank, backend_q=backend_q)
+                                           world=self.di.world, rank=self.di.rank, backend_q=backend_q,
+                                           gram_paths=self.gpaths)
         return self
 
     # ------------------------------------------------------------------ run

@@ -111,6 +111,8 @@ class TrainingParams:
     lm_lam0: float = 1e-3            # LM initial damping of every fit
     lm_lam_up: float = 4.0           # simple rule: damping x lam_up on a rejected trial
     lm_lam_down: float = 1.0 / 3.0   #              x lam_down on an accepted one
+    lm_lam0_first: float = 0.0       # first date's initial LM damping (0: lm_lam0)
+    lm_diag_floor: float = 0.0       # LM damping diagonal floor, relative to mean diag 2G (0: Marquardt scaling)
     mean_refit: bool = True          # after each Adam MSE fit: exact refit of the bond holding's bias (the
                                      # residual mean over all paths -> 0; no mean error drifts into V0)
     feature_norm: str = "date"       # input standardisation: none | global | date (driver.feature_norms);

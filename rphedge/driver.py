@@ -62,6 +62,7 @@ class InductionConfig:
     lm_stop_tol: float = 0.0             # later dates: adaptive LM pass budget (engine.FitConfig)
     lm_stop_min: int = 2
     lm_lam0_rest: float = 0.0            # later dates' initial LM damping (0: TrainConfig.lm_lam0)
+    lm_lam0_first: float = 0.0           # first date's initial LM damping (0: TrainConfig.lm_lam0)
     lm_lam_carry: float = 0.0            # later dates: start at the previous fit's final damping x this (0: off)
     lm_renorm: bool = False              # later dates: warm start re-expressed for the date's standardisation
     # first date: multi-start exploration (engine.FitConfig.lm_starts): lm_starts
@@ -132,8 +133,10 @@ class BackwardInduction:
     """Owns device buffers for one run; ``enqueue()`` is graph-capturable."""
 
     def __init__(self, paths: Paths, v_terminal: torch.Tensor, spec: NetSpec, w0: np.ndarray, backend,
-                 icfg: InductionConfig, world: int = 1, rank: int = 0, backend_q=None):
+                 icfg: InductionConfig, world: int = 1, rank: int = 0, backend_q=None, gram_paths: Paths | None = None):
         self.paths, self.spec, self.backend, self.cfg = paths, spec, backend, icfg
+        # LM fits: the global Gram subsample simulated on this rank (engine.gram_subsample)
+        self.gram_paths = gram_paths
         # independent-network model parallelism: with two networks (corrected
         # Q1 semantics) the pinball fit of a date does not depend on that date's
         # MSE fit, so it runs on its own backend (own buffers) on a side stream,
@@ -212,7 +215,8 @@ class BackwardInduction:
             return FitConfig(epochs=c.lm_passes_first if first else c.lm_passes_rest, loss=loss,
                              optimizer="lm", early_stopping=False, lm_stop_tol=0.0 if first else c.lm_stop_tol,
                              lm_stop_min=c.lm_stop_min,
-                             lm_lam0=None if (first or c.lm_lam0_rest <= 0) else c.lm_lam0_rest,
+                             lm_lam0=((c.lm_lam0_first if c.lm_lam0_first > 0 else None) if first else
+                                      (c.lm_lam0_rest if c.lm_lam0_rest > 0 else None)),
                              lm_lam_carry=0.0 if first else c.lm_lam_carry,
                              lm_starts=c.lm_starts if ms else 1,
                              lm_explore_passes=c.lm_explore_passes if ms else 0,
@@ -226,9 +230,11 @@ class BackwardInduction:
     def date_data(self, t: int) -> DateData:
         p = self.paths
         mu, isd = self.norms[t] if self.norms else ((), ())
+        gp = self.gram_paths
         return DateData(feats=p.features(t), prices_next=p.prices(t + 1), bond_next=float(p.bond[t + 1]),
                         target=self.values[t + 1], prices_now=p.prices(t), bond_now=float(p.bond[t]),
-                        fmu=mu, fisd=isd)
+                        fmu=mu, fisd=isd, gram_feats=gp.features(t) if gp is not None else None,
+                        gram_prices_next=gp.prices(t + 1) if gp is not None else None)
 
     def enqueue(self, start: int | None = None):
         """Enqueue dates ``start, start-1, ..., 0`` (default: all, from n-2).

@@ -143,6 +143,12 @@ class TrainConfig:
     lm_lam_min: float = 1e-9
     lm_lam_max: float = 1e10
     lm_ridge: float = 1e-10
+    # damping diagonal floor (relative to the mean of diag 2G): a parameter with
+    # no curvature on the Gram subsample is still damped, so lam -> inf shortens
+    # its step (tests/test_lm_cpu.py: a teacher fit that stalls at lam_max
+    # without it).  0 = plain Marquardt scaling (the presets: 1e-6 moved the
+    # euro30 8-seed P&L 0.890 -> 0.897 in tools/lm_lab.py, 1e-9 changed nothing)
+    lm_diag_floor: float = 0.0
     # damping update: "simple" (x lam_down on accept, x lam_up on reject) or
     # "nielsen" (gain ratio rho of actual / predicted reduction: accept
     # x max(1/3, 1 - (2 rho - 1)^3), reject x nu with nu doubling)
@@ -195,6 +201,11 @@ class DateData:
     # feature loads (empty: identity = the reference's raw inputs)
     fmu: tuple = ()
     fisd: tuple = ()
+    # LM fits: the global Gram subsample (gram_subsample) simulated on this
+    # rank, slot order: state_t features and traded assets at t+1, each [ns]
+    # (None: the Gram reads the shard; data parallel it is then summed over ranks)
+    gram_feats: list | None = None
+    gram_prices_next: list | None = None
 
 
 @dataclass
@@ -234,6 +245,22 @@ def _lm_out_n(spec, t) -> int:
     return spec.hidden * spec.nout + spec.nout if (t.lm_out_fix and lm_out_means(spec)) else 0
 
 
+def gram_subsample(n_total: int, lm_gram_paths: int) -> tuple[int, int, int]:
+    """(ns, blk, stride) of the LM Gram subsample of a ``n_total``-path run: the
+    first ``blk`` paths of each of ns / blk aligned global blocks of ``stride``
+    paths (GRAM_BLOCKS blocks where the sizes allow: aligned prefixes of a
+    Sobol sequence are nets; a strided subset is not).  The same global paths
+    at every world size: every rank simulates them (index-addressable Sobol /
+    Philox) and builds the identical Gram matrix, so the data-parallel exchange
+    carries only the gradient region [g | stats | out-means]."""
+    n_total = int(n_total)
+    ns = max(L.LM_TILE, min(int(lm_gram_paths), n_total) // L.LM_TILE * L.LM_TILE)
+    nb = GRAM_BLOCKS
+    while nb > 1 and (ns % (L.LM_TILE * nb) or n_total % nb):
+        nb //= 2
+    return ns, ns // nb, n_total // nb
+
+
 def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
     """Workgroups of the LM pass kernel (HipBackend._lm_buffers; the torch
     oracle derives its Gram subsample from the same number): 512 where two
@@ -242,9 +269,13 @@ def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
     return int(max(1, min(512 if two_per_cu else 256, n_local // 256)))
 
 
+LM_PAIR_WPS = 1  # csrc/hedge_lm.hip RPH_LM_PAIR_WPS default (one pass workgroup per CU)
+
+
 def lm_two_per_cu(spec) -> bool:
-    """csrc/hedge_lm.hip LmKernels::TWO for a net shape (no native library needed)."""
-    return spec.hidden == 8 and spec.nin <= 3 and spec.red_width <= 128
+    """csrc/hedge_lm.hip LmKernels::TWO for a net shape (no native library
+    needed; tests/test_lm_cpu.py checks it against native.lm_shape)."""
+    return LM_PAIR_WPS == 2 and spec.hidden == 8 and spec.nin <= 3 and spec.red_width <= 128
 
 
 def lm_gram_geometry(n_local: int, ns_local: int, world: int) -> tuple[int, int]:
@@ -416,6 +447,7 @@ class HipBackend:
         ewg = int(os.environ.get("RPH_EVAL_WGS", "512"))
         self.eval_wgs = int(max(1, min(ewg, (self.n_local + 255) // 256)))
         self._cache = _Cache()
+        self._lm_same_gram = True  # the last LM fit built the world-invariant Gram (exchange: gradient region only)
 
     # -- state ---------------------------------------------------------------
     def new_weights(self, w0):
@@ -553,21 +585,34 @@ class HipBackend:
             P, R, nblk, two = shp
             t = self.tcfg
             nw = lm_pass_wgs(self.n_local, bool(two))
-            ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // max(self.world, 1), self.n_local))
-            gw = int(max(1, min(ns_local // L.LM_TILE, nw)))
+            W = max(self.world, 1)
+            # the global Gram subsample (every rank: gw = ns / 64 Gram workgroups,
+            # past the path grid where it is larger)
+            ns, gblk, gstride = gram_subsample(self.n_local * W, t.lm_gram_paths)
+            gw = ns // L.LM_TILE
+            # fallback without simulated subsample data, data parallel: this
+            # rank's part of the subsample from its shard, the Gram summed over ranks
+            ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // W, self.n_local))
+            gw_local = int(max(1, min(ns_local // L.LM_TILE, nw)))
             dev = self.device
             lm = self.native.LmDesc()
             bufs = dict(state=torch.zeros(L.LMS_FLOATS, dtype=torch.float64, device=dev),
                         red=torch.zeros(L.LM_RED, dtype=torch.float64, device=dev),
                         slab_b=torch.zeros(nw, R, dtype=torch.float32, device=dev),
-                        slab_g=torch.zeros(gw, nblk * 1024, dtype=torch.float32, device=dev))
+                        slab_g=torch.zeros(max(gw, gw_local), nblk * 1024, dtype=torch.float32, device=dev))
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
-            lm.num_wgs, lm.gram_wgs, lm.red_wgs = nw, gw, nblk * 1024 // 64 + R // 4
-            lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, gw * L.LM_TILE, self.world)
-            lm.inv_ns = 1.0 / float(gw * L.LM_TILE * max(self.world, 1))
-            lm.inv_n = 1.0 / float(self.n_local * max(self.world, 1))
+            lm.num_wgs, lm.red_wgs = nw, nblk * 1024 // 64 + R // 4
+            lm.inv_n = 1.0 / float(self.n_local * W)
+            # (Gram geometry: per fit, _lm_gram_mode)
+            bufs["gram"] = dict(side=(gw, gblk, gstride, 1.0 / float(ns)),
+                                local=(gw_local,) + lm_gram_geometry(self.n_local, gw_local * L.LM_TILE, W) +
+                                (1.0 / float(gw_local * L.LM_TILE * W),))
+            # default (no subsample data): one rank reads the global subsample from its shard
+            lm.gram_side = 0
+            lm.gram_wgs, lm.gram_blk, lm.gram_blk_stride, lm.inv_ns = bufs["gram"]["side" if W == 1 else "local"]
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
+            lm.diag_floor = float(t.lm_diag_floor)
             lm.bias_index = _lm_bias_index(self.spec, t)
             lm.out_n, lm.out_mu = _lm_out_n(self.spec, t), float(t.lm_out_mu)
             lm.out_mean = 1 if lm.out_n > 0 else 0
@@ -577,15 +622,51 @@ class HipBackend:
             return bufs
         return self._cache.get(("lm",), make)
 
+    def _lm_gram_mode(self, lm, data: DateData) -> bool:
+        """Set the Gram subsample of ``lm`` for a fit on ``data``; returns True
+        when every rank builds the same Gram matrix (the exchange then carries
+        only the gradient region).  One rank reads the subsample from its shard
+        (the shard is the whole range) unless simulated subsample data is given;
+        data parallel, the simulated subsample is required for the small exchange
+        (without it: this rank's part of the subsample, Gram summed over ranks)."""
+        g = self._lm_buffers()["gram"]
+        side = data.gram_feats is not None and data.gram_prices_next is not None
+        if side:
+            gw, blk, stride, inv = g["side"]
+            if data.gram_feats[0].numel() != gw * L.LM_TILE:
+                raise ValueError(f"Gram subsample data has {data.gram_feats[0].numel()} paths, expected {gw * L.LM_TILE}")
+            for i, f in enumerate(data.gram_feats):
+                lm.gfeat[i] = f.data_ptr()
+            for i, p in enumerate(data.gram_prices_next):
+                lm.gprice[i] = p.data_ptr()
+        elif self.world <= 1:
+            gw, blk, stride, inv = g["side"]
+        else:
+            gw, blk, stride, inv = g["local"]
+        lm.gram_side = 1 if side else 0
+        lm.gram_wgs, lm.gram_blk, lm.gram_blk_stride, lm.inv_ns = gw, blk, stride, inv
+        return side or self.world <= 1
+
+    def lm_exchange_bytes(self) -> int:
+        """Bytes one rank pushes to EACH peer per LM pass (the gradient region
+        when the Gram is built redundantly, else the whole reduced block)."""
+        if self.world <= 1:
+            return 0
+        P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+        return 8 * (L.LM_RED - L.LM_GBLK_MAX) if self._lm_same_gram else 8 * (nblk * 1024 + P + 4 + L.LM_OUTM)
+
     def _lm_fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
         """Enqueue a full-batch Levenberg-Marquardt fit (MSE): ``fcfg.epochs``
         trial points after the start point, 3 launches each (pass, reduce,
-        solve), graph-capturable; data parallel: the reduced [G | g | stats]
-        block is all-reduced between reduce and solve (one collective)."""
+        solve), graph-capturable; data parallel: the gradient region [g |
+        stats | out-means] (2.1 KB) is all-reduced between reduce and solve
+        (every rank builds the same Gram matrix from the simulated global
+        subsample; without it the whole reduced block travels)."""
         if fcfg.loss != L.LOSS_MSE:
             raise ValueError("Levenberg-Marquardt fits minimise the MSE loss only")
         b = self._lm_buffers()
         lm = b["desc"]
+        self._lm_same_gram = self._lm_gram_mode(lm, data)
         lm.passes = int(fcfg.epochs)
         lm.stop_tol, lm.stop_min = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
         lm.lam0 = float(self.tcfg.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
@@ -609,7 +690,7 @@ class HipBackend:
             return
         for k in range(lm.passes + 1):
             n.lm_eval(d, lm, b["red"], k, self.stream)
-            self._lm_allreduce(b["red"])
+            self._lm_allreduce(b["red"], gram=not self._lm_same_gram)
             n.lm_solve(d, lm, b["red"], k, self.stream)
 
     def lm_explore_paths(self, fcfg: FitConfig) -> int:
@@ -651,13 +732,24 @@ class HipBackend:
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
             lm.w0 = bufs["w0"].data_ptr()
             lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
-            lm.out_n, lm.out_mean = 0, 0
+            lm.out_n, lm.out_mean, lm.gram_side = 0, 0, 0  # (rank-local fits on a shard prefix)
+            bufs["w0_rows"] = np.ascontiguousarray(rows).tobytes()
             lm.num_wgs, lm.gram_wgs = nw, gw
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
             lm.inv_ns, lm.inv_n = 1.0 / float(gw * L.LM_TILE), 1.0 / float(nsub)
             bufs["desc"] = lm
             return bufs
         x = self._cache.get(("lm_explore", K, nsub), make)
+        # this call's start points: a cached buffer must not keep an earlier
+        # fit's candidates (a new set is uploaded; not inside a graph capture)
+        rows = np.ascontiguousarray(np.asarray(fcfg.lm_w0s, dtype=np.float32)[self.rank * K:(self.rank + 1) * K, :P])
+        if rows.tobytes() != x["w0_rows"]:
+            if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("multi-start start points changed inside a graph capture")
+            w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
+            w0[:, :P] = torch.from_numpy(rows)
+            x["w0"].copy_(w0)
+            x["w0_rows"] = rows.tobytes()
         lm = x["desc"]
         lm.passes = int(fcfg.lm_explore_passes)
         lm.lam0 = float(self.tcfg.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
@@ -677,15 +769,17 @@ class HipBackend:
         n.lm_select(d, lm, x["sel"], b["state"], W, self.rank, P, 1, self.stream)
         self.lm_explore_last = x
 
-    def _lm_allreduce(self, red: torch.Tensor):
+    def _lm_allreduce(self, red: torch.Tensor, gram: bool = True):
         """Sum the reduced LM block over the ranks: in-kernel exchange over the
-        IPC mailboxes (xGMI transport) or one RCCL all-reduce."""
+        IPC mailboxes (xGMI transport) or one RCCL all-reduce.  ``gram=False``
+        (every rank built the same Gram matrix): only the gradient region
+        red[LM_GBLK_MAX:LM_RED] (264 doubles) travels."""
+        P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
         if self.lm_mailbox is not None:
-            P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
-            self.native.lm_dp_exchange(x, red, nblk * 1024, P, self.stream)
+            self.native.lm_dp_exchange(x, red, nblk * 1024 if gram else 0, P, self.stream)
             return
-        self._lm_comm().allreduce_(red, self.stream)
+        self._lm_comm().allreduce_(red if gram else red[L.LM_GBLK_MAX:L.LM_RED], self.stream)
 
     def bias_refit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
         """Exact refit of the bond holding's output bias after an Adam fit (one
@@ -728,6 +822,7 @@ class HipBackend:
             src = b["desc"]
             lm = type(src).from_buffer_copy(src)
             lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol, lm.out_n, lm.out_mean = 0, 1, 1, 0.0, 0, 0
+            lm.renorm, lm.lam_carry, lm.gram_side = 0, 0.0, 0  # (not inherited from the main fit's desc)
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
             return lm
@@ -946,32 +1041,61 @@ class TorchBackend:
         def v_one(w, x, p):
             return (torch_forward(spec, w, x[None])[0] * p).sum()
 
-        def make_eval(n_loc: int, world: int):
+        side = None
+        if data.gram_feats is not None and data.gram_prices_next is not None:
+            # the simulated global Gram subsample (identical on every rank)
+            Xs = _normalise(torch.stack([f.to(dt) for f in data.gram_feats], dim=1), data)
+            ps = torch.stack([p.to(dt) for p in data.gram_prices_next] +
+                             [torch.full((Xs.shape[0],), float(data.bond_next), dtype=dt)], dim=1)
+            side = (Xs, ps)
+
+        def make_eval(n_loc: int, world: int, main: bool = False):
             """evaluate(w) -> (G, g, stats) over the first n_loc local paths
-            (all-reduced over the ranks when world > 1)."""
+            (all-reduced over the ranks when world > 1).  ``main``: the fit
+            over every local path, whose Gram subsample is the global one of
+            engine.gram_subsample (HipBackend._lm_gram_mode): from the
+            simulated subsample data (the same G on every rank: only g and the
+            statistics are summed) or, on one rank, from the shard."""
             Xn, prn, yn = X[:n_loc], pr[:n_loc], y[:n_loc]
-            nw = lm_pass_wgs(n_loc, lm_two_per_cu(spec))
-            ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // world, n_loc))
-            gw = max(1, min(ns_local // L.LM_TILE, nw))
-            ns = gw * L.LM_TILE
-            inv_ns = 1.0 / float(ns * world)
-            blk, bstride = lm_gram_geometry(n_loc, ns, world)
-            sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
             n_glob = float(n_loc * world)
+            same_g = main and (side is not None or world == 1)
+            if same_g:
+                ns, blk, bstride = gram_subsample(n_loc * world, t.lm_gram_paths)
+                inv_ns = 1.0 / float(ns)
+                if side is not None:
+                    Xg, pg = side
+                else:
+                    sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
+                    Xg, pg = Xn[sub], prn[sub]
+            else:
+                nw = lm_pass_wgs(n_loc, lm_two_per_cu(spec))
+                ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // world, n_loc))
+                gw = max(1, min(ns_local // L.LM_TILE, nw))
+                ns = gw * L.LM_TILE
+                inv_ns = 1.0 / float(ns * world)
+                blk, bstride = lm_gram_geometry(n_loc, ns, world)
+                sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
+                Xg, pg = Xn[sub], prn[sub]
 
             def evaluate(w):
                 wg = w.detach().clone().requires_grad_(True)
                 e = (torch_forward(spec, wg, Xn) * prn).sum(1) - yn
                 lsum = (e * e).sum()
                 (lsum / n_glob).backward()
-                J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), Xn[sub], prn[sub])
-                red = torch.cat([(J.T @ J).reshape(-1) * inv_ns, wg.grad.detach(),
-                                 torch.stack([lsum.detach(), e.detach().abs().sum(),
-                                              (e.detach().abs() / yn.abs().clamp_min(1e-7)).sum(),
-                                              torch.tensor(float(len(yn)), dtype=dt)])])
+                J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), Xg, pg)
+                G = (J.T @ J).reshape(-1) * inv_ns
+                rest = torch.cat([wg.grad.detach(),
+                                  torch.stack([lsum.detach(), e.detach().abs().sum(),
+                                               (e.detach().abs() / yn.abs().clamp_min(1e-7)).sum(),
+                                               torch.tensor(float(len(yn)), dtype=dt)])])
                 if world > 1:
-                    self._allreduce(red)
-                return red[: P * P].reshape(P, P), red[P * P: P * P + P], red[P * P + P:]
+                    if same_g:
+                        self._allreduce(rest)  # (the gradient region only)
+                    else:
+                        red = torch.cat([G, rest])
+                        self._allreduce(red)
+                        G, rest = red[: P * P], red[P * P:]
+                return G.reshape(P, P), rest[:P], rest[P:]
             return evaluate
 
         nielsen = str(t.lm_damping).lower() == "nielsen"
@@ -987,7 +1111,8 @@ class TorchBackend:
                 Lb_old = Lb
                 A = 2.0 * G
                 dg = torch.diagonal(A).clone()
-                dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
+                dmp = torch.clamp_min(dg, float(np.float32(t.lm_diag_floor)) * float(dg.mean())) * lam + \
+                    float(t.lm_ridge) * float(dg.mean())
                 A = A + torch.diag(dmp)
                 Lc, info = torch.linalg.cholesky_ex(A)
                 pred = 0.0
@@ -1063,7 +1188,8 @@ class TorchBackend:
             lam = max(float(sel[pick, 1]), t.lm_lam_min)
             self.lm_explore_last = {"losses": sel[:, 0].tolist(), "pick": pick}
         tol, kmin = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
-        w_best, G, g, stb, Lb, lam, hist = run(w_best, make_eval(self.n_local, W), int(fcfg.epochs), lam, tol, kmin)
+        w_best, G, g, stb, Lb, lam, hist = run(w_best, make_eval(self.n_local, W, main=True), int(fcfg.epochs), lam,
+                                               tol, kmin)
         self._lm_lam_last = lam
         bi = _lm_bias_index(spec, t)
         n_out, out_ok = _lm_out_n(spec, t), False

@@ -89,9 +89,10 @@ class LmDesc(C.Structure):
         ("lam0", C.c_float), ("lam_up", C.c_float), ("lam_down", C.c_float), ("lam_min", C.c_float),
         ("lam_max", C.c_float), ("ridge", C.c_float), ("bias_index", C.c_int), ("weights_only", C.c_int),
         ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("gram_skip", C.c_int),
-        ("inst", C.c_int), ("explore", C.c_int), ("lam_carry", C.c_float), ("pad0", C.c_int), ("w0", VP),
+        ("inst", C.c_int), ("explore", C.c_int), ("lam_carry", C.c_float), ("diag_floor", C.c_float), ("w0", VP),
         ("renorm", C.c_int), ("pad1", C.c_int), ("ren_mu", C.c_float * MAXIN), ("ren_isd", C.c_float * MAXIN),
         ("out_n", C.c_int), ("out_mu", C.c_float), ("out_mean", C.c_int), ("pad3", C.c_int),
+        ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("pad4", C.c_int),
     ]
 
     def __init__(self, *a, **kw):
@@ -120,6 +121,7 @@ class SimDesc(C.Structure):
         ("l0", C.c_double), ("lc", C.c_double), ("eta", C.c_double), ("n0", C.c_int), ("seed", C.c_uint32),
         ("out", VP), ("out2", VP), ("out3", VP), ("final_out", VP), ("final2_out", VP),
         ("sv_tscale", C.c_double), ("scheme", C.c_int), ("pad0", C.c_int),
+        ("map_blk", C.c_longlong), ("map_stride", C.c_longlong),
     ]
 
 
@@ -146,13 +148,15 @@ def _expected_layout() -> list[int]:
         LmDesc.passes.offset, LmDesc.gram_blk.offset, LmDesc.inv_ns.offset, LmDesc.lam0.offset,
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
         LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, LmDesc.renorm.offset,
-        LmDesc.ren_isd.offset, LmDesc.out_n.offset, C.sizeof(LmDesc), L.LMS_LFIN, L.LM_SEL_W,
+        LmDesc.ren_isd.offset, LmDesc.out_n.offset, LmDesc.gfeat.offset, LmDesc.gprice.offset,
+        LmDesc.gram_side.offset, C.sizeof(LmDesc), L.LMS_LFIN, L.LM_SEL_W,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         L.LM_SPEC, L.LMS_SPEC_W, L.LMS_SLOTS, L.LM_SLOT, L.LSS_LBEST, L.LSS_STOP,
         C.sizeof(S), S.path_offset.offset, S.sv1.offset, S.dims1.offset, S.sv2.offset, S.dims2.offset,
         S.s0.offset, S.chol.offset, S.dt.offset, S.inv_norm.offset, S.v0.offset, S.rho.offset, S.l0.offset,
         S.n0.offset, S.seed.offset, S.out.offset, S.final2_out.offset, S.sv_tscale.offset, S.scheme.offset,
+        S.map_blk.offset, S.map_stride.offset,
         L.LAG_SLOTS,
     ]
 

@@ -99,13 +99,27 @@ def _dev_is_gpu(device) -> bool:
 # ---------------------------------------------------------------------------
 # device simulation
 # ---------------------------------------------------------------------------
-def _desc(model, n_local, offset, grid: Grid, fp64, parity):
+def path_indices(n_local: int, offset: int, index_map=None) -> np.ndarray:
+    """Global (Sobol / Philox) indices of the local paths: ``offset + p``, or
+    with ``index_map = (blk, stride)`` ``offset + (p // blk) * stride + p % blk``
+    (the LM Gram subsample: the first ``blk`` paths of aligned global blocks,
+    simulated on every rank; csrc/paths.hip sim_gidx)."""
+    p = np.arange(int(n_local), dtype=np.uint64)
+    if index_map is None:
+        return p + np.uint64(offset)
+    blk, stride = (int(v) for v in index_map)
+    return np.uint64(offset) + (p // np.uint64(blk)) * np.uint64(stride) + p % np.uint64(blk)
+
+
+def _desc(model, n_local, offset, grid: Grid, fp64, parity, index_map=None):
     from . import native
 
     d = native.SimDesc()
     d.model = model
     d.n_local = int(n_local)
     d.path_offset = int(offset)
+    if index_map is not None:
+        d.map_blk, d.map_stride = (int(v) for v in index_map)
     d.n_fine = grid.n_fine
     d.reduction = grid.reduction
     d.n_coarse = grid.n_coarse
@@ -118,11 +132,12 @@ def _desc(model, n_local, offset, grid: Grid, fp64, parity):
 
 def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, scheme: str = "arith",
                  norm: float = 1.0, device="cuda", offset: int = 0, fp64: bool = False, seed: int = SEED_W1,
-                 stream=None, out: Paths | None = None) -> Paths:
+                 stream=None, out: Paths | None = None, index_map=None) -> Paths:
     """Fund/stock GBM on the fine grid, stored on the coarse grid (K1+K2+K3).
 
     ``out``: re-simulate into the buffers of an existing :class:`Paths`
-    (no allocation: graph-capturable)."""
+    (no allocation: graph-capturable).  ``index_map``: (blk, stride) global
+    path-index map (:func:`path_indices`)."""
     dev = torch.device(device)
     S = out.S if out is not None else torch.empty(grid.n_coarse, n_local, dtype=torch.float32, device=dev)
     fin = out.S_final if out is not None else torch.empty(n_local, dtype=torch.float32, device=dev)
@@ -130,26 +145,29 @@ def simulate_gbm(grid: Grid, n_local: int, s0: float, mu: float, sigma: float, s
         from . import native
 
         sv, sh, dims = device_table(grid.n_fine, seed, dev)
-        d = _desc(L.SIM_GBM_LOG if scheme == "log" else L.SIM_GBM_ARITH, n_local, offset, grid, fp64, False)
+        d = _desc(L.SIM_GBM_LOG if scheme == "log" else L.SIM_GBM_ARITH, n_local, offset, grid, fp64, False,
+                  index_map)
         d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), dims
         d.s0[0], d.mu[0], d.sigma[0], d.inv_norm[0] = s0, mu, sigma, 1.0 / norm
         d.out, d.final_out = S.data_ptr(), fin.data_ptr()
         native.simulate(d, stream)
     else:
-        s_np, f_np = _cpu_gbm(grid, n_local, s0, mu, sigma, scheme, offset, seed)
+        s_np, f_np = _cpu_gbm(grid, n_local, s0, mu, sigma, scheme, offset, seed, index_map)
         S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
     if out is not None:
         return out
-    return Paths(kind="gbm", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
-                 S_final=fin, norm=norm)
+    p = Paths(kind="gbm", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
+              S_final=fin, norm=norm)
+    p.meta["index_map"] = index_map
+    return p
 
 
 def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model: str = "sv_ref",
                 a=0.0, b=0.0, c=0.0, kappa=0.0, theta=0.0, xi=0.0, rho=0.0, norm: float = 1.0,
                 device="cuda", offset: int = 0, fp64: bool = False, parity_nan: bool = False,
                 seed1: int = SEED_W1, seed2: int = SEED_W2, stream=None, out: Paths | None = None,
-                scheme: str = "qe", sv_tscale: float = 0.0, joint: bool | None = None) -> Paths:
+                scheme: str = "qe", sv_tscale: float = 0.0, joint: bool | None = None, index_map=None) -> Paths:
     """Reference CIR-on-sigma SV (RP:282-289) or Heston (K4).
 
     ``scheme`` (Heston): "qe" = Andersen quadratic-exponential variance step
@@ -180,7 +198,7 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
     if _dev_is_gpu(dev):
         from . import native
 
-        d = _desc(mcode, n_local, offset, grid, fp64, parity_nan)
+        d = _desc(mcode, n_local, offset, grid, fp64, parity_nan, index_map)
         nf = grid.n_fine
         if joint:
             # ONE Sobol sequence of 2 n_fine dimensions: price shocks at dims
@@ -203,18 +221,21 @@ def simulate_sv(grid: Grid, n_local: int, s0: float, mu: float, v0: float, model
     else:
         s_np, v_np, f_np = _cpu_sv(grid, n_local, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset,
                                    parity_nan, seed1, seed2, scheme=scheme,
-                                   sv_tscale=float(sv_tscale) if model == "sv_ref" else 0.0, joint=joint)
+                                   sv_tscale=float(sv_tscale) if model == "sv_ref" else 0.0, joint=joint,
+                                   index_map=index_map)
         S.copy_(torch.from_numpy((s_np / norm).astype(np.float32)))
         V.copy_(torch.from_numpy(v_np.astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm).astype(np.float32)))
     if out is not None:
         return out
-    return Paths(kind="heston" if model == "heston" else "sv", grid=grid, n_local=n_local, path_offset=offset,
-                 S=S, vol=V, bond=grid.bond(0.0), S_final=fin, norm=norm)
+    p = Paths(kind="heston" if model == "heston" else "sv", grid=grid, n_local=n_local, path_offset=offset,
+              S=S, vol=V, bond=grid.bond(0.0), S_final=fin, norm=norm)
+    p.meta["index_map"] = index_map
+    return p
 
 
 def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, device="cuda", offset: int = 0,
-                    seed: int = SEED_W1, stream=None, out: Paths | None = None) -> Paths:
+                    seed: int = SEED_W1, stream=None, out: Paths | None = None, index_map=None) -> Paths:
     """Correlated log-GBM basket (K3 basket variant)."""
     na = len(s0)
     norm = np.asarray(norm if norm is not None else s0, dtype=np.float64)
@@ -227,7 +248,7 @@ def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, de
         from . import native
 
         sv, sh, dims = device_table(na * grid.n_fine, seed, dev)
-        d = _desc(L.SIM_BASKET, n_local, offset, grid, False, False)
+        d = _desc(L.SIM_BASKET, n_local, offset, grid, False, False, index_map)
         d.na = na
         d.sv1, d.shift1, d.dims1 = sv.data_ptr(), sh.data_ptr(), dims
         for i in range(na):
@@ -238,7 +259,7 @@ def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, de
         d.out, d.final_out = S.data_ptr(), fin.data_ptr()
         native.simulate(d, stream)
     else:
-        s_np, f_np = _cpu_basket(grid, n_local, s0, mu, sigma, chol, offset, seed)
+        s_np, f_np = _cpu_basket(grid, n_local, s0, mu, sigma, chol, offset, seed, index_map)
         S.copy_(torch.from_numpy((s_np / norm[None, :, None]).astype(np.float32)))
         fin.copy_(torch.from_numpy((f_np / norm[:, None]).astype(np.float32)))
     if out is not None:
@@ -246,6 +267,7 @@ def simulate_basket(grid: Grid, n_local: int, s0, mu, sigma, corr, norm=None, de
     p = Paths(kind="basket", grid=grid, n_local=n_local, path_offset=offset, S=S, bond=grid.bond(0.0),
               S_final=fin, norm=float(norm[0]), na=na)
     p.meta["norms"] = norm
+    p.meta["index_map"] = index_map
     return p
 
 
@@ -263,14 +285,14 @@ def simulate_mortality(paths: Paths, l0: float, c: float, eta: float, n0: int, l
         from . import native
 
         sv, sh, dims = device_table(grid.n_fine, seed, dev)
-        d = _desc(L.SIM_MORTALITY, n_local, offset, grid, fp64, lambda_fine_index)
+        d = _desc(L.SIM_MORTALITY, n_local, offset, grid, fp64, lambda_fine_index, paths.meta.get("index_map"))
         d.sv2, d.shift2, d.dims2 = sv.data_ptr(), sh.data_ptr(), dims
         d.l0, d.lc, d.eta, d.n0, d.seed = l0, c, eta, int(n0), int(philox_seed)
         d.out2, d.out3, d.final2_out = NF.data_ptr(), LM.data_ptr(), NT.data_ptr()
         native.simulate(d, stream)
     else:
         nf, lm, nt = _cpu_mortality(grid, n_local, l0, c, eta, n0, lambda_fine_index, offset, seed, philox_seed,
-                                    numpy_binomial)
+                                    numpy_binomial, paths.meta.get("index_map"))
         NF.copy_(torch.from_numpy(nf.astype(np.float32)))
         LM.copy_(torch.from_numpy(lm.astype(np.float32)))
         NT.copy_(torch.from_numpy(nt.astype(np.float32)))
@@ -317,14 +339,14 @@ def payoff(kind: str, paths: Paths, strike: float, weights=None, stream=None, ou
 # ---------------------------------------------------------------------------
 # numpy oracles (same Sobol points; fp64 recursion)
 # ---------------------------------------------------------------------------
-def _normals(table_dims, seed, n_local, offset, dims, f32=False):
+def _normals(table_dims, seed, n_local, offset, dims, f32=False, index_map=None):
     tab = sobol_table(table_dims, seed)
-    x = tab.points_u30(np.arange(offset, offset + n_local, dtype=np.uint64), dims=dims).astype(np.int64)
+    x = tab.points_u30(path_indices(n_local, offset, index_map), dims=dims).astype(np.int64)
     return ndtri_u30_f32(np.maximum(x, 1)).astype(np.float64) if f32 else ndtri_u30_f64(x)
 
 
-def _cpu_gbm(grid, n, s0, mu, sigma, scheme, offset, seed):
-    W = _normals(grid.n_fine, seed, n, offset, grid.n_fine)
+def _cpu_gbm(grid, n, s0, mu, sigma, scheme, offset, seed, index_map=None):
+    W = _normals(grid.n_fine, seed, n, offset, grid.n_fine, index_map=index_map)
     dt = grid.dt
     y = np.full(n, math.log(s0) if scheme == "log" else s0, dtype=np.float64)
     out = np.empty((grid.n_coarse, n))
@@ -340,9 +362,9 @@ def _cpu_gbm(grid, n, s0, mu, sigma, scheme, offset, seed):
     return out, fin
 
 
-def _u30(table_dims, seed, n_local, offset, dims):
+def _u30(table_dims, seed, n_local, offset, dims, index_map=None):
     tab = sobol_table(table_dims, seed)
-    return tab.points_u30(np.arange(offset, offset + n_local, dtype=np.uint64), dims=dims).astype(np.int64)
+    return tab.points_u30(path_indices(n_local, offset, index_map), dims=dims).astype(np.int64)
 
 
 def _qe_step(v, z1, x2, dt, mu, kappa, theta, xi, rho):
@@ -378,16 +400,16 @@ def _qe_step(v, z1, x2, dt, mu, kappa, theta, xi, rho):
 
 
 def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, parity_nan, seed1, seed2,
-            scheme="euler", sv_tscale=0.0, joint=None):
+            scheme="euler", sv_tscale=0.0, joint=None, index_map=None):
     if joint is None:
         joint = model == "heston" or (model == "sv_ref" and sv_tscale > 0)
     nf = grid.n_fine
     if joint:  # one 2 n_fine-dimensional sequence (see simulate_sv)
-        X = _u30(2 * nf, seed1, n, offset, 2 * nf)
+        X = _u30(2 * nf, seed1, n, offset, 2 * nf, index_map)
         W1, X2 = ndtri_u30_f64(X[:, :nf]), X[:, nf:]
     else:
-        W1 = _normals(nf, seed1, n, offset, nf)
-        X2 = _u30(nf, seed2, n, offset, nf)
+        W1 = _normals(nf, seed1, n, offset, nf, index_map=index_map)
+        X2 = _u30(nf, seed2, n, offset, nf, index_map)
     W2 = ndtri_u30_f64(X2)
     dt = grid.dt
     ly = np.full(n, math.log(s0))
@@ -422,11 +444,11 @@ def _cpu_sv(grid, n, s0, mu, v0, model, a, b, c, kappa, theta, xi, rho, offset, 
     return S, V, np.exp(ly)
 
 
-def _cpu_basket(grid, n, s0, mu, sigma, chol, offset, seed):
+def _cpu_basket(grid, n, s0, mu, sigma, chol, offset, seed, index_map=None):
     na = len(s0)
     dims = na * grid.n_fine
     tab = sobol_table(dims, seed)
-    idx = np.arange(offset, offset + n, dtype=np.uint64)
+    idx = path_indices(n, offset, index_map)
     x = tab.points_u30(idx, dims=dims).astype(np.int64)
     Wall = ndtri_u30_f64(np.maximum(x, 1))
     dt = grid.dt
@@ -443,15 +465,15 @@ def _cpu_basket(grid, n, s0, mu, sigma, chol, offset, seed):
     return out, np.exp(ly)
 
 
-def _cpu_mortality(grid, n, l0, c, eta, n0, q3, offset, seed, philox_seed, numpy_binomial):
-    W2 = _normals(grid.n_fine, seed, n, offset, grid.n_fine)
+def _cpu_mortality(grid, n, l0, c, eta, n0, q3, offset, seed, philox_seed, numpy_binomial, index_map=None):
+    W2 = _normals(grid.n_fine, seed, n, offset, grid.n_fine, index_map=index_map)
     dt = grid.dt
     lam = np.full(n, float(l0))
     N = np.full(n, int(n0), dtype=np.int64)
     NF = np.empty((grid.n_coarse, n))
     LM = np.empty((grid.n_coarse, n))
     NF[0], LM[0] = 1.0, l0
-    gidx = np.arange(offset, offset + n, dtype=np.uint64)
+    gidx = path_indices(n, offset, index_map)
     for t in range(1, grid.n_fine):
         lam = lam + (c * lam * dt + eta * math.sqrt(dt) * W2[:, t])
         p = np.exp(-lam * dt)

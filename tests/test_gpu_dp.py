@@ -143,9 +143,10 @@ def _ms_starts(spec, k):
     return np.stack([init_weights(spec, [0.5, 0.0], seed=1234 + 1000 * c) for c in range(k)])
 
 
-def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0, n_total=None):
-    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights
+def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0, n_total=None, side=False):
+    from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights, gram_subsample
     from rphedge.models.hedge_mlp import NetSpec, init_weights
+    from rphedge.ops.paths import path_indices
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
     per = n // world
@@ -153,7 +154,13 @@ def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0
     y = y + 0.02 * torch.sin(9 * f)
     be = HipBackend(spec, per, TrainConfig(batch_size=per, lm_gram_paths=2048), device=dev, world=world,
                     rank=rank, mailbox=mailbox, lm_mailbox=lm_mailbox)
-    data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f])
+    gk = {}
+    if side:  # the global Gram subsample, identical on every rank (engine.gram_subsample)
+        ns, blk, stride = gram_subsample(n, 2048)
+        fa, pa, _ = _data(n, dev)
+        idx = torch.as_tensor(path_indices(ns, 0, (blk, stride)).astype(np.int64), device=dev)
+        gk = dict(gram_feats=[fa[idx].contiguous()], gram_prices_next=[pa[idx].contiguous()])
+    data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f], **gk)
     w, o, fs = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
     fc = FitConfig(epochs=passes, optimizer="lm", early_stopping=False)
     if starts:  # multi-start exploration: rank-local starts on a 2^12-path prefix, candidates all-gathered
@@ -168,7 +175,7 @@ def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0
     return current_weights(spec, w), be.lm_state()
 
 
-def _worker_lm(rank, world, port, n, passes, out):
+def _worker_lm(rank, world, port, n, passes, out, side=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     from torch.distributed import distributed_c10d as c10d
@@ -183,7 +190,7 @@ def _worker_lm(rank, world, port, n, passes, out):
     mb = IpcMailbox(rank, world, 128, store, dev, tag="t_lm_a")
     lmb = IpcMailbox(rank, world, L.LM_RED + L.LM_DP_WGS, store, dev, tag="t_lm_b")
     dist.barrier()
-    w, st = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb)
+    w, st = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb, side=side)
     lmb.check()
     np.save(out + f".{rank}.npy", w)
     with open(out + f".{rank}.txt", "w") as fh:
@@ -194,17 +201,22 @@ def _worker_lm(rank, world, port, n, passes, out):
     dist.destroy_process_group()
 
 
-def test_lm_mailbox_exchange_two_ranks_one_gpu():
-    """Levenberg-Marquardt fit over 2 ranks with the reduced [G | g | stats]
-    block exchanged by k_lm_dp_exchange (IPC mailboxes, the xGMI transport):
-    bitwise-identical replicas, and the 1-rank fit of the same global paths
-    (world-invariant Gram subsample; only the fp64 summation order differs)."""
+@pytest.mark.parametrize("side", [False, True])
+def test_lm_mailbox_exchange_two_ranks_one_gpu(side):
+    """Levenberg-Marquardt fit over 2 ranks over the IPC mailboxes (the xGMI
+    transport): bitwise-identical replicas, and the 1-rank fit of the same
+    global paths.  side=True: every rank builds the same Gram matrix from the
+    global subsample (LmDesc.gram_side) and k_lm_dp_exchange_g carries only
+    the 2.1 KB gradient region; side=False: each rank's part of the subsample,
+    the whole [G | g | stats] block exchanged (only the fp64 summation order
+    differs from one rank)."""
     n, passes, world = 1 << 15, 12, 2
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "w")
         ctx = mp.get_context("spawn")
         port = _port()
-        procs = [ctx.Process(target=_worker_lm, args=(r, world, port, n, passes, out)) for r in range(world)]
+        procs = [ctx.Process(target=_worker_lm, args=(r, world, port, n, passes, out, side))
+                 for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
@@ -213,9 +225,19 @@ def test_lm_mailbox_exchange_two_ranks_one_gpu():
         w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
         s0, s1 = open(out + ".0.txt").read(), open(out + ".1.txt").read()
     assert np.array_equal(w0, w1) and s0 == s1
-    ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0))
+    ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0), side=side)
     assert s0 == f"{st['accepted']} {st['chol_failures']}"
     np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
+
+
+def test_lm_gram_side_one_rank_is_bitwise_the_shard_gram():
+    """One rank: the Gram subsample read from simulated subsample data
+    (LmDesc.gram_side) or from the shard (the same global paths) gives the
+    bitwise-identical fit."""
+    dev = torch.device("cuda", 0)
+    w_a, st_a = _lm_fit(0, 1, 1 << 15, 10, dev, side=False)
+    w_b, st_b = _lm_fit(0, 1, 1 << 15, 10, dev, side=True)
+    assert np.array_equal(w_a, w_b) and st_a == st_b
 
 
 def _worker_ms(rank, world, port, n, passes, out):

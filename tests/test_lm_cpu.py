@@ -31,13 +31,36 @@ def test_lm_recovers_teacher_network(shape):
     n = 1 << 12
     feats, pr, y = _teacher_problem(spec, n)
     data = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr)
-    be = TorchBackend(spec, n, TrainConfig(batch_size=n, shuffle=False, lm_gram_paths=2048))
+    be = TorchBackend(spec, n, TrainConfig(batch_size=n, shuffle=False, lm_gram_paths=1024))
     w, o, f = be.new_weights(init_weights(spec, [0.5] * spec.nout, seed=1)), be.new_opt(), be.new_fit()
     be.fit(w, o, f, data, FitConfig(epochs=60, optimizer="lm", early_stopping=False), seed=0)
     hist = be.lm_last["hist"]
     assert min(hist) < 1e-4 * hist[0], hist[-5:]
     assert all(b <= a for a, b in zip(np.minimum.accumulate(hist)[:-1], np.minimum.accumulate(hist)[1:]))
     assert float(f[2048 + 12]) == pytest.approx(min(hist), rel=1e-6)   # F_LAST_LOSS = best loss
+
+
+def test_lm_diag_floor_escapes_degenerate_subsample_curvature():
+    """A 2048-path Gram subsample of the 1-8-8-2 teacher problem gives one
+    parameter (almost) no curvature: with plain Marquardt scaling its step
+    never shrinks, every trial is rejected and the damping runs to lam_max
+    (the fit stalls at 2.6e-3 of the start loss); the damping floor
+    (TrainConfig.lm_diag_floor) makes growing damping shorten every step."""
+    from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig
+    from rphedge.models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(1, 8, 2, 0)
+    n = 1 << 12
+    feats, pr, y = _teacher_problem(spec, n)
+    data = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr)
+    out = {}
+    for floor in (0.0, 1e-6):
+        be = TorchBackend(spec, n, TrainConfig(batch_size=n, shuffle=False, lm_gram_paths=2048, lm_diag_floor=floor))
+        w, o, f = be.new_weights(init_weights(spec, [0.5] * spec.nout, seed=1)), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, FitConfig(epochs=60, optimizer="lm", early_stopping=False), seed=0)
+        out[floor] = (min(be.lm_last["hist"]) / be.lm_last["hist"][0], be.lm_last["lam"])
+    assert out[0.0][0] > 1e-3 and out[0.0][1] >= 1e9          # stalled at the damping ceiling
+    assert out[1e-6][0] < 1e-6                                 # converges with the floor
 
 
 def test_lm_adaptive_budget_stops_early_and_equals_fixed_budget():

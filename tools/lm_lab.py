@@ -46,6 +46,9 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
     from torch.func import jacrev, vmap
 
     flags = VARIANT["flags"]
+    if "fo" in flags and VARIANT["log"]:
+        # first-date-only variant: later dates run the base sequence
+        flags = {f for f in flags if f in ("fo",) or f.startswith("carry=") or f.startswith("adapt=")}
     spec, t = self.spec, self.tcfg
     P = spec.nparams
     dt = torch.float64
@@ -59,6 +62,8 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
     sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
 
     oi = torch.tensor(_out_slice(spec))
+    kvf = dict(f.split("=") for f in flags if "=" in f)
+    vpk = int(kvf["vp"]) if "vp" in kvf else (10**9 if "varpro" in flags else 0)
 
     def v_one(w, x, p):
         return (torch_forward(spec, w, x[None])[0] * p).sum()
@@ -70,7 +75,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
         (lsum / n_glob).backward()
         J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), X[sub], pr[sub])
         G = (J.T @ J) / ns
-        if "varpro" in flags:
+        if "varpro" in flags or "vp" in kvf:
             # output-layer Gram over EVERY path (the loss is exactly quadratic
             # in the output layer): its features are a2 x (price combination)
             with torch.no_grad():
@@ -79,11 +84,11 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
                 G[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
         return G, wg.grad.detach(), float(lsum) / n_glob
 
-    def project(w, G, g, Lv):
+    def project(w, G, g, Lv, Gsub=None):
         """Exact minimiser over the output layer (loss quadratic in it, Gram
         from the subsample): w_o += -G_oo^-1 g_o / 2, loss and gradient
         updated to first order."""
-        Goo = G[oi][:, oi]
+        Goo = (Gsub if Gsub is not None else G)[oi][:, oi]
         try:
             do = torch.linalg.solve(2.0 * Goo + 1e-9 * torch.eye(len(oi), dtype=dt) * Goo.diagonal().mean(), -g[oi])
         except RuntimeError:
@@ -94,10 +99,13 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
         L2 = Lv + 0.5 * float(g[oi] @ do)
         return w2, g2, L2
 
-    def factor(G, lam):
+    def factor(G, lam, k=0):
         A = 2.0 * G
         dg = torch.diagonal(A).clone()
-        dmp = dg * lam + float(t.lm_ridge) * float(dg.mean())
+        fl = float(kvf.get("floor", t.lm_diag_floor))
+        dmp = torch.clamp_min(dg, fl * float(dg.mean())) * lam + float(t.lm_ridge) * float(dg.mean())
+        if "nodo" in flags or k < int(kvf.get("nodo", 0)):
+            dmp[oi] = float(t.lm_ridge) * float(dg.mean())
         Lc, info = torch.linalg.cholesky_ex(A + torch.diag(dmp))
         return (Lc if int(info) == 0 else None), dmp
 
@@ -115,31 +123,34 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
             b1 += W1[f] * io * (mn - mo)
             W1[f] *= io / inn
     VARIANT["norm"] = (tuple(data.fmu), tuple(data.fisd)) if data.fmu else None
-    kv = dict(f.split("=") for f in flags if "=" in f)
+    kv = kvf
     first = not VARIANT["log"]
     lam = float(kv["lf"]) if (first and "lf" in kv) else float(t.lm_lam0)
     if not first and "carry" in kv:
         lam = max(VARIANT["lam_end"] * float(kv["carry"]), t.lm_lam_min)
     G, g, Lb = evaluate(w_best)
-    if "varpro" in flags:
+    if vpk > 0:
         w_best, g, Lb = project(w_best, G, g, Lb)
     hist = [Lb]
     nacc = 0
-    stale = "stale" in flags
+    stale = "stale" in flags or ("stale_rest" in VARIANT["flags"] and not first)
     pend = None  # stale accept-branch factor (pipelined variant)
     for k in range(1, int(fcfg.epochs) + 1):
         if pend is not None:
             Lc, pend = pend, None
         else:
-            Lc, _ = factor(G, lam)
+            Lc, _ = factor(G, lam, k)
         if Lc is None:
             trial = w_best.clone()
             lam = min(lam * t.lm_lam_up * t.lm_lam_up, t.lm_lam_max)
         else:
             trial = w_best + torch.cholesky_solve(-g[:, None], Lc)[:, 0]
         Gt, gt, Lt = evaluate(trial)
-        if "varpro" in flags:
+        if k < vpk:
             trial, gt, Lt = project(trial, Gt, gt, Lt)
+        elif k == vpk and vpk > 0:
+            # leaving the projected phase: re-evaluate the best point exactly
+            pass
         hist.append(Lt)
         Lb_prev = Lb
         if Lt == Lt and Lt < Lb:
@@ -157,7 +168,14 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
                 break
     if os.environ.get("LAB_DEBUG"): print("HIST", json.dumps([float("%.4g" % h) for h in hist]), file=sys.stderr)
     bi = E._lm_bias_index(spec, t)
-    if bi >= 0 and float(G[bi, bi]) > 0.0:
+    if "outfix" in flags:
+        # lm_out_fix: exact output-layer Newton step with the full-batch output Gram
+        with torch.no_grad():
+            Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w_best.detach(), X, pr)[:, oi]
+            Gf = G.clone()
+            Gf[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
+        w_best, g, Lb = project(w_best, Gf, g, Lb)
+    elif bi >= 0 and float(G[bi, bi]) > 0.0:
         w_best = w_best.clone()
         w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
     w32 = w_best.to(torch.float32)
