@@ -81,7 +81,7 @@ PRESETS = {
     "heston30": dict(model="heston", dates=30, substeps=10, paths_log2=20, epochs_first=1024, epochs_rest=16,
                      batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1,
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
-                     optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0,
+                     optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,

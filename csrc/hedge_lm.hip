@@ -73,6 +73,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   __shared__ __attribute__((aligned(16))) float scratch[B::SCRATCH_FLOATS];
   __shared__ __attribute__((aligned(16))) float wl[P + 4];
   __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
+  // the output-Gram image of the OG instantiation (the last passes of an lm_out_fix fit)
+  __shared__ __attribute__((aligned(16))) unsigned char og_img[B::OGM ? B::OG_LDS : 16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   prefetch_kernarg_end(kat);
   // diagnostic phase stamps of every workgroup but 0 and 1 (tools/stamp_lm.py;
@@ -131,11 +133,11 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     // reduced block (G, g, stats), spread over the grid; red_new is rewritten
     // only by this pass's reduce kernel, which runs after this one
     constexpr int NG = LmShape<P>::NBLK * 1024;
+    // g | stats | output Gram (its entry 0 is -1 when the trial's pass did not build it)
+    constexpr int NGR = LM_RED_OUTG - LM_GBLK_MAX + (B::NU <= LM_OG_MAX ? B::NU * (B::NU + 1) / 2 : 1);
     double* best_red = st + LMS_RED;
-    for (int e = blockIdx.x * 256 + tid; e < NG + P + 4 + LM_OUTM; e += (int)gridDim.x * 256) {
-      const int o = e < NG ? e
-                    : (e < NG + P ? LM_GBLK_MAX + e - NG
-                                  : (e < NG + P + 4 ? LM_GBLK_MAX + LM_NPMAX + e - NG - P : LM_RED_OUTM + e - NG - P - 4));
+    for (int e = blockIdx.x * 256 + tid; e < NG + NGR; e += (int)gridDim.x * 256) {
+      const int o = e < NG ? e : LM_GBLK_MAX + e - NG;
       best_red[o] = red_new[o];
     }
   }
@@ -164,7 +166,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     typename B::Frags fr;
     B::make_frags(wl + S::OW2, fr);
     float val[NR];
-    B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_mean != 0);
+    B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_gram != 0, og_img,
+               lm.slab_o + ((size_t)inst * lm.num_wgs + blockIdx.x) * 3 * 1024);
 #pragma unroll
     for (int j = 0; j < NR; ++j)
       if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
@@ -259,7 +262,10 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 // ---------------------------------------------------------------------------
 // Reduce kernel: red[e] = fixed-order sums of the slabs.
 // ---------------------------------------------------------------------------
-template <int P, int R>
+// workgroups of the output-Gram part of k_lm_reduce (64 packed entries each)
+constexpr int lm_og_wgs(int NU) { return NU <= LM_OG_MAX ? (NU * (NU + 1) / 2 + 63) / 64 : 0; }
+
+template <int P, int R, int NU>
 __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
   using LS = LmShape<P>;
   constexpr int NG = LS::NBLK * 1024;
@@ -270,6 +276,53 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
   const float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NG;
   const float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
   const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= NG / 64 + R / 4) {
+    // full-batch output-layer Gram (packed upper triangle, mean over every
+    // path); a pass that did not build it marks entry 0 with -1
+    const bool og_pass = lm.out_gram && pass > lm.passes - LM_OUTG_TAIL;
+    const int ob = blockIdx.x - (NG / 64 + R / 4);
+    if (!og_pass) {
+      if (ob == 0 && tid == 0) red[LM_RED_OUTG] = -1.0;
+      return;
+    }
+    const int l = tid & 63, g = tid >> 6;
+    const int e = ob * 64 + l;
+    constexpr int NPK = NU * (NU + 1) / 2;
+    int off = 0;
+    if (e < NPK) {
+      int i = 0, r = e;  // e -> (i, j), row-major upper triangle
+      while (r >= NU - i) {
+        r -= NU - i;
+        ++i;
+      }
+      const int j = i + r;
+      const int b = (i >> 5) == 0 ? ((j >> 5) == 0 ? 0 : 1) : 2;
+      const int ii = i & 31, jj = j & 31;
+      off = b * 1024 + ((ii & 3) + 4 * (ii >> 3)) * 64 + ((ii >> 2) & 1) * 32 + jj;
+    }
+    const float* const slab_o = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024 + off;
+    double s0 = 0.0, s1 = 0.0;
+    if (e < NPK) {
+      int w = g;
+      for (; w + 16 < lm.num_wgs; w += 32) {
+        s0 += (double)slab_o[(size_t)w * 3 * 1024];
+        s1 += (double)slab_o[(size_t)(w + 16) * 3 * 1024];
+      }
+      if (w < lm.num_wgs) s0 += (double)slab_o[(size_t)w * 3 * 1024];
+    }
+    part[tid] = s0 + s1;
+    __syncthreads();
+    if (g == 0 && e < NPK) {
+      double a = 0.0, bb = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        a += part[q * 64 + l];
+        bb += part[(q + 1) * 64 + l];
+      }
+      red[LM_RED_OUTG + e] = (a + bb) * (double)lm.inv_n;
+    }
+    return;
+  }
   if ((int)blockIdx.x < NG / 64) {
     // Gram: workgroup handles entries [64 b, 64 b + 64); thread (g, l) sums
     // the slabs g, g + 16, ... of entry 64 b + l (every load of a 64-slab
@@ -323,7 +376,6 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     const double v = part[tid];
     if (i < P) red[LM_GBLK_MAX + i] = v;
     else if (i < P + 4) red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
-    else if (i < P + 4 + LM_OUTM) red[LM_RED_OUTM + i - P - 4] = v;  // out-means (0 where unused)
   }
 }
 
@@ -361,24 +413,31 @@ namespace rph {
 
 // Exact Newton step on the OUTPUT block at the best point (the value is
 // linear in the output layer's N = out_n parameters [P - N, P), so the loss
-// is quadratic in them): 2 G_oo d = -g_o with the subsample Gram block, the
-// full-batch gradient, a Marquardt damping out_mu (relative, on the diagonal)
-// and a ridge of lm.ridge x mean diagonal.  The N x N system goes to LDS, the
-// whole workgroup eliminates it (LDL^T, one barrier per column), wave 0 runs
-// both triangular solves by v_readlane (lane i owns entry i, N <= 64), d ->
-// out[0, N).  False (nothing to apply) when a pivot is not positive.  Called
-// by workgroup 0 of the final pass only.
+// is exactly quadratic in them): 2 G_oo d = -g_o with the FULL-BATCH output
+// Gram matrix gog (packed upper triangle, built on the matrix cores by the
+// fit's last passes), the full-batch gradient, a Marquardt damping out_mu
+// (relative, on the diagonal) and a ridge of lm.ridge x mean diagonal.  The
+// N x N system goes to LDS, the whole workgroup eliminates it (LDL^T, one
+// barrier per column), wave 0 runs both triangular solves by v_readlane (lane
+// i owns entry i, N <= 64), d -> out[0, N).  *dl = the exact full-batch loss
+// change g_o.d + d.G_oo d (< 0 for any positive damping).  False (nothing to
+// apply) when a pivot is not positive.  Called by workgroup 0 of the final
+// pass only.
+RPH_INLINE double lm_og(const double* gog, int N, int i, int j) {
+  const int lo = i < j ? i : j, hi = i < j ? j : i;
+  return gog[lo * N - lo * (lo - 1) / 2 + (hi - lo)];
+}
+
 template <int P>
-RPH_INLINE bool lm_out_newton(const double* src, const double* g, const int N, const float ridge, const float mu,
-                              double* A, double* out) {
+RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, const float ridge, const float mu,
+                              double* A, double* out, double* dl) {
 #pragma clang fp contract(off)
-  constexpr int NBG = TileGrid<P>::NBG;
   const int tid = threadIdx.x, lane = tid & 63;
   const int o0 = P - N, LDA = 65;
   __shared__ double s_rid;
   for (int e = tid; e < N * N; e += 256) {
     const int i = e / N, j = e % N;
-    A[i * LDA + j] = 2.0 * lmc_gram<NBG>(src, o0 + i, o0 + j);
+    A[i * LDA + j] = 2.0 * lm_og(gog, N, i, j);
   }
   __syncthreads();
   if (tid < 64) {
@@ -412,7 +471,8 @@ RPH_INLINE bool lm_out_newton(const double* src, const double* g, const int N, c
     // 1 / D_i (v_rcp_f64 + one Newton step, as lm_rcp)
     const double di = lane < N ? A[lane * LDA + lane] : 1.0;
     const double ri = lm_rcp(di);
-    double b = lane < N ? -g[o0 + lane] : 0.0;
+    const double gi = lane < N ? g[o0 + lane] : 0.0;
+    double b = -gi;
     for (int k = 0; k < N; ++k) {
       const double zk = lmc_readlane(b, k) * lmc_readlane(ri, k);  // L_ik z_k = A_ik (z_k / D_k)
       if (lane > k && lane < N) b -= A[lane * LDA + k] * zk;
@@ -422,7 +482,15 @@ RPH_INLINE bool lm_out_newton(const double* src, const double* g, const int N, c
       const double dk = lmc_readlane(b, k);
       if (lane < k) b -= (A[k * LDA + lane] * ri) * dk;
     }
+    if (lane >= N) b = 0.0;
     if (lane < N) out[lane] = b;
+    // exact loss change of the quadratic: g.d + d.G d (G undamped, full batch)
+    double gd = 0.0;
+    for (int j = 0; j < N; ++j) gd += (lane < N ? lm_og(gog, N, lane, j) : 0.0) * lmc_readlane(b, j);
+    double t = b * (gi + gd);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) *dl = t;
   }
   __syncthreads();
   return ok;
@@ -452,9 +520,14 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   __shared__ double s_diag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m = blockIdx.x;
-#define RPH_STAMPS(k)                             \
-  do {                                            \
-    if (m == 0 && blockIdx.y == 0) RPH_STAMP(k);  \
+  // diagnostic phase stamps (tools/stamp_lm.py) of the own-step workgroup,
+  // kept in registers of thread 0 and written to stamp row 0 only at the end
+  // of a full factorising solve, so the row never mixes solves of different kinds
+  unsigned long long ts[8] = {};
+  const bool stamp_on = d.stamps != nullptr && m == 0 && blockIdx.y == 0 && tid == 0;
+#define RPH_STAMPS(k)                                        \
+  do {                                                       \
+    if (stamp_on) ts[(k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   RPH_STAMPS(0);
 #ifdef RPH_LDS_POISON
@@ -560,22 +633,14 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     }
     if (tid == 0) st[LMS_LFIN] = accept ? Lt : Lb;
     if (lm.explore) return;  // exploration: k_lm_select publishes the chosen start point
-    // exact Newton step on the whole (linear) output layer, else on the bond bias alone
+    // exact Newton step on the whole (linear) output layer with the
+    // full-batch output Gram (when the best point's pass built it), else on
+    // the bond bias alone
     const int on = lm.out_n;
-    // (the best point was evaluated by an out-means pass: its bond entry = count x B > 0)
-    const bool have_om = on > 0 && on <= 64 && on <= P && (!lm.out_mean || src[LM_RED_OUTM + on - 1] > 0.0);
-    const bool out_ok = have_om && lm_out_newton<P>(src, g, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65);
-    if (out_ok && lm.out_mean && tid < 64) {
-      // exact mean: the value is linear in the output layer, so after the step
-      // the full-batch mean residual is m + sum_j mu_j d_j (mu = the
-      // out-means / count, m = g_bias / (2 B)); the bond bias (J = B) absorbs it
-      const double* sb = src + LM_GBLK_MAX + LM_NPMAX;
-      const double cnt = fmax(sb[3], 1.0), B = (double)d.bond;
-      double t = tid < on ? (src[LM_RED_OUTM + tid] / cnt) * lds[64 * 65 + tid] : 0.0;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
-      if (tid == 0) lds[64 * 65 + on - 1] -= (g[P - 1] / (2.0 * B) + t) / B;
-    }
+    __shared__ double s_dl;
+    const bool have_og = on > 0 && on <= LM_OG_MAX && on <= P && lm.out_gram && src[LM_RED_OUTG] >= 0.0;
+    const bool out_ok = have_og && lm_out_newton<P>(src + LM_RED_OUTG, g, on, lm.ridge, lm.out_mu, lds,
+                                                    lds + 64 * 65, &s_dl);
     __syncthreads();
     for (int i = tid; i < P; i += 256) {
       double wd = st[LMS_W + best * LM_NPMAX + i];
@@ -599,7 +664,8 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       const double* sb = src + LM_GBLK_MAX + LM_NPMAX;
       const double c = fmax(sb[3], 1.0);
       FitState* f = d.fit;
-      const double lbest = accept ? Lt : Lb;
+      // (after an output step: the exact full-batch loss of the published weights)
+      const double lbest = (accept ? Lt : Lb) + (out_ok ? s_dl : 0.0);
       f->best_loss = (float)lbest;
       f->last_loss = (float)lbest;
       f->last_mae = (float)(sb[1] / c);
@@ -717,6 +783,8 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   RPH_STAMPS(5);
   if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest + vec[tid];
   publish(lam, pred, 1.0);
+  if (stamp_on)
+    for (int k = 0; k < 8; ++k) d.stamps[k] = ts[k];
 #undef RPH_STAMPS
 }
 
@@ -732,15 +800,16 @@ struct LmKernels {
 #endif
   static constexpr bool TWO = RPH_LM_PAIR_WPS == 2 && NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
   using Body = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1>;  // two paths per lane, packed fp32
-  // the same body accumulating the out-means (the last passes of an lm_out_fix fit)
-  using BodyOM = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true>;
+  // the same body + the full-batch output-layer Gram on the matrix cores (the
+  // last LM_OUTG_TAIL passes of an lm_out_fix fit)
+  using BodyOG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true>;
   using S = NetShape<NIN, H, NO, HEAD>;
   // the tile store + vectors + hand-off counters (lm_chol.h)
   static constexpr int smem() { return TileGrid<S::P>::LDS_BYTES; }
   static_assert(smem() + 128 <= 160 * 1024, "LM solve exceeds the LDS of one workgroup");
 };
 
-static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk) {
+static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int nblk, int nu) {
   if (int rc = validate_train(d, 3 /* no schedule buffers */, "rph_lm")) return rc;
   if (!lm->state || !lm->slab_b || !lm->slab_g) return rph_report("rph_lm", "null LM buffer");
   if (d->batch != d->n_local || d->steps_per_epoch != 1) return rph_report("rph_lm", "LM fits are full batch");
@@ -761,7 +830,8 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
     const long long last = ((ns - 1) / lm->gram_blk) * lm->gram_blk_stride + (ns - 1) % lm->gram_blk;
     if (last >= d->n_local) return rph_report("rph_lm", "Gram subsample leaves the shard");
   }
-  if (lm->red_wgs != nblk * 1024 / 64 + R / 4) return rph_report("rph_lm", "bad red_wgs");
+  if (lm->red_wgs != nblk * 1024 / 64 + R / 4 + lm_og_wgs(nu)) return rph_report("rph_lm", "bad red_wgs");
+  if (lm->out_gram && (!lm->slab_o || nu > LM_OG_MAX)) return rph_report("rph_lm", "output Gram needs slab_o (<= 64 output parameters)");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   if (lm->inst < 1 || lm->inst > LM_SEL_MAX) return rph_report("rph_lm", "bad instance count");
   if (lm->inst > 1 && !lm->explore) return rph_report("rph_lm", "several instances are exploration fits only");
@@ -775,10 +845,10 @@ static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const 
   using K = LmKernels<A, B, C, E>;
   // path workgroups + Gram-only workgroups past them (Gram subsample > 64 x path grid)
   const unsigned grid = (unsigned)(lm->gram_wgs > lm->num_wgs ? lm->gram_wgs : lm->num_wgs);
-  if constexpr (K::BodyOM::OUTM) {
-    // the last LM_OUTM_TAIL evaluations of an lm_out_fix fit carry the out-means
-    if (lm->out_mean && pass > lm->passes - LM_OUTM_TAIL) {
-      hipLaunchKernelGGL((k_lm_pass<typename K::BodyOM>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
+  if constexpr (K::BodyOG::OGM) {
+    // the last LM_OUTG_TAIL evaluations of an lm_out_fix fit build the output Gram
+    if (lm->out_gram && pass > lm->passes - LM_OUTG_TAIL) {
+      hipLaunchKernelGGL((k_lm_pass<typename K::BodyOG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
                          red_new);
       return (int)hipGetLastError();
     }
@@ -806,12 +876,11 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange(const LmDpDesc x, double
   __syncthreads();
   const unsigned seq = s_seq;
   const int slot = (int)(seq % DP_SLOTS);
-  const int len = ng + p + 4 + LM_OUTM, chunk = (len + LM_DP_WGS - 1) / LM_DP_WGS;
+  (void)p;
+  const int len = ng + (LM_RED - LM_GBLK_MAX), chunk = (len + LM_DP_WGS - 1) / LM_DP_WGS;
   const int e0 = wg * chunk, e1 = min(len, e0 + chunk);
-  auto off = [&](int e) {  // block entry -> offset in red
-    return e < ng ? e
-                  : (e < ng + p ? LM_GBLK_MAX + e - ng
-                                : (e < ng + p + 4 ? LM_GBLK_MAX + LM_NPMAX + e - ng - p : LM_RED_OUTM + e - ng - p - 4));
+  auto off = [&](int e) {  // block entry -> offset in red: the ng Gram entries, then the gradient region
+    return e < ng ? e : LM_GBLK_MAX + e - ng;
   };
   for (int e = e0 + tid; e < e1; e += 256) {
     const double v = red[off(e)];
@@ -859,10 +928,12 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange(const LmDpDesc x, double
 }
 
 // ---------------------------------------------------------------------------
-// Data-parallel all-reduce of the gradient region [g | stats | out-means] =
-// red[LM_GBLK_MAX, LM_RED) (264 doubles, 2.1 KB) when every rank builds the
-// same Gram matrix from the simulated global subsample (LmDesc.gram_side):
-// ONE workgroup, 132 lanes each push one 16-byte pair to every peer with a
+// Data-parallel all-reduce of the gradient region [g | stats | output Gram]
+// = the first `len` doubles of red[LM_GBLK_MAX, LM_RED) (200 doubles = 1.6 KB;
+// + the packed output Gram in the last passes of an lm_out_fix fit: 171 more
+// for the 1-8-8-2 net) when every rank builds the same Gram matrix from the
+// simulated global subsample (LmDesc.gram_side): ONE workgroup, every lane
+// pushes 16-byte pairs to every peer with a
 // write-through (sc0 sc1: system scope) global_store_dwordx4, drain, one
 // flag per peer (system-scope release), bounded acquire waits, fixed-rank-
 // order sums (bitwise-identical replicas).  Same mailbox rows, flag slot and
@@ -877,7 +948,7 @@ RPH_INLINE void lm_store_sys_b128(double* p, double a, double b) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-__global__ __launch_bounds__(256) void k_lm_dp_exchange_g(const LmDpDesc x, double* __restrict__ red) {
+__global__ __launch_bounds__(256) void k_lm_dp_exchange_g(const LmDpDesc x, double* __restrict__ red, const int len) {
   __shared__ unsigned s_seq;
   const int tid = threadIdx.x, W = x.world, me = x.rank;
   if (tid == 0) s_seq = __hip_atomic_load(x.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -885,12 +956,18 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange_g(const LmDpDesc x, doub
   const unsigned seq = s_seq;
   const int slot = (int)(seq % DP_SLOTS);
   double* const g = red + LM_GBLK_MAX;
-  double v0 = 0.0, v1 = 0.0;
-  if (2 * tid < LM_GREG) {
-    v0 = g[2 * tid];
-    v1 = g[2 * tid + 1];
-    for (int q = 0; q < W; ++q)
-      if (q != me) lm_store_sys_b128(x.mbox[q] + ((size_t)slot * W + me) * x.pitch + 2 * tid, v0, v1);
+  constexpr int NPR = (LM_GREG / 2 + 255) / 256;  // pairs per thread
+  double v0[NPR], v1[NPR];
+#pragma unroll
+  for (int r = 0; r < NPR; ++r) {
+    const int e = 2 * (tid + 256 * r);
+    v0[r] = v1[r] = 0.0;
+    if (e < len) {
+      v0[r] = g[e];
+      v1[r] = g[e + 1];
+      for (int q = 0; q < W; ++q)
+        if (q != me) lm_store_sys_b128(x.mbox[q] + ((size_t)slot * W + me) * x.pitch + e, v0[r], v1[r]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its pushes
   __syncthreads();
@@ -910,20 +987,23 @@ __global__ __launch_bounds__(256) void k_lm_dp_exchange_g(const LmDpDesc x, doub
     }
   }
   __syncthreads();
-  if (2 * tid < LM_GREG) {
+#pragma unroll
+  for (int r = 0; r < NPR; ++r) {
+    const int e = 2 * (tid + 256 * r);
+    if (e >= len) continue;
     double s0 = 0.0, s1 = 0.0;
     for (int q = 0; q < W; ++q) {
       if (q == me) {
-        s0 += v0;
-        s1 += v1;
+        s0 += v0[r];
+        s1 += v1[r];
       } else {
-        const double* m = x.mbox[me] + ((size_t)slot * W + q) * x.pitch + 2 * tid;
+        const double* m = x.mbox[me] + ((size_t)slot * W + q) * x.pitch + e;
         s0 += __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         s1 += __hip_atomic_load(m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    g[2 * tid] = s0;
-    g[2 * tid + 1] = s1;
+    g[e] = s0;
+    g[e + 1] = s1;
   }
   if (tid == 0) __hip_atomic_store(x.counter, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -998,14 +1078,16 @@ extern "C" int rph_lm_select(const TrainDesc* d, const LmDesc* lm, double* sel, 
 extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p, void* stream) {
   if (!x || !red || x->world < 2 || x->world > 8 || x->rank < 0 || x->rank >= x->world)
     return rph_report("rph_lm_dp_exchange", "bad world / rank");
-  if (x->pitch < LM_RED + LM_DP_WGS || ng < 0 || ng > LM_GBLK_MAX || p < 1 || p > LM_NPMAX)
+  if (x->pitch < LM_RED + LM_DP_WGS || ng < 0 || ng > LM_GBLK_MAX || p < 1 || (ng > 0 && p > LM_NPMAX))
     return rph_report("rph_lm_dp_exchange", "bad mailbox pitch / block geometry");
   if ((x->pitch % 2) != 0) return rph_report("rph_lm_dp_exchange", "mailbox rows must be 16-byte aligned");
   for (int q = 0; q < x->world; ++q)
     if (!x->mbox[q]) return rph_report("rph_lm_dp_exchange", "null peer mailbox");
   if (ng == 0) {
-    // no Gram entries: the whole gradient region in one workgroup (16-byte pushes)
-    hipLaunchKernelGGL(k_lm_dp_exchange_g, dim3(1), dim3(256), 0, (hipStream_t)stream, *x, red);
+    // no Gram entries: the first p doubles of the gradient region [g | stats |
+    // output Gram] in one workgroup (16-byte pushes)
+    if (p > LM_GREG || (p & 1)) return rph_report("rph_lm_dp_exchange", "bad gradient-region length");
+    hipLaunchKernelGGL(k_lm_dp_exchange_g, dim3(1), dim3(256), 0, (hipStream_t)stream, *x, red, p);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(k_lm_dp_exchange, dim3(LM_DP_WGS), dim3(256), 0, (hipStream_t)stream, *x, red, ng, p);
@@ -1048,10 +1130,10 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
 #define X(A, B, C, E)                                                                           \
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                  \
     using K = LmKernels<A, B, C, E>;                                                            \
-    if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK)) return rc;      \
+    if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK, K::Body::NU)) return rc; \
     if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R>), dim3(lm->red_wgs, lm->inst), dim3(1024), 0, s, *lm, red_new, \
-                       pass);                                                                   \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R, K::Body::NU>), dim3(lm->red_wgs, lm->inst), dim3(1024), 0, s, \
+                       *lm, red_new, pass);                                                     \
     return (int)hipGetLastError();                                                              \
   }
   RPH_LM_SHAPES(X)

@@ -189,7 +189,13 @@ RPH_INLINE nb_f2 nb_lrelu_bwd(nb_f2 a, nb_f2 da, float alpha) {
 // g += a.x * b.x + a.y * b.y (the pair's contribution to one gradient entry)
 RPH_INLINE float nb_acc(float g, nb_f2 a, nb_f2 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, g)); }
 
-template <int NIN, int H, int NO, int HEAD, int WPS = 2, bool OM = false>
+typedef __bf16 nb_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 nb_bf16x4 __attribute__((ext_vector_type(4)));
+typedef float nb_f32x16 __attribute__((ext_vector_type(16)));
+typedef short nb_s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) nb_s16x4 nb_lds_s16x4;
+
+template <int NIN, int H, int NO, int HEAD, int WPS = 2, bool OG = false>
 struct NarrowPairBody {
   static constexpr int WAVES_PER_SIMD = WPS;  // 2: two workgroups per CU (the 512-workgroup LM pass grid)
   static constexpr int NIN_ = NIN, H_ = H, NO_ = NO, HEAD_ = HEAD;
@@ -200,12 +206,24 @@ struct NarrowPairBody {
   static constexpr int NHOLD = S::NHOLD;
   static constexpr int SCRATCH_FLOATS = (4 * R > 1024 ? 4 * R : 1024) + 8;
   static_assert(R <= 256, "one packet entry per thread");
-  // out-means (free heads whose packet has room): packet slots [P + 4, P + 4 +
-  // OUTN) accumulate sum_p dV/dtheta_o (= a2_j price_k, price_k) for the
-  // exact-mean output-layer step of the LM solve (LmDesc.out_n)
-  static constexpr int OUTN = HEAD == HEAD_FREE ? H * NO + NO : 0;
-  static constexpr bool FITS_OUTM = HEAD == HEAD_FREE && P + 4 + OUTN <= R;
-  static constexpr bool OUTM = OM && FITS_OUTM;  // (its own kernel: the extra sums cost registers)
+  // Full-batch output-layer Gram matrix (OG: the last passes of an lm_out_fix
+  // fit): the value is linear in the output layer's NU parameters, u_p =
+  // dV/dtheta_o = [a2_j c_k (j, k), c_k] with c = the held prices (complement
+  // head: c_0 = S - B), and sum_p u_p u_p^T is a GEMM over the paths.  Per
+  // 128-path iteration every lane writes its two paths' u (bf16) as rows of a
+  // [path][unit] LDS image, the operands (unit r of 8 consecutive paths) come
+  // back with the transposing read ds_read_b64_tr_b16, and
+  // v_mfma_f32_32x32x16_bf16 accumulates the 32 x 32 block(s) in fp32 -
+  // 8 (NU <= 32) or 24 (NU <= 64) matrix-core ops per iteration, issued beside
+  // the VALU body.  bf16 rounding of u keeps the matrix an exact Gram matrix
+  // (positive semidefinite); the output step needs no better than 2^-8.
+  static constexpr int NU = HEAD == HEAD_FREE ? H * NO + NO : H + 1;
+  static constexpr int NUP = NU <= 32 ? 32 : 64;
+  static constexpr int NBO = NUP == 32 ? 1 : 3;  // upper-triangular 32 x 32 blocks
+  static constexpr int OG_PITCH = 2 * NUP + 8;   // bytes per image row (+8: write-conflict padding)
+  static constexpr int OG_LDS = 4 * 128 * OG_PITCH;
+  static constexpr bool OGM = OG && NU <= 64;
+  static_assert(!OG || NU <= 64, "output-layer Gram: at most 64 output parameters");
   struct Frags {};
   struct Pre {
     nb_f2 x[NIN], pr[NHOLD], y;
@@ -247,9 +265,39 @@ struct NarrowPairBody {
     p.m = nb_f2{va ? 1.f : 0.f, vb ? 1.f : 0.f};
   }
 
+  // wave-level LDS ordering around the image (all lanes of the wave active)
+  RPH_INLINE static void og_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // this lane's unit slice [c0, c0 + 4) of row `row` of the image, bf16
+  RPH_INLINE static void og_put(unsigned char* img, int row, int c0, float u0, float u1, float u2, float u3) {
+    const nb_bf16x4 v = {(__bf16)u0, (__bf16)u1, (__bf16)u2, (__bf16)u3};
+    *(nb_bf16x4*)(img + row * OG_PITCH + 2 * c0) = v;
+  }
+  // MFMA fragment of unit block ub, K-step s (16 paths): unit 32 ub + lane % 32
+  // of the 8 paths 16 s + 8 (lane / 32) .. + 7 (two transposing reads)
+  RPH_INLINE static nb_bf16x8 og_frag(const unsigned char* img, int s, int ub, int lane) {
+    const int grp = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int c0 = 32 * ub + 16 * (grp & 1), hh = grp >> 1;
+    nb_bf16x8 f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int off = (16 * s + 8 * hh + 4 * t + q) * OG_PITCH + (c0 + 4 * p) * 2;
+      const nb_s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) f[4 * t + e] = __builtin_bit_cast(__bf16, r[e]);
+    }
+    return f;
+  }
+
+  // og_lds: OG_LDS bytes of LDS (the OG instantiation), og_out: this
+  // workgroup's NBO x 1024 output-Gram floats (MFMA register layout)
   RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
                                  const Frags&, float* lds, Pre& pre, float (&val)[NR], const Sched& sc,
-                                 const bool outm = false) {
+                                 const bool og = false, unsigned char* og_lds = nullptr,
+                                 float* __restrict__ og_out = nullptr) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long long stride = sc.bstep * 128;
     const long long jend = sc.bend * 128 < d.batch ? sc.bend * 128 : d.batch;
@@ -259,6 +307,21 @@ struct NarrowPairBody {
     const float alpha = d.alpha;
     const float two_inv = 2.f * d.inv_batch;
     Pre cur = pre;
+    nb_f32x16 oacc[NBO];
+    unsigned char* const img = og_lds + wid * 128 * OG_PITCH;
+    if constexpr (OGM) {
+#pragma unroll
+      for (int b = 0; b < NBO; ++b) oacc[b] = nb_f32x16{};
+      if (og) {
+        // the image's padding units [NU4, NUP) stay zero (written once)
+        constexpr int NU4 = (NU + 3) / 4 * 4;
+#pragma unroll
+        for (int c0 = NU4; c0 < NUP; c0 += 4) {
+          og_put(img, lane, c0, 0.f, 0.f, 0.f, 0.f);
+          og_put(img, 64 + lane, c0, 0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
     for (long long j0 = sc.b0 * 128; j0 < jend; j0 += stride) {
       // opaque 16-byte-aligned weight base: every weight use is an LDS
       // broadcast read off one address register (register budget)
@@ -314,15 +377,49 @@ struct NarrowPairBody {
       g[P + 1] += ae.x + ae.y;
       g[P + 2] += ape.x + ape.y;
       g[P + 3] += m.x + m.y;
-      if constexpr (OUTM) {
-        if (outm) {
+      if constexpr (OGM) {
+        if (og) {
+          // u of both paths (masked) -> image rows lane, 64 + lane
+          nb_f2 c[NO];
+          if (HEAD == HEAD_COMPLEMENT) {
+            c[0] = (pr[0] - pr[1]) * m;
+          } else {
 #pragma unroll
-        for (int k = 0; k < NO; ++k) {
-          const nb_f2 mp = m * pr[k];
-          g[P + 4 + H * NO + k] += mp.x + mp.y;
+            for (int k = 0; k < NO; ++k) c[k] = pr[k] * m;
+          }
+          float ua[(NU + 3) / 4 * 4], ub[(NU + 3) / 4 * 4];
 #pragma unroll
-          for (int j = 0; j < H; ++j) g[P + 4 + j * NO + k] = nb_acc(g[P + 4 + j * NO + k], a2[j], mp);
-        }
+          for (int j = 0; j < H; ++j)
+#pragma unroll
+            for (int k = 0; k < NO; ++k) {
+              const nb_f2 v = a2[j] * c[k];
+              ua[j * NO + k] = v.x;
+              ub[j * NO + k] = v.y;
+            }
+#pragma unroll
+          for (int k = 0; k < NO; ++k) {
+            ua[H * NO + k] = c[k].x;
+            ub[H * NO + k] = c[k].y;
+          }
+#pragma unroll
+          for (int e = NU; e < (NU + 3) / 4 * 4; ++e) ua[e] = ub[e] = 0.f;
+          og_wave_sync();  // the previous iteration's fragment reads are done
+#pragma unroll
+          for (int c0 = 0; c0 < NU; c0 += 4) {
+            og_put(img, lane, c0, ua[c0], ua[c0 + 1], ua[c0 + 2], ua[c0 + 3]);
+            og_put(img, 64 + lane, c0, ub[c0], ub[c0 + 1], ub[c0 + 2], ub[c0 + 3]);
+          }
+          og_wave_sync();
+#pragma unroll
+          for (int s2 = 0; s2 < 8; ++s2) {
+            const nb_bf16x8 f0 = og_frag(img, s2, 0, lane);
+            oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, f0, oacc[0], 0, 0, 0);
+            if constexpr (NBO == 3) {
+              const nb_bf16x8 f1 = og_frag(img, s2, 1, lane);
+              oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, f1, oacc[1], 0, 0, 0);
+              oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, f1, oacc[2], 0, 0, 0);
+            }
+          }
         }
       }
       const nb_f2 dV = e * m * two_inv;
@@ -368,9 +465,27 @@ struct NarrowPairBody {
     constexpr int PER = R / 64;
 #pragma unroll
     for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
+    if constexpr (OGM) {
+      if (og) {
+        // the four waves' output-Gram tiles -> one workgroup tile (fixed order)
+        float* ot = reinterpret_cast<float*>(og_lds);
+        __syncthreads();  // every wave's last fragment reads are done
+#pragma unroll
+        for (int b = 0; b < NBO; ++b)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) ot[(wid * NBO + b) * 1024 + q * 64 + lane] = oacc[b][q];
+      }
+    }
     __syncthreads();
     const int t = threadIdx.x;
     val[0] = (t < R) ? (lds[t] + lds[R + t]) + (lds[2 * R + t] + lds[3 * R + t]) : 0.f;
+    if constexpr (OGM) {
+      if (og) {
+        const float* ot = reinterpret_cast<const float*>(og_lds);
+        for (int e = t; e < NBO * 1024; e += 256)
+          og_out[e] = (ot[e] + ot[NBO * 1024 + e]) + (ot[2 * NBO * 1024 + e] + ot[3 * NBO * 1024 + e]);
+      }
+    }
     __syncthreads();
   }
 };

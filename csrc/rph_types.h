@@ -182,12 +182,16 @@ constexpr int LM_TILE = 64;          // Gram subsample paths per gram workgroup 
 //   G: NB(NB+1)/2 upper-triangular 32x32 blocks in MFMA register order
 //   g: gradient of mean((V - y)^2) [LM_NPMAX]; stats: loss sum, |e| sum, ape sum, count
 constexpr int LM_GBLK_MAX = 21 * 1024;
-// + out-means: the full-batch sums of the output-layer Jacobian (sum over
-// paths of dV/dtheta_o, free-head nets whose packet has room) at LM_RED_OUTM
-constexpr int LM_OUTM = 64;
-constexpr int LM_OUTM_TAIL = 3;  // evaluations of an lm_out_fix fit that carry them: passes - 2 .. passes
-constexpr int LM_RED_OUTM = LM_GBLK_MAX + LM_NPMAX + 8;
-constexpr int LM_RED = LM_RED_OUTM + LM_OUTM;
+// + the output-layer Gram matrix over EVERY path (the value is linear in the
+// output layer's NU <= 64 parameters, so the loss is exactly quadratic in
+// them): G_oo = mean_p u_p u_p^T, u = dV/dtheta_o, packed upper triangle
+// (i <= j, row-major) at LM_RED_OUTG, accumulated on the matrix cores by the
+// last LM_OUTG_TAIL evaluations of an lm_out_fix fit (NarrowPairBody OG)
+constexpr int LM_OUTG = 64 * 65 / 2;
+constexpr int LM_OUTG_TAIL = 3;  // evaluations of an lm_out_fix fit that carry it: passes - 2 .. passes
+constexpr int LM_RED_OUTG = LM_GBLK_MAX + LM_NPMAX + 8;
+constexpr int LM_RED = LM_RED_OUTG + LM_OUTG;
+constexpr int LM_OG_MAX = 64;    // output-layer parameters of the full-batch Gram (two 32-row MFMA blocks)
 // k_lm_solve workgroups of a full solve: workgroup m factorises the system at
 // the damping that m consecutive rejections would reach, so a rejection's
 // solve only publishes a step computed ahead (speculative reject branch)
@@ -281,14 +285,15 @@ struct LmDesc {
   // them); 0: only the bond bias (bias_index) does
   int out_n;
   float out_mu;                  // its Marquardt damping: A_ii = 2 G_ii (1 + out_mu) + ridge x mean diagonal
-  // 1: the pass packet carries the out-means (NarrowPairBody::OUTM, free heads):
-  // the bond bias then absorbs the step's full-batch mean residual exactly
-  int out_mean;
+  // 1: the last LM_OUTG_TAIL passes accumulate the full-batch output-layer
+  // Gram matrix (slab_o -> red[LM_RED_OUTG]); the output step then uses it
+  int out_gram;
   int pad3;
+  float* slab_o;                 // [num_wgs][3][1024] per-workgroup output-layer Gram tiles (MFMA layout)
   // 1: the Gram subsample is read from gfeat / gprice ([ns] per feature /
   // traded asset, slot order = the global subsample, simulated identically on
   // every rank), so every rank builds the same Gram matrix and the data-
-  // parallel exchange carries only [g | stats | out-means]; 0: slot j reads
+  // parallel exchange carries only [g | stats | output Gram]; 0: slot j reads
   // local path (j / gram_blk) * gram_blk_stride + j % gram_blk of the shard
   // (this rank's part of the subsample; the Gram is then summed over ranks)
   const float* gfeat[MAXIN];

@@ -232,17 +232,29 @@ def _lm_bias_index(spec, t) -> int:
     return spec.nparams - 1 if (t.lm_bias_fix and spec.head == L.HEAD_FREE) else -1
 
 
-def lm_out_means(spec) -> bool:
-    """csrc/hedge_narrow.h NarrowPairBody::OUTM: the pass packet has room for
-    the full-batch out-means (free heads with P + 4 + out_n <= R)."""
-    return spec.head == L.HEAD_FREE and spec.nparams + 4 + spec.hidden * spec.nout + spec.nout <= spec.red_width
+def lm_out_nu(spec) -> int:
+    """Output-layer parameters of a net (csrc/hedge_narrow.h NarrowPairBody::NU):
+    free head H x NO + NO, complement head H + 1."""
+    return spec.hidden * spec.nout + spec.nout if spec.head == L.HEAD_FREE else spec.hidden + 1
+
+
+def lm_out_gram(spec) -> bool:
+    """The LM pass can build the full-batch output-layer Gram matrix on the
+    matrix cores (NarrowPairBody OG: at most LM_OG_MAX output parameters)."""
+    return spec.hidden == 8 and lm_out_nu(spec) <= L.LM_OG_MAX
+
+
+def lm_og_wgs(spec) -> int:
+    """Output-Gram workgroups of k_lm_reduce (64 packed entries each)."""
+    nu = lm_out_nu(spec)
+    return (nu * (nu + 1) // 2 + 63) // 64 if nu <= L.LM_OG_MAX else 0
 
 
 def _lm_out_n(spec, t) -> int:
     """LmDesc.out_n: output-layer parameters of the final exact Newton step
-    (TrainConfig.lm_out_fix; only where the out-means keep the full-batch mean
-    residual exact), 0 = the bias step alone."""
-    return spec.hidden * spec.nout + spec.nout if (t.lm_out_fix and lm_out_means(spec)) else 0
+    with the full-batch output Gram (TrainConfig.lm_out_fix), 0 = the bias
+    step alone."""
+    return lm_out_nu(spec) if (t.lm_out_fix and lm_out_gram(spec)) else 0
 
 
 def gram_subsample(n_total: int, lm_gram_paths: int) -> tuple[int, int, int]:
@@ -599,9 +611,12 @@ class HipBackend:
             bufs = dict(state=torch.zeros(L.LMS_FLOATS, dtype=torch.float64, device=dev),
                         red=torch.zeros(L.LM_RED, dtype=torch.float64, device=dev),
                         slab_b=torch.zeros(nw, R, dtype=torch.float32, device=dev),
+                        slab_o=torch.zeros(nw if _lm_out_n(self.spec, t) else 1, 3 * 1024, dtype=torch.float32,
+                                           device=dev),
                         slab_g=torch.zeros(max(gw, gw_local), nblk * 1024, dtype=torch.float32, device=dev))
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
-            lm.num_wgs, lm.red_wgs = nw, nblk * 1024 // 64 + R // 4
+            lm.slab_o = bufs["slab_o"].data_ptr()
+            lm.num_wgs, lm.red_wgs = nw, nblk * 1024 // 64 + R // 4 + lm_og_wgs(self.spec)
             lm.inv_n = 1.0 / float(self.n_local * W)
             # (Gram geometry: per fit, _lm_gram_mode)
             bufs["gram"] = dict(side=(gw, gblk, gstride, 1.0 / float(ns)),
@@ -615,7 +630,7 @@ class HipBackend:
             lm.diag_floor = float(t.lm_diag_floor)
             lm.bias_index = _lm_bias_index(self.spec, t)
             lm.out_n, lm.out_mu = _lm_out_n(self.spec, t), float(t.lm_out_mu)
-            lm.out_mean = 1 if lm.out_n > 0 else 0
+            lm.out_gram = 1 if lm.out_n > 0 else 0
             lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
             lm.gram_skip = int(os.environ.get("RPH_LM_GRAM_SKIP", t.lm_gram_skip))  # (env: tuning sweeps)
             bufs["desc"] = lm
@@ -653,7 +668,31 @@ class HipBackend:
         if self.world <= 1:
             return 0
         P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
-        return 8 * (L.LM_RED - L.LM_GBLK_MAX) if self._lm_same_gram else 8 * (nblk * 1024 + P + 4 + L.LM_OUTM)
+        return 8 * self._lm_greg(False) if self._lm_same_gram else 8 * (nblk * 1024 + L.LM_RED - L.LM_GBLK_MAX)
+
+    def _lm_greg(self, og: bool) -> int:
+        """Doubles of the gradient region a pass exchanges (even: 16-byte
+        pushes): [g (LM_NPMAX) | stats (8)], + the packed output Gram in the
+        passes that build it."""
+        n = L.LM_RED_OUTG - L.LM_GBLK_MAX
+        if og:
+            nu = lm_out_nu(self.spec)
+            n += nu * (nu + 1) // 2
+        return n + (n & 1)
+
+    def lm_exchange_bytes_run(self, passes_first: int, passes_rest: int, dates: int) -> int:
+        """Bytes one rank pushes to each peer over a whole induction (the
+        output-Gram passes carry the packed output Gram as well)."""
+        if self.world <= 1:
+            return 0
+        if not self._lm_same_gram:
+            return self.lm_exchange_bytes() * (passes_first + 1 + (dates - 1) * (passes_rest + 1))
+        og = bool(_lm_out_n(self.spec, self.tcfg))
+        tot = 0
+        for n in [passes_first] + [passes_rest] * (dates - 1):
+            k_og = min(L.LM_OUTG_TAIL, n + 1) if og else 0
+            tot += 8 * ((n + 1 - k_og) * self._lm_greg(False) + k_og * self._lm_greg(True))
+        return tot
 
     def _lm_fit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
         """Enqueue a full-batch Levenberg-Marquardt fit (MSE): ``fcfg.epochs``
@@ -690,7 +729,8 @@ class HipBackend:
             return
         for k in range(lm.passes + 1):
             n.lm_eval(d, lm, b["red"], k, self.stream)
-            self._lm_allreduce(b["red"], gram=not self._lm_same_gram)
+            og = bool(lm.out_gram) and k > lm.passes - L.LM_OUTG_TAIL
+            self._lm_allreduce(b["red"], gram=not self._lm_same_gram, og=og)
             n.lm_solve(d, lm, b["red"], k, self.stream)
 
     def lm_explore_paths(self, fcfg: FitConfig) -> int:
@@ -732,7 +772,7 @@ class HipBackend:
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
             lm.w0 = bufs["w0"].data_ptr()
             lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
-            lm.out_n, lm.out_mean, lm.gram_side = 0, 0, 0  # (rank-local fits on a shard prefix)
+            lm.out_n, lm.out_gram, lm.gram_side = 0, 0, 0  # (rank-local fits on a shard prefix)
             bufs["w0_rows"] = np.ascontiguousarray(rows).tobytes()
             lm.num_wgs, lm.gram_wgs = nw, gw
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
@@ -769,17 +809,24 @@ class HipBackend:
         n.lm_select(d, lm, x["sel"], b["state"], W, self.rank, P, 1, self.stream)
         self.lm_explore_last = x
 
-    def _lm_allreduce(self, red: torch.Tensor, gram: bool = True):
+    def _lm_allreduce(self, red: torch.Tensor, gram: bool = True, og: bool = False):
         """Sum the reduced LM block over the ranks: in-kernel exchange over the
         IPC mailboxes (xGMI transport) or one RCCL all-reduce.  ``gram=False``
         (every rank built the same Gram matrix): only the gradient region
-        red[LM_GBLK_MAX:LM_RED] (264 doubles) travels."""
+        travels, [g | stats] = 200 doubles (1.6 KB), + the packed output Gram
+        in the passes that build it (``og``)."""
         P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
         if self.lm_mailbox is not None:
             x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
-            self.native.lm_dp_exchange(x, red, nblk * 1024 if gram else 0, P, self.stream)
+            if gram:
+                self.native.lm_dp_exchange(x, red, nblk * 1024, P, self.stream)
+            else:
+                self.native.lm_dp_exchange(x, red, 0, self._lm_greg(og), self.stream)
             return
-        self._lm_comm().allreduce_(red if gram else red[L.LM_GBLK_MAX:L.LM_RED], self.stream)
+        if gram:
+            self._lm_comm().allreduce_(red, self.stream)
+        else:
+            self._lm_comm().allreduce_(red[L.LM_GBLK_MAX:L.LM_GBLK_MAX + self._lm_greg(og)], self.stream)
 
     def bias_refit(self, wts, opt, fit, data: DateData, fcfg: FitConfig):
         """Exact refit of the bond holding's output bias after an Adam fit (one
@@ -807,7 +854,7 @@ class HipBackend:
             if self.world > 1:
                 if self.lm_mailbox is not None:
                     x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
-                    self.native.lm_dp_exchange(x, red, 0, 1, self.stream)
+                    self.native.lm_dp_exchange(x, red, 0, L.LM_RED_OUTG - L.LM_GBLK_MAX, self.stream)
                 else:
                     self._lm_comm().allreduce_(red[G:S + 1], self.stream)
             torch.clamp_min(red[S:S + 1], 1.0, out=c["cnt"])
@@ -821,7 +868,7 @@ class HipBackend:
         def make():
             src = b["desc"]
             lm = type(src).from_buffer_copy(src)
-            lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol, lm.out_n, lm.out_mean = 0, 1, 1, 0.0, 0, 0
+            lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol, lm.out_n, lm.out_gram = 0, 1, 1, 0.0, 0, 0
             lm.renorm, lm.lam_carry, lm.gram_side = 0, 0.0, 0  # (not inherited from the main fit's desc)
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
@@ -1193,31 +1240,32 @@ class TorchBackend:
         self._lm_lam_last = lam
         bi = _lm_bias_index(spec, t)
         n_out, out_ok = _lm_out_n(spec, t), False
-        # (only when the best point came from an out-means pass: the last
-        # LM_OUTM_TAIL evaluations, k_lm_pass<BodyOM>)
-        if n_out and self._lm_best_k > int(fcfg.epochs) - L.LM_OUTM_TAIL:  # the solve kernel's lm_out_newton
-            A = 2.0 * G[P - n_out:, P - n_out:]
+        # (only when the best point came from an output-Gram pass: the last
+        # LM_OUTG_TAIL evaluations, k_lm_pass<BodyOG>)
+        self.lm_out_dl = 0.0
+        if n_out and self._lm_best_k > int(fcfg.epochs) - L.LM_OUTG_TAIL:  # the solve kernel's lm_out_newton
+            # the full-batch output-layer Gram matrix G_oo = mean_p u u^T, u = dV/dtheta_o
+            h, no = spec.hidden, spec.nout
+            o = spec.offsets
+            W1 = w_best[o["W1"]:o["b1"]].view(spec.nin, h)
+            a1 = torch.nn.functional.leaky_relu(X @ W1 + w_best[o["b1"]:o["W2"]], spec.alpha)
+            a2 = torch.nn.functional.leaky_relu(a1 @ w_best[o["W2"]:o["b2"]].view(h, h) + w_best[o["b2"]:o["W3"]],
+                                                spec.alpha)
+            c = pr if spec.head == L.HEAD_FREE else (pr[:, 0] - pr[:, 1])[:, None]
+            u = torch.cat([(a2[:, :, None] * c[:, None, :]).reshape(len(c), -1), c], dim=1)
+            Goo = u.T @ u
+            if self.world > 1:
+                self._allreduce(Goo)
+            Goo = Goo / float(self.n_local * self.world)
+            A = 2.0 * Goo
             dgA = torch.diagonal(A).clone()
             A = A + torch.diag(dgA * float(np.float32(t.lm_out_mu))) + \
                 torch.eye(n_out, dtype=dt) * (float(np.float32(t.lm_ridge)) * float(dgA.sum()) / n_out)
             Lc, info = torch.linalg.cholesky_ex(A)
             if int(info) == 0:
-                dlt = torch.cholesky_solve(-g[P - n_out:, None], Lc)[:, 0]
-                # exact mean (lm_out_means): the bond bias absorbs the step's
-                # full-batch mean residual m + mean(J_o) . d
-                h, no = spec.hidden, spec.nout
-                o = spec.offsets
-                W1 = w_best[o["W1"]:o["b1"]].view(spec.nin, h)
-                a1 = torch.nn.functional.leaky_relu(X @ W1 + w_best[o["b1"]:o["W2"]], spec.alpha)
-                a2 = torch.nn.functional.leaky_relu(a1 @ w_best[o["W2"]:o["b2"]].view(h, h) + w_best[o["b2"]:o["W3"]],
-                                                    spec.alpha)
-                mu = torch.cat([(a2[:, :, None] * pr[:, None, :]).mean(0).reshape(-1), pr.mean(0)])
-                if self.world > 1:
-                    mu = mu * float(self.n_local)
-                    self._allreduce(mu)
-                    mu = mu / float(self.n_local * self.world)
-                B = float(data.bond_next)
-                dlt[-1] -= (float(g[P - 1]) / (2.0 * B) + float(mu @ dlt)) / B
+                go = g[P - n_out:]
+                dlt = torch.cholesky_solve(-go[:, None], Lc)[:, 0]
+                self.lm_out_dl = float(go @ dlt + dlt @ Goo @ dlt)  # exact full-batch loss change
                 w_best = w_best.clone()
                 w_best[P - n_out:] += dlt
                 out_ok = True
@@ -1232,8 +1280,8 @@ class TorchBackend:
         fit[L.F_HIST:] = float("nan")  # (as k_lm_pass: passes never run stay NaN)
         fit[L.F_WBEST:L.F_WBEST + P] = w32
         c = max(float(stb[3]), 1.0)
-        fit[L.F_BEST] = Lb
-        fit[L.F_LAST_LOSS] = Lb
+        fit[L.F_BEST] = Lb + self.lm_out_dl
+        fit[L.F_LAST_LOSS] = Lb + self.lm_out_dl
         fit[L.F_LAST_MAE] = float(stb[1]) / c
         fit[L.F_LAST_MAPE] = 100.0 * float(stb[2]) / c
         fit[L.F_EPOCH] = len(hist)

@@ -63,10 +63,11 @@ HESTON_EULER, HESTON_QE = 0, 1   # SimDesc.scheme (csrc/rph_types.h HestonScheme
 LM_NPMAX = 192
 LM_TILE = 64
 LM_GBLK_MAX = 21 * 1024
-LM_OUTM = 64                         # full-batch sums of the output-layer Jacobian (out-means)
-LM_OUTM_TAIL = 3                     # the last evaluations of an lm_out_fix fit carry them
-LM_RED_OUTM = LM_GBLK_MAX + LM_NPMAX + 8
-LM_RED = LM_RED_OUTM + LM_OUTM
+LM_OUTG = 64 * 65 // 2               # full-batch output-layer Gram, packed upper triangle (NU <= 64)
+LM_OUTG_TAIL = 3                     # the last evaluations of an lm_out_fix fit carry it
+LM_RED_OUTG = LM_GBLK_MAX + LM_NPMAX + 8
+LM_RED = LM_RED_OUTG + LM_OUTG
+LM_OG_MAX = 64
 LMS_W = 0
 LMS_RED = 2 * LM_NPMAX
 LMS_BEST = LMS_RED + 2 * LM_RED      # host mirrors of the last solve

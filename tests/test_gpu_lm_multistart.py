@@ -174,29 +174,37 @@ def test_renorm_reexpresses_the_warm_start():
     np.testing.assert_array_equal(got[o_["W1"]:o_["W2"]], current_weights(spec, wc)[o_["W1"]:o_["W2"]])
 
 
-@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (5, 8, 6, 0)])
-def test_output_newton_step_matches_torch(shape):
-    """lm_out_fix: the last solve's Newton step on the output layer
-    (2 G_oo (1 + mu I) d = -g_o, lm_out_newton in one wave) at a fitted point:
-    only the output layer moves, the full-batch loss drops, and by the same
-    amount as with the fp64 torch oracle's step."""
-    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+@pytest.mark.parametrize("shape,fitted", [((1, 8, 2, 0), True), ((5, 8, 6, 0), True), ((2, 8, 2, 0), True),
+                                          ((1, 8, 1, 1), True), ((3, 8, 2, 0), True),
+                                          ((1, 8, 2, 0), False), ((2, 8, 2, 0), False)])
+def test_output_newton_step_matches_torch(shape, fitted):
+    """lm_out_fix: the last solve's Newton step on the output layer with the
+    FULL-BATCH output Gram matrix (built on the matrix cores by the pass,
+    bf16 operands, fp32 accumulation): only the output layer moves, the
+    full-batch loss drops (also from the random init, where the Gram
+    subsample's output block is near-singular), by the fp64 torch oracle's
+    amount, the full-batch mean residual vanishes, and FitState.best_loss
+    reports the full-batch loss of the published weights."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights, lm_out_nu
     from rphedge.models.hedge_mlp import torch_forward
+    from rphedge.ops import layout as L
 
     dev = torch.device("cuda", 0)
     n = 1 << 13
     spec, feats, pr, y, data, w_init = _setup(shape, n, dev, seed=7)
-    # a fitted point (at the random init the output Gram is near-singular)
-    b0 = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=2048), device=dev)
-    w1 = b0.new_weights(w_init)
-    b0.fit(w1, b0.new_opt(), b0.new_fit(), data, FitConfig(epochs=20, optimizer="lm", early_stopping=False), seed=0)
-    torch.cuda.synchronize()
-    w0 = current_weights(spec, w1)
+    w0 = w_init
+    if fitted:
+        b0 = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=2048), device=dev)
+        w1 = b0.new_weights(w_init)
+        b0.fit(w1, b0.new_opt(), b0.new_fit(), data, FitConfig(epochs=20, optimizer="lm", early_stopping=False),
+               seed=0)
+        torch.cuda.synchronize()
+        w0 = current_weights(spec, w1)
     tc = TrainConfig(batch_size=n, lm_gram_paths=2048, lm_out_fix=True)
     fc = FitConfig(epochs=0, optimizer="lm", early_stopping=False)
     be = HipBackend(spec, n, tc, device=dev)
-    w = be.new_weights(w0)
-    be.fit(w, be.new_opt(), be.new_fit(), data, fc, seed=0)
+    w, fit = be.new_weights(w0), be.new_fit()
+    be.fit(w, be.new_opt(), fit, data, fc, seed=0)
     torch.cuda.synchronize()
     got = current_weights(spec, w)
     cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
@@ -204,37 +212,38 @@ def test_output_newton_step_matches_torch(shape):
     wc = tb.new_weights(w0)
     tb.fit(wc, tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
     want = current_weights(spec, wc)
-    n_out = spec.hidden * spec.nout + spec.nout
+    n_out = lm_out_nu(spec)
     np.testing.assert_array_equal(got[:-n_out], w0[:-n_out])
     assert not np.array_equal(got[-n_out:], w0[-n_out:])
+    X = (torch.stack([f.double() for f in feats], 1) - torch.tensor(data.fmu, dtype=torch.float64)) * \
+        torch.tensor(data.fisd, dtype=torch.float64)
+    if spec.head == L.HEAD_FREE:
+        Pm = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
+    else:
+        Pm = torch.stack([pr[0].double(), torch.full((n,), 1.01, dtype=torch.float64)], 1)
 
-    def loss(wv):
-        X = (torch.stack([f.double() for f in feats], 1) - torch.tensor(data.fmu, dtype=torch.float64)) * \
-            torch.tensor(data.fisd, dtype=torch.float64)
-        P = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
-        return float((((torch_forward(spec, torch.tensor(wv, dtype=torch.float64), X) * P).sum(1) - y.double()) ** 2).mean())
-    # the fitted values (not the weights: near-collinear hidden units leave
-    # near-null directions that the fp32 Gram resolves differently) agree
-    l0, lg, lt = loss(w0), loss(got), loss(want)
+    def res(wv):
+        out = torch_forward(spec, torch.tensor(wv, dtype=torch.float64), X)
+        return (out * Pm).sum(1) - y.double()
+
+    l0, lg, lt = [float((res(v) ** 2).mean()) for v in (w0, got, want)]
     assert lg < l0 and lt < l0
+    # the same step (bf16 Gram vs fp64): the fitted values agree
     assert abs(lg - lt) <= 2e-2 * (l0 - lt), (l0, lg, lt)
-
-    def mean_res(wv):
-        X = (torch.stack([f.double() for f in feats], 1) - torch.tensor(data.fmu, dtype=torch.float64)) * \
-            torch.tensor(data.fisd, dtype=torch.float64)
-        P = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
-        return float(((torch_forward(spec, torch.tensor(wv, dtype=torch.float64), X) * P).sum(1) - y.double()).mean())
-    # the out-means keep the full-batch mean residual exact (as the bias step did)
-    assert abs(mean_res(got)) < 1e-4 * float(y.double().abs().mean()) + 1e-6, mean_res(got)
+    # full-batch optimum of the output layer: the mean residual vanishes
+    assert abs(float(res(got).mean())) < 1e-3 * float(y.double().abs().mean()) + 1e-6
+    # FitState: the full-batch loss after the step (predicted exactly from the quadratic)
+    fb = float(fit[L.F_BEST].item())
+    assert abs(fb - lg) <= 2e-2 * (l0 - lg) + 1e-6 * l0, (fb, lg, l0)
 
 
-def test_output_newton_step_needs_out_means():
-    """Nets whose pass packet has no room for the out-means (complement head,
-    the 2-4 input 8-unit nets) keep the bias step: lm_out_fix is off there."""
-    from rphedge.engine import TrainConfig, _lm_out_n, lm_out_means
+def test_output_newton_step_every_lm_shape():
+    """The full-batch output Gram needs no packet room: every 8-unit LM net
+    (complement head and 1-6 inputs included) takes the output-layer step."""
+    from rphedge.engine import TrainConfig, _lm_out_n, lm_out_nu
     from rphedge.models.hedge_mlp import NetSpec
 
     tc = TrainConfig(lm_out_fix=True)
-    assert lm_out_means(NetSpec(1, 8, 2, 0)) and lm_out_means(NetSpec(5, 8, 6, 0))
-    for shp in [(1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0)]:
-        assert _lm_out_n(NetSpec(*shp), tc) == 0
+    for shp in [(1, 8, 2, 0), (5, 8, 6, 0), (1, 8, 1, 1), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (6, 8, 7, 0)]:
+        sp = NetSpec(*shp)
+        assert _lm_out_n(sp, tc) == lm_out_nu(sp) == (9 if shp[3] == 1 else 8 * shp[2] + shp[2])

@@ -14,9 +14,6 @@ from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig  # noqa:
 from rphedge.models.hedge_mlp import NetSpec, init_weights  # noqa: E402
 
 
-TILE_SOLVER = True  # csrc/lm_chol.h (False: the RPH_LM_CHOL_V1 panel stamps)
-
-
 def run(n_log2=20, nin=1, passes=40):
     dev = torch.device("cuda", 0)
     nout = 2 if nin <= 4 else nin + 1
@@ -44,8 +41,9 @@ def run(n_log2=20, nin=1, passes=40):
     order = [k for k in (0, 1, 2, 6, 7, 3, 4, 5) if st[k]]
     ph = {f"solve_phase_{a}_{b}_us": (st[b] - st[a]) / 100.0 for a, b in zip(order, order[1:])}
     s1 = be.stamps[1].cpu().tolist()
-    if TILE_SOLVER and all(s1[k] for k in range(6)) and st[2]:
-        # csrc/lm_chol.h: row 1 = panel wave stamps (0/1 panel 0 wait passed / done, 2/3 panel 1, 4/5 last)
+    if all(s1[k] for k in range(6)) and st[2]:
+        # row 0 = the last FULL solve (k_lm_solve writes it only then), row 1 = its
+        # panel wave (csrc/lm_chol.h: 0/1 panel 0 wait passed / done, 2/3 panel 1, 4/5 last)
         ph["tile_solver_us"] = {"setup_to_panel0_ready": (s1[0] - st[2]) / 100.0,
                                 "panel0": (s1[1] - s1[0]) / 100.0, "wait_panel1": (s1[2] - s1[1]) / 100.0,
                                 "panel1": (s1[3] - s1[2]) / 100.0, "wait_last": (s1[4] - s1[3]) / 100.0,
@@ -53,14 +51,6 @@ def run(n_log2=20, nin=1, passes=40):
                                 "factor_total": (s1[5] - s1[0]) / 100.0,
                                 "backward": (st[7] - st[6]) / 100.0 if st[6] and st[7] else None,
                                 "total_kernel": (st[5] - st[0]) / 100.0 if st[5] else None}
-    elif s1[0] and s1[1] and s1[2]:
-        ph["panel6_phase1_us"] = (s1[1] - s1[0]) / 100.0
-        ph["panel6_phase2_us"] = (s1[2] - s1[1]) / 100.0
-    if s1[4] and st[7]:
-        ph["tri_solves_us"] = (s1[4] - st[7]) / 100.0
-    if s1[3] and s1[4]:
-        ph["forward_solve_us"] = (s1[3] - st[7]) / 100.0
-        ph["backward_solve_us"] = (s1[4] - s1[3]) / 100.0
     # k_lm_pass phases of the last pass over all workgroups >= 2 (rows 0/1 are the solve's)
     import numpy as np
     lmd = be._lm_buffers()["desc"]
