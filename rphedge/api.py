@@ -233,7 +233,8 @@ class HedgeRun:
             if self.kind == "basket":
                 bias = [p_itm / c.n_assets] * c.n_assets + [stats["E_payoff"] - p_itm]
         return hm.init_weights(spec, bias[: spec.nout], seed=c.train.seed,
-                               spread=str(getattr(c.train, "init", "reference")) == "spread")
+                               spread=str(getattr(c.train, "init", "reference")) == "spread",
+                               shared_stream=bool(c.parity.shared_initializer))
 
     def build(self, w0: np.ndarray | None = None):
         c = self.cfg

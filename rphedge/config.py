@@ -44,6 +44,10 @@ class ParityFlags:
                                         # False = one sequence of 2 n_fine dimensions
     keras_fit_only: bool = False        # the Keras fit's weights are used as they are (no exact bias refit
                                         # after the Adam MSE fits, TrainingParams.mean_refit)
+    shared_initializer: bool = False    # ONE seeded RandomNormal instance for every kernel (RP:149, :154-156):
+                                        # with a stateless seeded generator each call restarts the same normal
+                                        # stream, so W2 / W3 begin with W1's values (Keras >= 2.10); False: an
+                                        # independent stream per kernel (what a stateful op seed gives)
 
     @classmethod
     def reference(cls) -> "ParityFlags":

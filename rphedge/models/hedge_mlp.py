@@ -132,7 +132,7 @@ def philox_normal(n: int, seed: int, stream: int = 0) -> np.ndarray:
 
 
 def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1,
-                 spread: bool = False) -> np.ndarray:
+                 spread: bool = False, shared_stream: bool = False) -> np.ndarray:
     """Reference initialisation: kernels ~ N(0, 0.1) (seed 1234), hidden biases 0,
     output bias data-dependent (Q11: ``[1-p_oom, p_oom]`` pension,
     ``mean(payoff)/S0`` European).
@@ -141,14 +141,19 @@ def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1,
     standardised input range instead of all sitting at 0 (b1_j = -c_j |W1_j|,
     c_j evenly spaced in [-1.5, 1.5]), so a kinked target has hidden units
     near its kink from the start (an LM-mode option; the reference keeps
-    zero biases)."""
+    zero biases).
+
+    ``shared_stream``: every kernel is a prefix of ONE normal stream (the
+    reference's single seeded initializer instance reused for all layers,
+    RP:149 / :154-156, under a stateless seeded generator): W2 and W3 begin
+    with W1's values (ParityFlags.shared_initializer)."""
     o = spec.offsets
     w = np.zeros(spec.nparams, dtype=np.float32)
     for k, (name, shp) in enumerate(spec.shapes()):
         if name.endswith("kernel"):
             n = int(np.prod(shp))
             start = {0: o["W1"], 2: o["W2"], 4: o["W3"]}[k]
-            w[start:start + n] = (stddev * philox_normal(n, seed, stream=k)).astype(np.float32)
+            w[start:start + n] = (stddev * philox_normal(n, seed, stream=0 if shared_stream else k)).astype(np.float32)
     if spread and spec.hidden > 1:
         W1 = w[o["W1"]:o["b1"]].reshape(spec.nin, spec.hidden).astype(np.float64)
         c = np.linspace(-1.5, 1.5, spec.hidden)

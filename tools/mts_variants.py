@@ -22,6 +22,9 @@ VARIANTS = {
     "alpha02_restore_end": {"leaky_alpha": 0.2, "parity_flags": {"restore_best_at_end": True}},
     "unshared_q99": {"parity_flags": {"shared_q99_model": False}},
     "blend_sign_corrected": {"parity_flags": {"holdings_blend_sign_rp": False}},
+    # round 4: one seeded initializer instance reused for every kernel (RP:149, :154-156)
+    "shared_init": {"parity_flags": {"shared_initializer": True}},
+    "shared_init_alpha02": {"leaky_alpha": 0.2, "parity_flags": {"shared_initializer": True}},
 }
 
 
