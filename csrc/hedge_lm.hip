@@ -75,6 +75,8 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
   // the output-Gram image of the OG instantiation (the last passes of an lm_out_fix fit)
   __shared__ __attribute__((aligned(16))) unsigned char og_img[B::OGM ? B::OG_LDS : 16];
+  // the gradient-outer-product images of the MG instantiation (A/B, LmDesc.mfma_grad)
+  __shared__ __attribute__((aligned(16))) float mg_img[B::MGM ? B::MG_LDS / 4 : 4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   prefetch_kernarg_end(kat);
   // diagnostic phase stamps of every workgroup but 0 and 1 (tools/stamp_lm.py;
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     B::make_frags(wl + S::OW2, fr);
     float val[NR];
     B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_gram != 0, og_img,
-               lm.slab_o + ((size_t)inst * lm.num_wgs + blockIdx.x) * 3 * 1024);
+               lm.slab_o + ((size_t)inst * lm.num_wgs + blockIdx.x) * 3 * 1024, mg_img);
 #pragma unroll
     for (int j = 0; j < NR; ++j)
       if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
@@ -803,6 +805,10 @@ struct LmKernels {
   // the same body + the full-batch output-layer Gram on the matrix cores (the
   // last LM_OUTG_TAIL passes of an lm_out_fix fit)
   using BodyOG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true>;
+  // A/B (LmDesc.mfma_grad): the W2 / W3 gradient outer products on the matrix cores
+  using BodyMG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, false, true>;
+  using BodyMGOG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true, true>;
+  static constexpr bool HAS_MG = BodyMG::MGM && NIN <= 3;
   using S = NetShape<NIN, H, NO, HEAD>;
   // the tile store + vectors + hand-off counters (lm_chol.h)
   static constexpr int smem() { return TileGrid<S::P>::LDS_BYTES; }
@@ -832,6 +838,8 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   }
   if (lm->red_wgs != nblk * 1024 / 64 + R / 4 + lm_og_wgs(nu)) return rph_report("rph_lm", "bad red_wgs");
   if (lm->out_gram && (!lm->slab_o || nu > LM_OG_MAX)) return rph_report("rph_lm", "output Gram needs slab_o (<= 64 output parameters)");
+  if (lm->mfma_grad && !(d->h == 8 && d->nin <= 3 && (d->head == HEAD_COMPLEMENT || d->nout <= 8)))
+    return rph_report("rph_lm", "mfma_grad: 8-unit nets with up to 3 inputs only");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   if (lm->inst < 1 || lm->inst > LM_SEL_MAX) return rph_report("rph_lm", "bad instance count");
   if (lm->inst > 1 && !lm->explore) return rph_report("rph_lm", "several instances are exploration fits only");
@@ -845,9 +853,21 @@ static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const 
   using K = LmKernels<A, B, C, E>;
   // path workgroups + Gram-only workgroups past them (Gram subsample > 64 x path grid)
   const unsigned grid = (unsigned)(lm->gram_wgs > lm->num_wgs ? lm->gram_wgs : lm->num_wgs);
+  const bool og = lm->out_gram && pass > lm->passes - LM_OUTG_TAIL;
+  if constexpr (K::HAS_MG) {
+    if (lm->mfma_grad) {
+      if (og && K::BodyMGOG::OGM)
+        hipLaunchKernelGGL((k_lm_pass<typename K::BodyMGOG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
+                           red_new);
+      else
+        hipLaunchKernelGGL((k_lm_pass<typename K::BodyMG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
+                           red_new);
+      return (int)hipGetLastError();
+    }
+  }
   if constexpr (K::BodyOG::OGM) {
     // the last LM_OUTG_TAIL evaluations of an lm_out_fix fit build the output Gram
-    if (lm->out_gram && pass > lm->passes - LM_OUTG_TAIL) {
+    if (og) {
       hipLaunchKernelGGL((k_lm_pass<typename K::BodyOG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
                          red_new);
       return (int)hipGetLastError();

@@ -299,7 +299,7 @@ struct LmDesc {
   const float* gfeat[MAXIN];
   const float* gprice[MAXIN];
   int gram_side;
-  int pad4;
+  int mfma_grad;                 // A/B: the W2 / W3 gradient outer products on the matrix cores (NarrowPairBody MG)
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)

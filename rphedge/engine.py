@@ -149,6 +149,9 @@ class TrainConfig:
     # without it).  0 = plain Marquardt scaling (the presets: 1e-6 moved the
     # euro30 8-seed P&L 0.890 -> 0.897 in tools/lm_lab.py, 1e-9 changed nothing)
     lm_diag_floor: float = 0.0
+    # A/B of the LM pass body: the two largest weight-gradient outer products
+    # (W2, W3) on v_mfma_f32_16x16x4_f32 instead of the packed-fp32 VALU
+    lm_mfma_grad: bool = False
     # damping update: "simple" (x lam_down on accept, x lam_up on reject) or
     # "nielsen" (gain ratio rho of actual / predicted reduction: accept
     # x max(1/3, 1 - (2 rho - 1)^3), reject x nu with nu doubling)
@@ -628,6 +631,8 @@ class HipBackend:
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
             lm.diag_floor = float(t.lm_diag_floor)
+            # A/B: W2 / W3 gradient outer products on the matrix cores (RPH_LM_MFMA_GRAD=1 overrides)
+            lm.mfma_grad = int(os.environ.get("RPH_LM_MFMA_GRAD", "1" if t.lm_mfma_grad else "0"))
             lm.bias_index = _lm_bias_index(self.spec, t)
             lm.out_n, lm.out_mu = _lm_out_n(self.spec, t), float(t.lm_out_mu)
             lm.out_gram = 1 if lm.out_n > 0 else 0
