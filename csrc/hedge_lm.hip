@@ -599,9 +599,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   // trial's, copied by the next pass kernel), next precomputed step, best loss
   auto publish = [&](double lam_out, double pred_out, double sidx_out) {
     if (tid == 0) {
-      // adaptive budget: this pass lowered the best loss by less than stop_tol
-      const double lnew = accept ? Lt : Lb;
-      const bool stop_now = lm.stop_tol > 0.f && pass >= lm.stop_min && !(Lb - lnew > (double)lm.stop_tol * lnew);
+      // adaptive budget: an ACCEPTED step that lowered the best loss by less
+      // than stop_tol (rejections only raise the damping: with lam_carry warm
+      // starts the first trial is often rejected before any progress)
+      const bool stop_now = lm.stop_tol > 0.f && pass >= lm.stop_min && accept && !(Lb - Lt > (double)lm.stop_tol * Lt);
       sout[LSS_STOP] = stop_now ? (double)pass : 0.0;
       sout[LSS_BEST] = (double)best;
       sout[LSS_LAM] = lam_out;

@@ -252,8 +252,9 @@ struct LmDesc {
   int weights_only;              // 1: publish the weights only (no FitState / loss history: a bias refit
                                  // after an Adam fit, passes = 0)
   int damping;                   // 0: lam x lam_down / x lam_up on accept / reject; 1: Nielsen (gain ratio)
-  // adaptive pass budget: from the solve of pass stop_min on, a pass that
-  // lowers the best loss by less than stop_tol (relative) ends the fit; the
+  // adaptive pass budget: from the solve of pass stop_min on, an accepted
+  // pass that lowers the best loss by less than stop_tol (relative) ends the
+  // fit (a rejection never does); the
   // remaining launches of the fit return at once (stop_tol = 0: off)
   int stop_min;
   float stop_tol;

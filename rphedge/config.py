@@ -93,8 +93,9 @@ class TrainingParams:
                                      # Levenberg-Marquardt on the GPU: csrc/hedge_lm.hip; pinball fits stay Adam)
     lm_passes_first: int = 80        # LM trial points on the first date (from the random init)
     lm_passes_rest: int = 3          # LM trial points on later dates (warm start, Q18)
-    lm_stop_tol: float = 0.0         # later dates: adaptive pass budget, lm_passes_rest = the cap; a pass that
-                                     # lowers the best loss by < lm_stop_tol (relative) ends the fit (0: off)
+    lm_stop_tol: float = 0.0         # later dates: adaptive pass budget, lm_passes_rest = the cap; an accepted
+                                     # pass that lowers the best loss by < lm_stop_tol (relative) ends the
+                                     # fit; rejections never do (0: off)
     lm_stop_min: int = 2             # ... never before this pass
     init: str = "reference"          # weight init: reference (N(0, 0.1) kernels, zero hidden biases) | spread
                                      # (first-layer breakpoints spread over the standardised inputs)

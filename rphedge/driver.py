@@ -72,6 +72,10 @@ class InductionConfig:
     lm_starts: int = 1
     lm_explore_passes: int = 45
     lm_explore_log2: int = 16
+    # the extra start points use the run's initialiser (TrainingParams.init,
+    # ParityFlags.shared_initializer), so candidate 0 is not the odd one out
+    init_spread: bool = False
+    init_shared_stream: bool = False
     # after each Adam MSE fit: exact refit of the bond holding's output bias
     # (engine bias_refit; LM fits do it in their last solve)
     mean_refit: bool = False
@@ -168,7 +172,9 @@ class BackwardInduction:
             from .models import hedge_mlp as hm
             o = spec.offsets
             b3 = np.asarray(w0, np.float32)[o["b3"]:o["P"]]
-            rows = [np.asarray(w0, np.float32)] + [hm.init_weights(spec, b3, seed=icfg.seed + 1000 * c)
+            rows = [np.asarray(w0, np.float32)] + [hm.init_weights(spec, b3, seed=icfg.seed + 1000 * c,
+                                                                   spread=icfg.init_spread,
+                                                                   shared_stream=icfg.init_shared_stream)
                                                    for c in range(1, icfg.lm_starts * max(world, 1))]
             self.lm_w0s = np.stack(rows)
         self.opt_init = backend.new_opt()

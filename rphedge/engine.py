@@ -86,8 +86,9 @@ class FitConfig:
     # Levenberg-Marquardt passes (MSE fits of the 8-unit nets; ``epochs`` = the
     # number of trial points after the start point; csrc/hedge_lm.hip)
     optimizer: str = "adam"
-    # LM adaptive pass budget: from pass lm_stop_min on, a pass that lowers the
-    # best loss by less than lm_stop_tol (relative) ends the fit (0: off;
+    # LM adaptive pass budget: from pass lm_stop_min on, an accepted pass that
+    # lowers the best loss by less than lm_stop_tol (relative) ends the fit
+    # (rejections never do; 0: off;
     # ``epochs`` stays the cap)
     lm_stop_tol: float = 0.0
     lm_stop_min: int = 2
@@ -1178,7 +1179,8 @@ class TorchBackend:
                 Gt, gt, stt = evaluate(trial)
                 Lt = float(stt[0] / stt[3].clamp_min(1.0))
                 hist.append(Lt)
-                if Lt == Lt and Lt < Lb:
+                accepted = Lt == Lt and Lt < Lb
+                if accepted:
                     if nielsen:
                         rho = (Lb - Lt) / pred if pred > 0.0 else 1.0
                         lam = max(lam * max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3), t.lm_lam_min)
@@ -1192,8 +1194,9 @@ class TorchBackend:
                     nu *= 2.0
                 else:
                     lam = min(lam * t.lm_lam_up, t.lm_lam_max)
-                # adaptive budget (the solve kernel's LSS_STOP rule; fp32 tolerance)
-                if tol > 0.0 and k >= kmin and not (Lb_old - Lb > float(np.float32(tol)) * Lb):
+                # adaptive budget (the solve kernel's LSS_STOP rule, accepted
+                # steps only; fp32 tolerance)
+                if tol > 0.0 and k >= kmin and accepted and not (Lb_old - Lb > float(np.float32(tol)) * Lb):
                     break
             return w_best, G, g, stb, Lb, lam, hist
 

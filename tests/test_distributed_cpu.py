@@ -184,17 +184,17 @@ def test_dp_verbose_save_and_resume_two_ranks():
     assert dp["resumed_phi"] == pytest.approx(r1.phi, rel=2e-3)
 
 
-def _lm_cfg():
+def _lm_cfg(out_fix=False):
     from rphedge.config import ParityFlags, RunConfig, TrainingParams
 
     tr = TrainingParams(batch_size=2048, early_stopping=False, q99=False, optimizer="lm", lm_passes_first=15,
-                        lm_passes_rest=2, lm_gram_paths=2048)
+                        lm_passes_rest=2, lm_gram_paths=2048, lm_out_fix=out_fix)
     return RunConfig(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=0.25, dt=0.25, n_paths=11,
                      payoff="call", option_type="CALL", model="gbm_log", mortality=False, N=1, P=1.0,
                      verbose=False, train=tr, parity=ParityFlags(), device="cpu", backend="torch")
 
 
-def _lm_worker(rank, world, port, out):
+def _lm_worker(rank, world, port, out, out_fix=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -202,22 +202,27 @@ def _lm_worker(rank, world, port, out):
     from rphedge.parallel import dist as D
 
     di = D.init(device="cpu")
-    res = HedgeRun(_lm_cfg(), dist_info=di).run()
+    run = HedgeRun(_lm_cfg(out_fix), dist_info=di)
+    res = run.run()
     if rank == 0:
         with open(out, "w") as f:
-            json.dump({"phi": res.phi, "v0": res.v0, "pnl": res.terminal_pnl["std"]}, f)
+            json.dump({"phi": res.phi, "v0": res.v0, "pnl": res.terminal_pnl["std"],
+                       "out_dl": float(getattr(run.backend, "lm_out_dl", 0.0))}, f)
     D.shutdown()
 
 
-def test_dp_lm_two_ranks_matches_single_process():
+@pytest.mark.parametrize("out_fix", [False, True])
+def test_dp_lm_two_ranks_matches_single_process(out_fix):
     """Levenberg-Marquardt fits data parallel: the per-pass reduced block
     [G | g | stats] is all-reduced, and with the Gram subsample covering every
-    path the 2-rank fit is the 1-process fit."""
+    path the 2-rank fit is the 1-process fit.  out_fix: the final
+    output-layer Newton step's full-batch output Gram matrix is all-reduced
+    too (its step predicts the same loss drop on both sides)."""
     world, port = 2, _free_port()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "lm.json")
         ctx = mp.get_context("spawn")
-        procs = [ctx.Process(target=_lm_worker, args=(r, world, port, out)) for r in range(world)]
+        procs = [ctx.Process(target=_lm_worker, args=(r, world, port, out, out_fix)) for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
@@ -227,7 +232,10 @@ def test_dp_lm_two_ranks_matches_single_process():
     from rphedge.api import HedgeRun
     from rphedge.parallel import dist as D
 
-    ref = HedgeRun(_lm_cfg(), dist_info=D.DistInfo(device=torch.device("cpu"))).run()
+    run = HedgeRun(_lm_cfg(out_fix), dist_info=D.DistInfo(device=torch.device("cpu")))
+    ref = run.run()
+    if out_fix:
+        assert dp["out_dl"] == pytest.approx(run.backend.lm_out_dl, rel=1e-4, abs=1e-12)
     assert dp["phi"] == pytest.approx(ref.phi, rel=1e-5)
     assert dp["v0"] == pytest.approx(ref.v0, rel=1e-5)
     assert dp["pnl"] == pytest.approx(ref.terminal_pnl["std"], rel=1e-4)

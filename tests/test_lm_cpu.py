@@ -64,10 +64,10 @@ def test_lm_diag_floor_escapes_degenerate_subsample_curvature():
 
 
 def test_lm_adaptive_budget_stops_early_and_equals_fixed_budget():
-    """lm_stop_tol: from pass lm_stop_min on, the first pass that lowers the
-    best loss by less than the tolerance (a rejection lowers it by 0) ends
-    the fit.  The stopped fit is the fixed-budget fit of that many passes
-    (same weights, same history)."""
+    """lm_stop_tol: from pass lm_stop_min on, the first ACCEPTED pass that
+    lowers the best loss by less than the tolerance ends the fit (rejections
+    never stop it).  The stopped fit is the fixed-budget fit of that many
+    passes (same weights, same history)."""
     from rphedge.engine import DateData, FitConfig, TorchBackend, TrainConfig
     from rphedge.models.hedge_mlp import NetSpec, init_weights
     from rphedge.ops import layout as L
@@ -87,10 +87,11 @@ def test_lm_adaptive_budget_stops_early_and_equals_fixed_budget():
     w_s, f_s, h_s = run(epochs=60, lm_stop_tol=0.05, lm_stop_min=3)
     k = len(h_s) - 1                      # passes run
     assert 3 <= k < 60
-    # the stopping pass gained < 5 %; every earlier pass from lm_stop_min on gained more
+    # the stopping pass was accepted and gained < 5 %; every earlier accepted
+    # pass from lm_stop_min on gained more
     best = np.minimum.accumulate(h_s)
-    assert not (best[k - 1] - best[k] > 0.05 * best[k])
-    assert all(best[j - 1] - best[j] > np.float32(0.05) * best[j] for j in range(3, k))
+    assert h_s[k] < best[k - 1] and not (best[k - 1] - best[k] > 0.05 * best[k])
+    assert all(best[j - 1] - best[j] > np.float32(0.05) * best[j] for j in range(3, k) if h_s[j] < best[j - 1])
     w_f, f_f, h_f = run(epochs=k)
     assert h_f == h_s
     assert torch.equal(w_s, w_f)
