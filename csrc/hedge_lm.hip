@@ -831,7 +831,8 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
     for (int k = 0; k < nhold - 1; ++k)
       if (!lm->gprice[k]) return rph_report("rph_lm", "null Gram subsample price");
   } else {
-    if (lm->gram_wgs > lm->num_wgs || lm->gram_blk < 1 || lm->gram_blk > lm->gram_blk_stride)
+    // (Gram-only workgroups past num_wgs read the shard too)
+    if (lm->gram_blk < 1 || lm->gram_blk > lm->gram_blk_stride)
       return rph_report("rph_lm", "bad Gram subsample geometry");
     const long long ns = (long long)lm->gram_wgs * LM_TILE;  // the last slot must stay inside the shard
     const long long last = ((ns - 1) / lm->gram_blk) * lm->gram_blk_stride + (ns - 1) % lm->gram_blk;
