@@ -210,20 +210,26 @@ struct NarrowPairBody {
   // fit): the value is linear in the output layer's NU parameters, u_p =
   // dV/dtheta_o = [a2_j c_k (j, k), c_k] with c = the held prices (complement
   // head: c_0 = S - B), and sum_p u_p u_p^T is a GEMM over the paths.  Per
-  // 128-path iteration every lane writes its two paths' u (bf16) as rows of a
-  // [path][unit] LDS image, the operands (unit r of 8 consecutive paths) come
-  // back with the transposing read ds_read_b64_tr_b16, and
-  // v_mfma_f32_32x32x16_bf16 accumulates the 32 x 32 block(s) in fp32 -
-  // 8 (NU <= 32) or 24 (NU <= 64) matrix-core ops per iteration, issued beside
-  // the VALU body.  bf16 rounding of u keeps the matrix an exact Gram matrix
-  // (positive semidefinite); the output step needs no better than 2^-8.
+  // 64-path half of an iteration every lane writes its path's u as a row of a
+  // [path][unit] LDS image, split u = hi + lo into two bf16 halves (hi =
+  // bf16(u), lo = bf16(u - hi): 16 significant bits), the operands (unit r of
+  // 8 consecutive paths) come back with the transposing read
+  // ds_read_b64_tr_b16, and v_mfma_f32_32x32x16_bf16 accumulates hi hi^T +
+  // hi lo^T + lo hi^T of the 32 x 32 block(s) in fp32 - 24 (NU <= 32) or 72
+  // (NU <= 64) matrix-core ops per 128 paths, issued beside the VALU body.
+  // bf16 alone is not enough: the output Gram of a fitted net has condition
+  // numbers of 1e9 and beyond (collinear hidden units), and 2^-8 rounding of u
+  // moved the Newton step by 100x its length (tools/og_precision.py); the
+  // split matches the fp64 step to 1e-5 of its loss reduction.
   static constexpr int NU = HEAD == HEAD_FREE ? H * NO + NO : H + 1;
   static constexpr int NUP = NU <= 32 ? 32 : 64;
   static constexpr int NBO = NUP == 32 ? 1 : 3;  // upper-triangular 32 x 32 blocks
-  static constexpr int OG_PITCH = 2 * NUP + 8;   // bytes per image row (+8: write-conflict padding)
-  static constexpr int OG_LDS = 4 * 128 * OG_PITCH;
+  static constexpr int OG_PITCH = 4 * NUP + 8;   // bytes per image row: [hi | lo] (+8: write-conflict padding)
+  static constexpr int OG_ROWS = 64;             // one path per lane per half-iteration
+  static constexpr int OG_LDS = 4 * OG_ROWS * OG_PITCH;
   static constexpr bool OGM = OG && NU <= 64;
   static_assert(!OG || NU <= 64, "output-layer Gram: at most 64 output parameters");
+  static_assert(4 * NBO * 1024 * 4 <= OG_LDS, "the waves' output-Gram tiles reuse the image LDS");
   // MG (A/B variant, LmDesc.mfma_grad): the two largest weight-gradient outer
   // products, sum_p a1 (x) dz2 (W2, H x H) and sum_p a2 (x) dout (W3, H x NO),
   // on v_mfma_f32_16x16x4_f32 (exact fp32 products) instead of the VALU: per
@@ -282,13 +288,19 @@ struct NarrowPairBody {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // this lane's unit slice [c0, c0 + 4) of row `row` of the image, bf16
+  // this lane's unit slice [c0, c0 + 4) of row `row` of the image: hi at
+  // units c0.., lo at NUP + c0..
   RPH_INLINE static void og_put(unsigned char* img, int row, int c0, float u0, float u1, float u2, float u3) {
-    const nb_bf16x4 v = {(__bf16)u0, (__bf16)u1, (__bf16)u2, (__bf16)u3};
-    *(nb_bf16x4*)(img + row * OG_PITCH + 2 * c0) = v;
+    const __bf16 h0 = (__bf16)u0, h1 = (__bf16)u1, h2 = (__bf16)u2, h3 = (__bf16)u3;
+    const nb_bf16x4 h = {h0, h1, h2, h3};
+    const nb_bf16x4 l = {(__bf16)(u0 - (float)h0), (__bf16)(u1 - (float)h1), (__bf16)(u2 - (float)h2),
+                         (__bf16)(u3 - (float)h3)};
+    *(nb_bf16x4*)(img + row * OG_PITCH + 2 * c0) = h;
+    *(nb_bf16x4*)(img + row * OG_PITCH + 2 * (NUP + c0)) = l;
   }
-  // MFMA fragment of unit block ub, K-step s (16 paths): unit 32 ub + lane % 32
-  // of the 8 paths 16 s + 8 (lane / 32) .. + 7 (two transposing reads)
+  // MFMA fragment of unit block ub (ub + NUP / 32: its lo half), K-step s (16
+  // paths): unit 32 ub + lane % 32 of the 8 paths 16 s + 8 (lane / 32) .. + 7
+  // (two transposing reads)
   RPH_INLINE static nb_bf16x8 og_frag(const unsigned char* img, int s, int ub, int lane) {
     const int grp = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int c0 = 32 * ub + 16 * (grp & 1), hh = grp >> 1;
@@ -319,7 +331,7 @@ struct NarrowPairBody {
     const float two_inv = 2.f * d.inv_batch;
     Pre cur = pre;
     nb_f32x16 oacc[NBO];
-    unsigned char* const img = og_lds + wid * 128 * OG_PITCH;
+    unsigned char* const img = og_lds + wid * OG_ROWS * OG_PITCH;
     typedef float mg_f4 __attribute__((ext_vector_type(4)));
     mg_f4 macc = {0.f, 0.f, 0.f, 0.f};
     float* const mgL = mg_lds + wid * 2 * 128 * 16;  // [path][a1 | a2]
@@ -331,10 +343,7 @@ struct NarrowPairBody {
         // the image's padding units [NU4, NUP) stay zero (written once)
         constexpr int NU4 = (NU + 3) / 4 * 4;
 #pragma unroll
-        for (int c0 = NU4; c0 < NUP; c0 += 4) {
-          og_put(img, lane, c0, 0.f, 0.f, 0.f, 0.f);
-          og_put(img, 64 + lane, c0, 0.f, 0.f, 0.f, 0.f);
-        }
+        for (int c0 = NU4; c0 < NUP; c0 += 4) og_put(img, lane, c0, 0.f, 0.f, 0.f, 0.f);
       }
     }
     for (long long j0 = sc.b0 * 128; j0 < jend; j0 += stride) {
@@ -418,21 +427,31 @@ struct NarrowPairBody {
           }
 #pragma unroll
           for (int e = NU; e < (NU + 3) / 4 * 4; ++e) ua[e] = ub[e] = 0.f;
-          og_wave_sync();  // the previous iteration's fragment reads are done
+          constexpr int LO = NUP / 32;  // unit block of the lo half
 #pragma unroll
-          for (int c0 = 0; c0 < NU; c0 += 4) {
-            og_put(img, lane, c0, ua[c0], ua[c0 + 1], ua[c0 + 2], ua[c0 + 3]);
-            og_put(img, 64 + lane, c0, ub[c0], ub[c0 + 1], ub[c0 + 2], ub[c0 + 3]);
-          }
-          og_wave_sync();
+          for (int h2 = 0; h2 < 2; ++h2) {
+            og_wave_sync();  // the previous half's fragment reads are done
 #pragma unroll
-          for (int s2 = 0; s2 < 8; ++s2) {
-            const nb_bf16x8 f0 = og_frag(img, s2, 0, lane);
-            oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, f0, oacc[0], 0, 0, 0);
-            if constexpr (NBO == 3) {
-              const nb_bf16x8 f1 = og_frag(img, s2, 1, lane);
-              oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, f1, oacc[1], 0, 0, 0);
-              oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, f1, oacc[2], 0, 0, 0);
+            for (int c0 = 0; c0 < NU; c0 += 4) {
+              if (h2) og_put(img, lane, c0, ub[c0], ub[c0 + 1], ub[c0 + 2], ub[c0 + 3]);
+              else og_put(img, lane, c0, ua[c0], ua[c0 + 1], ua[c0 + 2], ua[c0 + 3]);
+            }
+            og_wave_sync();
+#pragma unroll
+            for (int s2 = 0; s2 < OG_ROWS / 16; ++s2) {
+              const nb_bf16x8 h0 = og_frag(img, s2, 0, lane), l0 = og_frag(img, s2, LO, lane);
+              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h0, oacc[0], 0, 0, 0);
+              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l0, oacc[0], 0, 0, 0);
+              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h0, oacc[0], 0, 0, 0);
+              if constexpr (NBO == 3) {
+                const nb_bf16x8 h1 = og_frag(img, s2, 1, lane), l1 = og_frag(img, s2, LO + 1, lane);
+                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h1, oacc[1], 0, 0, 0);
+                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l1, oacc[1], 0, 0, 0);
+                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h1, oacc[1], 0, 0, 0);
+                oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, h1, oacc[2], 0, 0, 0);
+                oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, l1, oacc[2], 0, 0, 0);
+                oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l1, h1, oacc[2], 0, 0, 0);
+              }
             }
           }
         }

@@ -105,6 +105,8 @@ class TrainingParams:
                                      # (0: off, lm_lam0 / lm_lam0_rest)
     lm_out_fix: bool = False         # LM fits end with the exact Newton step on the whole output layer (linear
                                      # in the value) instead of the bond bias alone
+    lm_out_mu: float = 1e-5          # ... its relative Marquardt damping: directions of the output Gram below
+                                     # ~1e-5 of its scale are rounding noise of the fp32-accumulated matrix
     lm_renorm: bool = False          # later dates: the warm start's first layer re-expressed for the date's input
                                      # standardisation (the previous hedge as a function of the raw state)
     lm_starts: int = 1               # first date: multi-start LM exploration, starts per rank (1: off)

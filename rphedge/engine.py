@@ -167,7 +167,10 @@ class TrainConfig:
     # after the last pass: exact Newton step on the whole output layer (the
     # value is linear in it; 2 G_oo d = -g_o), subsuming the bias step
     lm_out_fix: bool = False
-    lm_out_mu: float = 1e-6        # its relative Marquardt damping (near-collinear hidden units)
+    # its relative Marquardt damping (near-collinear hidden units: the output
+    # Gram's condition number reaches 1e9+; below ~1e-5 of its scale the
+    # fp32-accumulated matrix is rounding noise, tools/og_precision.py)
+    lm_out_mu: float = 1e-5
     # run the data-parallel LM sequence (pass + reduce -> all-reduce of the
     # reduced block -> solve, one launch each) even on one rank: the test hook
     # that exercises the RCCL / mailbox exchange path at world size 1

@@ -14,6 +14,8 @@ Variants (combinable with '+'):
   varpro  accept / reject on the loss projected over the (linear) output
           layer: the exact output-layer minimiser is applied to every
           evaluated point before the comparison
+  outfix  lm_out_fix's final output-layer Newton step (full-batch output
+          Gram, fp64); omu=<x>: its relative damping (TrainConfig.lm_out_mu)
 """
 from __future__ import annotations
 
@@ -84,13 +86,14 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
                 G[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
         return G, wg.grad.detach(), float(lsum) / n_glob
 
-    def project(w, G, g, Lv, Gsub=None):
+    def project(w, G, g, Lv, Gsub=None, mu=0.0):
         """Exact minimiser over the output layer (loss quadratic in it, Gram
         from the subsample): w_o += -G_oo^-1 g_o / 2, loss and gradient
-        updated to first order."""
+        updated to first order (mu: lm_out_newton's relative damping)."""
         Goo = (Gsub if Gsub is not None else G)[oi][:, oi]
         try:
-            do = torch.linalg.solve(2.0 * Goo + 1e-9 * torch.eye(len(oi), dtype=dt) * Goo.diagonal().mean(), -g[oi])
+            do = torch.linalg.solve(2.0 * Goo + torch.diag(2.0 * mu * Goo.diagonal()) +
+                                    1e-9 * torch.eye(len(oi), dtype=dt) * Goo.diagonal().mean(), -g[oi])
         except RuntimeError:
             return w, g, Lv
         w2 = w.clone()
@@ -174,7 +177,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
             Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w_best.detach(), X, pr)[:, oi]
             Gf = G.clone()
             Gf[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
-        w_best, g, Lb = project(w_best, Gf, g, Lb)
+        w_best, g, Lb = project(w_best, Gf, g, Lb, mu=float(kvf.get("omu", 0.0)))
     elif bi >= 0 and float(G[bi, bi]) > 0.0:
         w_best = w_best.clone()
         w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
