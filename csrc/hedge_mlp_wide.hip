@@ -191,18 +191,15 @@ RPH_INLINE void outer_mfma_tr(unsigned char* img, const bf16x8 (&a1b)[2], const 
   const int c0 = 16 * (grp & 1), hh = grp >> 1;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    bf16x8 fa, fb;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int off = (16 * s + 8 * hh + 4 * t + q) * TR_PITCH + (c0 + 4 * p) * 2;
-      const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IA + off));
-      const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IB + off));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        fa[4 * t + e] = __builtin_bit_cast(__bf16, ra[e]);
-        fb[4 * t + e] = __builtin_bit_cast(__bf16, rb[e]);
-      }
-    }
+    const int off = (16 * s + 8 * hh + q) * TR_PITCH + (c0 + 4 * p) * 2;
+    const s16x4 ra0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IA + off));
+    const s16x4 ra1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IA + off + 4 * TR_PITCH));
+    const s16x4 rb0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IB + off));
+    const s16x4 rb1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(IB + off + 4 * TR_PITCH));
+    // whole-vector bit casts (element-wise bit_cast<__bf16> inserts were
+    // miscompiled into splats of element 0 in the narrow body's twin)
+    const bf16x8 fa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ra0, ra1, 0, 1, 2, 3, 4, 5, 6, 7));
+    const bf16x8 fb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(rb0, rb1, 0, 1, 2, 3, 4, 5, 6, 7));
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
   }
   // the next tile rewrites the images: its writes must follow these reads

@@ -193,6 +193,7 @@ typedef __bf16 nb_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 nb_bf16x4 __attribute__((ext_vector_type(4)));
 typedef float nb_f32x16 __attribute__((ext_vector_type(16)));
 typedef short nb_s16x4 __attribute__((ext_vector_type(4)));
+typedef short nb_s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) nb_s16x4 nb_lds_s16x4;
 
 template <int NIN, int H, int NO, int HEAD, int WPS = 2, bool OG = false, bool MG = false>
@@ -304,15 +305,12 @@ struct NarrowPairBody {
   RPH_INLINE static nb_bf16x8 og_frag(const unsigned char* img, int s, int ub, int lane) {
     const int grp = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int c0 = 32 * ub + 16 * (grp & 1), hh = grp >> 1;
-    nb_bf16x8 f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int off = (16 * s + 8 * hh + 4 * t + q) * OG_PITCH + (c0 + 4 * p) * 2;
-      const nb_s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) f[4 * t + e] = __builtin_bit_cast(__bf16, r[e]);
-    }
-    return f;
+    const int off = (16 * s + 8 * hh + q) * OG_PITCH + (c0 + 4 * p) * 2;
+    const nb_s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off));
+    const nb_s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off + 4 * OG_PITCH));
+    // whole-vector bit cast: inserting the elements one by one as
+    // bit_cast<__bf16>(r[e]) was miscompiled into splats of r[0]
+    return __builtin_bit_cast(nb_bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 
   // og_lds: OG_LDS bytes of LDS (the OG instantiation), og_out: this
