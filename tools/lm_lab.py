@@ -15,7 +15,9 @@ Variants (combinable with '+'):
           layer: the exact output-layer minimiser is applied to every
           evaluated point before the comparison
   outfix  lm_out_fix's final output-layer Newton step (full-batch output
-          Gram, fp64); omu=<x>: its relative damping (TrainConfig.lm_out_mu)
+          Gram, fp64); omu=<x>: its relative damping (TrainConfig.lm_out_mu);
+          ogtail=<k>: only when the best point is one of the last k
+          evaluations (else the bias step)
 """
 from __future__ import annotations
 
@@ -135,6 +137,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
     if vpk > 0:
         w_best, g, Lb = project(w_best, G, g, Lb)
     hist = [Lb]
+    kbest = 0  # the evaluation the best point came from
     nacc = 0
     stale = "stale" in flags or ("stale_rest" in VARIANT["flags"] and not first)
     pend = None  # stale accept-branch factor (pipelined variant)
@@ -163,6 +166,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
                 # factorised while this pass ran: the previous best Gram
                 pend, _ = factor(G, lam)
             w_best, G, g, Lb = trial, Gt, gt, Lt
+            kbest = k
         else:
             lam = min(lam * t.lm_lam_up, t.lm_lam_max)
         if "adapt" in kv and not first and k >= int(kv.get("kmin", 2)):
@@ -171,7 +175,8 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
                 break
     if os.environ.get("LAB_DEBUG"): print("HIST", json.dumps([float("%.4g" % h) for h in hist]), file=sys.stderr)
     bi = E._lm_bias_index(spec, t)
-    if "outfix" in flags:
+    ntail = int(kvf.get("ogtail", 10**9))  # the output Gram exists for the last ntail evaluations only
+    if "outfix" in flags and kbest > len(hist) - 1 - ntail:
         # lm_out_fix: exact output-layer Newton step with the full-batch output Gram
         with torch.no_grad():
             Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w_best.detach(), X, pr)[:, oi]
