@@ -290,11 +290,7 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     const int l = tid & 63, g = tid >> 6;
     const int e = ob * 64 + l;
     constexpr int NPK = NU * (NU + 1) / 2;
-    // (NU <= 32: a workgroup's slab is [HH | HL], G = HH + HL + HL^T; else
-    // the three upper 32 x 32 blocks of the whole product)
-    constexpr bool HL = NU <= 32;
-    auto reg = [](int ii, int jj) { return ((ii & 3) + 4 * (ii >> 3)) * 64 + ((ii >> 2) & 1) * 32 + jj; };
-    int off = 0, off_hl = 0, off_lh = 0;
+    int off = 0;
     if (e < NPK) {
       int i = 0, r = e;  // e -> (i, j), row-major upper triangle
       while (r >= NU - i) {
@@ -303,23 +299,18 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       }
       const int j = i + r;
       const int b = (i >> 5) == 0 ? ((j >> 5) == 0 ? 0 : 1) : 2;
-      off = b * 1024 + reg(i & 31, j & 31);
-      off_hl = 1024 + reg(i, j);
-      off_lh = 1024 + reg(j, i);
+      const int ii = i & 31, jj = j & 31;
+      off = b * 1024 + ((ii & 3) + 4 * (ii >> 3)) * 64 + ((ii >> 2) & 1) * 32 + jj;
     }
-    const float* const slab_o = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024;
+    const float* const slab_o = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024 + off;
     double s0 = 0.0, s1 = 0.0;
     if (e < NPK) {
-      auto at = [&](int w) {
-        const float* sw = slab_o + (size_t)w * 3 * 1024;
-        return HL ? (double)sw[off] + ((double)sw[off_hl] + (double)sw[off_lh]) : (double)sw[off];
-      };
       int w = g;
       for (; w + 16 < lm.num_wgs; w += 32) {
-        s0 += at(w);
-        s1 += at(w + 16);
+        s0 += (double)slab_o[(size_t)w * 3 * 1024];
+        s1 += (double)slab_o[(size_t)(w + 16) * 3 * 1024];
       }
-      if (w < lm.num_wgs) s0 += at(w);
+      if (w < lm.num_wgs) s0 += (double)slab_o[(size_t)w * 3 * 1024];
     }
     part[tid] = s0 + s1;
     __syncthreads();

@@ -230,13 +230,7 @@ struct NarrowPairBody {
   static constexpr int OG_LDS = 4 * OG_ROWS * OG_PITCH;
   static constexpr bool OGM = OG && NU <= 64;
   static_assert(!OG || NU <= 64, "output-layer Gram: at most 64 output parameters");
-  // NBO = 1: two accumulators, HH = hi hi^T and HL = hi lo^T (lo hi^T = HL^T
-  // is added by k_lm_reduce): 2 matrix-core ops per K-step and no dependency
-  // chain between them; NBO = 3: the three upper blocks, hi hi^T + hi lo^T +
-  // lo hi^T each
-  static constexpr bool OG_HL = NBO == 1;
-  static constexpr int NACC = OG_HL ? 2 : NBO;
-  static_assert(4 * NACC * 1024 * 4 <= OG_LDS, "the waves' output-Gram tiles reuse the image LDS");
+  static_assert(4 * NBO * 1024 * 4 <= OG_LDS, "the waves' output-Gram tiles reuse the image LDS");
   // MG (A/B variant, LmDesc.mfma_grad): the two largest weight-gradient outer
   // products, sum_p a1 (x) dz2 (W2, H x H) and sum_p a2 (x) dout (W3, H x NO),
   // on v_mfma_f32_16x16x4_f32 (exact fp32 products) instead of the VALU: per
@@ -320,7 +314,7 @@ struct NarrowPairBody {
   }
 
   // og_lds: OG_LDS bytes of LDS (the OG instantiation), og_out: this
-  // workgroup's NACC x 1024 output-Gram floats (MFMA register layout)
+  // workgroup's NBO x 1024 output-Gram floats (MFMA register layout)
   RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
                                  const Frags&, float* lds, Pre& pre, float (&val)[NR], const Sched& sc,
                                  const bool og = false, unsigned char* og_lds = nullptr,
@@ -334,7 +328,7 @@ struct NarrowPairBody {
     const float alpha = d.alpha;
     const float two_inv = 2.f * d.inv_batch;
     Pre cur = pre;
-    nb_f32x16 oacc[NACC];
+    nb_f32x16 oacc[NBO];
     unsigned char* const img = og_lds + wid * OG_ROWS * OG_PITCH;
     typedef float mg_f4 __attribute__((ext_vector_type(4)));
     mg_f4 macc = {0.f, 0.f, 0.f, 0.f};
@@ -342,7 +336,7 @@ struct NarrowPairBody {
     float* const mgR = mgL + 128 * 16;              // [path][dz2 | dout | 0]
     if constexpr (OGM) {
 #pragma unroll
-      for (int b = 0; b < NACC; ++b) oacc[b] = nb_f32x16{};
+      for (int b = 0; b < NBO; ++b) oacc[b] = nb_f32x16{};
       if (og) {
         // the image's padding units [NU4, NUP) stay zero (written once)
         constexpr int NU4 = (NU + 3) / 4 * 4;
@@ -445,12 +439,8 @@ struct NarrowPairBody {
             for (int s2 = 0; s2 < OG_ROWS / 16; ++s2) {
               const nb_bf16x8 h0 = og_frag(img, s2, 0, lane), l0 = og_frag(img, s2, LO, lane);
               oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h0, oacc[0], 0, 0, 0);
-              if constexpr (OG_HL) {
-                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l0, oacc[1], 0, 0, 0);
-              } else {
-                oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l0, oacc[0], 0, 0, 0);
-                oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h0, oacc[0], 0, 0, 0);
-              }
+              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l0, oacc[0], 0, 0, 0);
+              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h0, oacc[0], 0, 0, 0);
               if constexpr (NBO == 3) {
                 const nb_bf16x8 h1 = og_frag(img, s2, 1, lane), l1 = og_frag(img, s2, LO + 1, lane);
                 oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h1, oacc[1], 0, 0, 0);
@@ -551,9 +541,9 @@ struct NarrowPairBody {
         float* ot = reinterpret_cast<float*>(og_lds);
         __syncthreads();  // every wave's last fragment reads are done
 #pragma unroll
-        for (int b = 0; b < NACC; ++b)
+        for (int b = 0; b < NBO; ++b)
 #pragma unroll
-          for (int q = 0; q < 16; ++q) ot[(wid * NACC + b) * 1024 + q * 64 + lane] = oacc[b][q];
+          for (int q = 0; q < 16; ++q) ot[(wid * NBO + b) * 1024 + q * 64 + lane] = oacc[b][q];
       }
     }
     __syncthreads();
@@ -569,8 +559,8 @@ struct NarrowPairBody {
     if constexpr (OGM) {
       if (og) {
         const float* ot = reinterpret_cast<const float*>(og_lds);
-        for (int e = t; e < NACC * 1024; e += 256)
-          og_out[e] = (ot[e] + ot[NACC * 1024 + e]) + (ot[2 * NACC * 1024 + e] + ot[3 * NACC * 1024 + e]);
+        for (int e = t; e < NBO * 1024; e += 256)
+          og_out[e] = (ot[e] + ot[NBO * 1024 + e]) + (ot[2 * NBO * 1024 + e] + ot[3 * NBO * 1024 + e]);
       }
     }
     __syncthreads();
