@@ -17,7 +17,8 @@ Variants (combinable with '+'):
   outfix  lm_out_fix's final output-layer Newton step (full-batch output
           Gram, fp64); omu=<x>: its relative damping (TrainConfig.lm_out_mu);
           ogtail=<k>: only when the best point is one of the last k
-          evaluations (else the bias step)
+          evaluations (else the bias step); ogsub=<k>: output Gram over
+          every k-th path only (the gradient stays full-batch)
 """
 from __future__ import annotations
 
@@ -181,7 +182,9 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
         with torch.no_grad():
             Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w_best.detach(), X, pr)[:, oi]
             Gf = G.clone()
-            Gf[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
+            ks = int(kvf.get("ogsub", 1))  # output Gram over every ks-th path only
+            Js = Jo[::ks]
+            Gf[oi[:, None], oi[None, :]] = (Js.T @ Js) / float(len(Js))
         w_best, g, Lb = project(w_best, Gf, g, Lb, mu=float(kvf.get("omu", 0.0)))
     elif bi >= 0 and float(G[bi, bi]) > 0.0:
         w_best = w_best.clone()

@@ -2,7 +2,10 @@
 csrc/hedge_lm.hip) from in-kernel s_memrealtime stamps (100 MHz), plus the
 event-timed cost per LM pass of whole fits.  Diagnostic only.
 
-usage: python tools/stamp_lm.py [n_log2] [nin]
+usage: python tools/stamp_lm.py [n_log2] [nin] [og]
+
+og: lm_out_fix fits (the last LM_OUTG_TAIL passes build the full-batch output
+Gram, k_lm_pass<BodyOG>; the stamped pass is the last one).
 """
 import json
 import sys
@@ -14,7 +17,7 @@ from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig  # noqa:
 from rphedge.models.hedge_mlp import NetSpec, init_weights  # noqa: E402
 
 
-def run(n_log2=20, nin=1, passes=40):
+def run(n_log2=20, nin=1, passes=40, og=False):
     dev = torch.device("cuda", 0)
     nout = 2 if nin <= 4 else nin + 1
     spec = NetSpec(nin=nin, hidden=8, nout=nout, head=0)
@@ -23,7 +26,7 @@ def run(n_log2=20, nin=1, passes=40):
     feats = [(torch.rand(n, generator=g) * 0.5 + 0.75).to(dev) for _ in range(nin)]
     prices = [f * 1.01 for f in feats[: spec.nhold - 1]]
     target = torch.relu(prices[0] - 1.0)
-    be = HipBackend(spec, n, TrainConfig(batch_size=n), device=dev)
+    be = HipBackend(spec, n, TrainConfig(batch_size=n, lm_out_fix=og), device=dev)
     be.stamps = torch.zeros(1024, 8, dtype=torch.int64, device=dev)
     data = DateData(feats=feats, prices_next=prices, bond_next=1.0, target=target, prices_now=feats[:1])
     w0 = init_weights(spec, [0.5] + [0.0] * (nout - 1))
@@ -68,11 +71,12 @@ def run(n_log2=20, nin=1, passes=40):
     pth = (S[:, 2] - S[:, 1]) / 100.0
     ph["pass_paths_us_by_group"] = {f"{'second' if b else 'first'}_half_xcd{x}": round(float(pth[(wg % 8 == x) & ((wg >= len(S) // 2) == b)].mean()), 2)
                                     for b in (False, True) for x in range(8)}
-    return {"n_log2": n_log2, "nin": nin, "passes": passes, "us_per_pass": 1000.0 * e0.elapsed_time(e1) / (passes + 1),
+    return {"n_log2": n_log2, "nin": nin, "passes": passes, "og": og, "us_per_pass": 1000.0 * e0.elapsed_time(e1) / (passes + 1),
             **ph, "lm": be.lm_state()}
 
 
 if __name__ == "__main__":
     n_log2 = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     nin = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    print(json.dumps(run(n_log2, nin)))
+    og = len(sys.argv) > 3 and sys.argv[3] == "og"
+    print(json.dumps(run(n_log2, nin, og=og)))
