@@ -641,12 +641,25 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     // the bond bias alone
     const int on = lm.out_n;
     __shared__ double s_dl;
-    const bool have_og = on > 0 && on <= LM_OG_MAX && on <= P && lm.out_gram && src[LM_RED_OUTG] >= 0.0;
-    const bool out_ok = have_og && lm_out_newton<P>(src + LM_RED_OUTG, g, on, lm.ridge, lm.out_mu, lds,
-                                                    lds + 64 * 65, &s_dl);
+    const bool on_ok = on > 0 && on <= LM_OG_MAX && on <= P && lm.out_gram;
+    // the last evaluation (this pass) built the output Gram: the out step at
+    // the best point when it was accepted, else at the rejected last trial -
+    // published when trial + step beats the best point (its loss change is
+    // exact: the trial's own full-batch Gram and gradient)
+    const bool have_og = on_ok && src[LM_RED_OUTG] >= 0.0;
+    bool out_ok = have_og && lm_out_newton<P>(src + LM_RED_OUTG, g, on, lm.ridge, lm.out_mu, lds,
+                                              lds + 64 * 65, &s_dl);
+    bool use_trial = false;
+    if (!have_og && !stopped && !accept && on_ok && red_new[LM_RED_OUTG] >= 0.0) {
+      const bool ok_t = lm_out_newton<P>(red_new + LM_RED_OUTG, red_new + LM_GBLK_MAX, on, lm.ridge, lm.out_mu,
+                                         lds, lds + 64 * 65, &s_dl);
+      use_trial = ok_t && Lt == Lt && Lt + s_dl < Lb;
+      out_ok = use_trial;
+    }
     __syncthreads();
+    const int pub_pt = use_trial ? trial : best;  // the point the published weights start from
     for (int i = tid; i < P; i += 256) {
-      double wd = st[LMS_W + best * LM_NPMAX + i];
+      double wd = st[LMS_W + pub_pt * LM_NPMAX + i];
       if (out_ok) {
         if (i >= P - on) wd += lds[64 * 65 + i - (P - on)];
       } else if (i == lm.bias_index) {
@@ -668,7 +681,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       const double c = fmax(sb[3], 1.0);
       FitState* f = d.fit;
       // (after an output step: the exact full-batch loss of the published weights)
-      const double lbest = (accept ? Lt : Lb) + (out_ok ? s_dl : 0.0);
+      const double lbest = (use_trial ? Lt : accept ? Lt : Lb) + (out_ok ? s_dl : 0.0);
       f->best_loss = (float)lbest;
       f->last_loss = (float)lbest;
       f->last_mae = (float)(sb[1] / c);

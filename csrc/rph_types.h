@@ -188,7 +188,7 @@ constexpr int LM_GBLK_MAX = 21 * 1024;
 // (i <= j, row-major) at LM_RED_OUTG, accumulated on the matrix cores by the
 // last LM_OUTG_TAIL evaluations of an lm_out_fix fit (NarrowPairBody OG)
 constexpr int LM_OUTG = 64 * 65 / 2;
-constexpr int LM_OUTG_TAIL = 3;  // evaluations of an lm_out_fix fit that carry it: passes - 2 .. passes
+constexpr int LM_OUTG_TAIL = 1;  // evaluations of an lm_out_fix fit that carry it: the last one (passes)
 constexpr int LM_RED_OUTG = LM_GBLK_MAX + LM_NPMAX + 8;
 constexpr int LM_RED = LM_RED_OUTG + LM_OUTG;
 constexpr int LM_OG_MAX = 64;    // output-layer parameters of the full-batch Gram (two 32-row MFMA blocks)

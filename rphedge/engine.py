@@ -1163,6 +1163,7 @@ class TorchBackend:
             Lb = float(stb[0] / stb[3].clamp_min(1.0))
             hist = [Lb]
             self._lm_best_k = 0  # the evaluation the best point came from
+            self._lm_last_eval = (w_best, g, Lb)
             for k in range(1, int(passes) + 1):
                 Lb_old = Lb
                 A = 2.0 * G
@@ -1182,6 +1183,7 @@ class TorchBackend:
                 Gt, gt, stt = evaluate(trial)
                 Lt = float(stt[0] / stt[3].clamp_min(1.0))
                 hist.append(Lt)
+                self._lm_last_eval = (trial, gt, Lt)  # (the last trial: the final out step may start there)
                 accepted = Lt == Lt and Lt < Lb
                 if accepted:
                     if nielsen:
@@ -1251,17 +1253,15 @@ class TorchBackend:
         self._lm_lam_last = lam
         bi = _lm_bias_index(spec, t)
         n_out, out_ok = _lm_out_n(spec, t), False
-        # (only when the best point came from an output-Gram pass: the last
-        # LM_OUTG_TAIL evaluations, k_lm_pass<BodyOG>)
-        self.lm_out_dl = 0.0
-        if n_out and self._lm_best_k > int(fcfg.epochs) - L.LM_OUTG_TAIL:  # the solve kernel's lm_out_newton
-            # the full-batch output-layer Gram matrix G_oo = mean_p u u^T, u = dV/dtheta_o
-            h, no = spec.hidden, spec.nout
+
+        def out_step(wp, gp):
+            """lm_out_newton at point wp (gradient gp): the full-batch output-layer
+            Gram G_oo = mean_p u u^T, u = dV/dtheta_o; (step, exact loss change) or None."""
+            h = spec.hidden
             o = spec.offsets
-            W1 = w_best[o["W1"]:o["b1"]].view(spec.nin, h)
-            a1 = torch.nn.functional.leaky_relu(X @ W1 + w_best[o["b1"]:o["W2"]], spec.alpha)
-            a2 = torch.nn.functional.leaky_relu(a1 @ w_best[o["W2"]:o["b2"]].view(h, h) + w_best[o["b2"]:o["W3"]],
-                                                spec.alpha)
+            W1 = wp[o["W1"]:o["b1"]].view(spec.nin, h)
+            a1 = torch.nn.functional.leaky_relu(X @ W1 + wp[o["b1"]:o["W2"]], spec.alpha)
+            a2 = torch.nn.functional.leaky_relu(a1 @ wp[o["W2"]:o["b2"]].view(h, h) + wp[o["b2"]:o["W3"]], spec.alpha)
             c = pr if spec.head == L.HEAD_FREE else (pr[:, 0] - pr[:, 1])[:, None]
             u = torch.cat([(a2[:, :, None] * c[:, None, :]).reshape(len(c), -1), c], dim=1)
             Goo = u.T @ u
@@ -1273,13 +1273,32 @@ class TorchBackend:
             A = A + torch.diag(dgA * float(np.float32(t.lm_out_mu))) + \
                 torch.eye(n_out, dtype=dt) * (float(np.float32(t.lm_ridge)) * float(dgA.sum()) / n_out)
             Lc, info = torch.linalg.cholesky_ex(A)
-            if int(info) == 0:
-                go = g[P - n_out:]
-                dlt = torch.cholesky_solve(-go[:, None], Lc)[:, 0]
-                self.lm_out_dl = float(go @ dlt + dlt @ Goo @ dlt)  # exact full-batch loss change
-                w_best = w_best.clone()
-                w_best[P - n_out:] += dlt
-                out_ok = True
+            if int(info) != 0:
+                return None
+            go = gp[P - n_out:]
+            dlt = torch.cholesky_solve(-go[:, None], Lc)[:, 0]
+            return dlt, float(go @ dlt + dlt @ Goo @ dlt)  # exact full-batch loss change
+
+        # the solve kernel's final step: the last evaluation (k_lm_pass<BodyOG>,
+        # LM_OUTG_TAIL = 1) built the output Gram; out step at the best point
+        # when the last trial was accepted, else at the rejected last trial,
+        # published when trial + step beats the best point; otherwise the bias step
+        self.lm_out_dl = 0.0
+        ran_all = len(hist) - 1 == int(fcfg.epochs)  # (an adaptive stop skips the output-Gram pass)
+        if n_out and ran_all:
+            if self._lm_best_k == int(fcfg.epochs):
+                r = out_step(w_best, g)
+                if r is not None:
+                    w_best = w_best.clone()
+                    w_best[P - n_out:] += r[0]
+                    self.lm_out_dl, out_ok = r[1], True
+            else:
+                lw, lg, lL = self._lm_last_eval
+                r = out_step(lw, lg) if lL == lL else None
+                if r is not None and lL + r[1] < Lb:
+                    w_best = lw.clone()
+                    w_best[P - n_out:] += r[0]
+                    Lb, self.lm_out_dl, out_ok = lL, r[1], True
         if not out_ok and bi >= 0 and float(G[bi, bi]) > 0.0:
             w_best = w_best.clone()
             w_best[bi] -= g[bi] / (2.0 * G[bi, bi])

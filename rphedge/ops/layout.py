@@ -64,7 +64,7 @@ LM_NPMAX = 192
 LM_TILE = 64
 LM_GBLK_MAX = 21 * 1024
 LM_OUTG = 64 * 65 // 2               # full-batch output-layer Gram, packed upper triangle (NU <= 64)
-LM_OUTG_TAIL = 3                     # the last evaluations of an lm_out_fix fit carry it
+LM_OUTG_TAIL = 1                     # the last evaluation of an lm_out_fix fit carries it
 LM_RED_OUTG = LM_GBLK_MAX + LM_NPMAX + 8
 LM_RED = LM_RED_OUTG + LM_OUTG
 LM_OG_MAX = 64

@@ -19,6 +19,9 @@ Variants (combinable with '+'):
           ogtail=<k>: only when the best point is one of the last k
           evaluations (else the bias step); ogsub=<k>: output Gram over
           every k-th path only (the gradient stays full-batch)
+  oglast  with outfix: the output Gram of the last evaluation only; a
+          rejected last trial + its out step is published when it beats
+          the best point (else the bias step at the best point)
 """
 from __future__ import annotations
 
@@ -138,6 +141,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
     if vpk > 0:
         w_best, g, Lb = project(w_best, G, g, Lb)
     hist = [Lb]
+    last = (w_best, G, g, Lb)  # the last evaluated point
     kbest = 0  # the evaluation the best point came from
     nacc = 0
     stale = "stale" in flags or ("stale_rest" in VARIANT["flags"] and not first)
@@ -159,6 +163,7 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
             # leaving the projected phase: re-evaluate the best point exactly
             pass
         hist.append(Lt)
+        last = (trial, Gt, gt, Lt)
         Lb_prev = Lb
         if Lt == Lt and Lt < Lb:
             nacc += 1
@@ -177,7 +182,22 @@ def lab_lm_fit(self, wts, fit, data, fcfg):
     if os.environ.get("LAB_DEBUG"): print("HIST", json.dumps([float("%.4g" % h) for h in hist]), file=sys.stderr)
     bi = E._lm_bias_index(spec, t)
     ntail = int(kvf.get("ogtail", 10**9))  # the output Gram exists for the last ntail evaluations only
-    if "outfix" in flags and kbest > len(hist) - 1 - ntail:
+    if "oglast" in flags and kbest != len(hist) - 1:
+        # the output Gram of the LAST evaluation only: the out step at the
+        # rejected last trial (its own exact Gram and gradient) is published
+        # when it beats the best point
+        lw, lG, lg, lL = last
+        with torch.no_grad():
+            Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(lw.detach(), X, pr)[:, oi]
+            Gf = lG.clone()
+            Gf[oi[:, None], oi[None, :]] = (Jo.T @ Jo) / n_glob
+        w2, g2, L2 = project(lw, Gf, lg, lL, mu=float(kvf.get("omu", 0.0)))
+        if L2 < Lb:
+            w_best, g, Lb = w2, g2, L2
+        elif bi >= 0 and float(G[bi, bi]) > 0.0:
+            w_best = w_best.clone()
+            w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
+    elif "outfix" in flags and kbest > len(hist) - 1 - ntail:
         # lm_out_fix: exact output-layer Newton step with the full-batch output Gram
         with torch.no_grad():
             Jo = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w_best.detach(), X, pr)[:, oi]
