@@ -650,7 +650,11 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     bool out_ok = have_og && lm_out_newton<P>(src + LM_RED_OUTG, g, on, lm.ridge, lm.out_mu, lds,
                                               lds + 64 * 65, &s_dl);
     bool use_trial = false;
-    if (!have_og && !stopped && !accept && on_ok && red_new[LM_RED_OUTG] >= 0.0) {
+    // (only for a trial within 2x the best loss: the step must then remove
+    // little more than Lt - Lb, and its predicted change, exact up to the
+    // Gram's ~1e-5 rounding, is a reliable decision - a far-off trial's
+    // Lt + dl would cancel catastrophically)
+    if (!have_og && !stopped && !accept && on_ok && red_new[LM_RED_OUTG] >= 0.0 && Lt == Lt && Lt < 2.0 * Lb) {
       const bool ok_t = lm_out_newton<P>(red_new + LM_RED_OUTG, red_new + LM_GBLK_MAX, on, lm.ridge, lm.out_mu,
                                          lds, lds + 64 * 65, &s_dl);
       use_trial = ok_t && Lt == Lt && Lt + s_dl < Lb;

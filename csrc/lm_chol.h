@@ -197,123 +197,17 @@ struct LmcOwner {
 // the store, 1 / L_kk to rdg.
 // diagnostic stamps (row of d.stamps, thread 0 = lane 0 of the panel wave;
 // tools/stamp_lm.py): 0/1 panel 0 wait passed / written back, 2/3 panel 1,
-// 4/5 last panel
+// 4/5 last panel, 6 its rows loaded, 7 its columns factored
 #define LMC_STAMP(k)                                                                    \
   do {                                                                                  \
     if (stamps != nullptr && lane == 0) stamps[k] = __builtin_amdgcn_s_memrealtime();  \
   } while (0)
-
-// One panel (runtime K) with NS row slots per lane and NC factored columns:
-// the grouped form of lmc_panels (RPH_LMC_GROUPED) runs panels of the same
-// shape through one code copy.  False when the hand-off timed out.
-template <int P, int NS, int NC>
-RPH_INLINE bool lmc_panel(const int K, double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac,
-                          int* s_fail, unsigned long long* stamps, bool& ok) {
-#pragma clang fp contract(off)
-  using TG = TileGrid<P>;
-  const int lane = threadIdx.x & 63;
-  const int ROWS = TG::PT - 16 * K;  // rows of the panel (tile rows K..NT-1)
-  if (!lmc_wait(&pub[K], 3u)) {
-    *s_fail = 2;
-    return false;
-  }
-  if (K < 2) LMC_STAMP(2 * K);
-  else if (K == TG::NK - 1) LMC_STAMP(4);
-  double a[NS][16];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int row = 16 * K + lane + 64 * s;
-    if (s + 1 < NS || lane + 64 * s < ROWS) {
-      const double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
-      const int sw = ((row & 15) >> 1) << 1;
-#pragma unroll
-      for (int c = 0; c < 16; c += 2) {
-        const double2 v = *reinterpret_cast<const double2*>(tr + (c ^ sw));
-        a[s][c] = v.x;
-        a[s][c + 1] = v.y;
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
-    }
-  }
-  double dg = lane < 16 ? T[TG::tidx(K, K) * 256 + tg_off(lane, lane)] : 1.0;
-  lm_static_for<NC>([&](auto cc) {
-    constexpr int c = decltype(cc)::value;
-    const double piv = lmc_readlane(dg, c);
-    ok = ok && piv > 0.0;
-    const double rl = lmc_rsq(piv);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) a[s][c] *= rl;
-    if (lane == c) rdg[16 * K + c] = rl;
-    if constexpr (c + 1 < NC) {
-      const double l1 = lmc_readlane(a[0][c], c + 1);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) a[s][c + 1] = __builtin_fma(-a[s][c], l1, a[s][c + 1]);
-    }
-    dg = __builtin_fma(-a[0][c], a[0][c], dg);
-    if constexpr (c + 2 < NC) {
-      double* b = bc + 16 * (c & 1);
-      if (lane < 16) b[lane] = a[0][c];
-      lmc_wave_sync();
-#pragma unroll
-      for (int j = c + 2; j < NC; ++j) {
-        const double lj = b[j];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
-      }
-    }
-  });
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int row = 16 * K + lane + 64 * s;
-    if (s + 1 < NS || lane + 64 * s < ROWS) {
-      double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
-      const int sw = ((row & 15) >> 1) << 1;
-#pragma unroll
-      for (int c = 0; c < 16; c += 2) {
-        double2 v;
-        v.x = (s == 0 && c > lane) ? 0.0 : a[s][c];
-        v.y = (s == 0 && c + 1 > lane) ? 0.0 : a[s][c + 1];
-        *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
-      }
-    }
-  }
-  lmc_signal(&fac[K]);
-  if (K < 2) LMC_STAMP(2 * K + 1);
-  else if (K == TG::NK - 1) LMC_STAMP(5);
-  return true;
-}
-
-#ifndef RPH_LMC_GROUPED
-#define RPH_LMC_GROUPED 0
-#endif
 
 template <int P>
 RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail,
                            unsigned long long* stamps) {
 #pragma clang fp contract(off)
   using TG = TileGrid<P>;
-#if RPH_LMC_GROUPED
-  // one code copy per panel shape (row slots, columns), K a runtime loop: the
-  // solve runs with a cold instruction cache (the pass kernel ran between two
-  // solves), and the fully unrolled form fetches every panel's code afresh
-  const int lane = threadIdx.x & 63;
-  bool ok = true;
-  constexpr int NK = TG::NK, NCL = P - 16 * (NK - 1), NSL = (TG::PT - 16 * (NK - 1) + 63) / 64;
-  for (int K = 0; K < NK - 1; ++K) {
-    const int ns = (TG::PT - 16 * K + 63) / 64;
-    bool alive = true;
-    lm_static_for<TG::NSLOT>([&](auto sc) {
-      constexpr int S = decltype(sc)::value + 1;
-      if (ns == S) alive = lmc_panel<P, S, 16>(K, T, rdg, bc, pub, fac, s_fail, stamps, ok);
-    });
-    if (!alive) return;
-  }
-  if (!lmc_panel<P, NSL, NCL>(NK - 1, T, rdg, bc, pub, fac, s_fail, stamps, ok)) return;
-  if (!ok && lane == 0) *s_fail = 1;
-  return;
-#else
   const int lane = threadIdx.x & 63;
   bool ok = true, alive = true;
   // every panel is its own straight-line code (static column count, static
@@ -350,6 +244,7 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
         for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
       }
     }
+    if constexpr (K == TG::NK - 1) LMC_STAMP(6);
     // the lane's own diagonal entry (lanes 0..15: row 16K + lane of the diagonal
     // tile), updated with its OWN L entries - the same fma sequence the column
     // updates apply to it - so the pivot chain never waits for a broadcast
@@ -384,6 +279,7 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
         }
       }
     });
+    if constexpr (K == TG::NK - 1) LMC_STAMP(7);
     // write L back (the diagonal tile's upper triangle as zeros)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -405,7 +301,6 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
     else if constexpr (K == TG::NK - 1) LMC_STAMP(5);
   });
   if (!ok && lane == 0) *s_fail = 1;
-#endif
 }
 #undef LMC_STAMP
 

@@ -1294,7 +1294,7 @@ class TorchBackend:
                     self.lm_out_dl, out_ok = r[1], True
             else:
                 lw, lg, lL = self._lm_last_eval
-                r = out_step(lw, lg) if lL == lL else None
+                r = out_step(lw, lg) if (lL == lL and lL < 2.0 * Lb) else None
                 if r is not None and lL + r[1] < Lb:
                     w_best = lw.clone()
                     w_best[P - n_out:] += r[0]

@@ -255,12 +255,11 @@ def test_output_newton_step_every_lm_shape():
 
 def test_out_step_from_rejected_last_trial():
     """LM_OUTG_TAIL = 1: only the last evaluation builds the output Gram.  When
-    the last trial is rejected, the final solve still takes the out step at
-    that trial (its own exact Gram and gradient) and publishes trial + step
-    if it beats the best point.  Over a few tiny-damping fits (long, often
-    rejected final trials) both branches occur, and every published point's
-    fp64 full-batch loss equals FitState.best_loss and is no worse than the
-    best LM point's."""
+    the last trial is rejected (and within 2x the best loss), the final solve
+    still takes the out step at that trial (its own exact Gram and gradient)
+    and publishes trial + step if it beats the best point.  Over short fits
+    both branches occur, and every published point's fp64 full-batch loss
+    equals FitState.best_loss and is no worse than the best LM point's."""
     from rphedge.engine import FitConfig, HipBackend, TrainConfig, current_weights
     from rphedge.models.hedge_mlp import torch_forward
     from rphedge.ops import layout as L
@@ -268,20 +267,19 @@ def test_out_step_from_rejected_last_trial():
     dev = torch.device("cuda", 0)
     n = 1 << 13
     branches = set()
-    for seed in range(8):
-        spec, feats, pr, y, data, w0 = _setup((1, 8, 2, 0), n, dev, seed=20 + seed)
-        tc = TrainConfig(batch_size=n, lm_gram_paths=2048, lm_out_fix=True, lm_lam0=1e-7)
+    for k in range(24):
+        spec, feats, pr, y, data, w0 = _setup((1, 8, 2, 0), n, dev, seed=20 + k)
+        tc = TrainConfig(batch_size=n, lm_gram_paths=2048, lm_out_fix=True)
         be = HipBackend(spec, n, tc, device=dev)
         w, fit = be.new_weights(w0), be.new_fit()
-        be.fit(w, be.new_opt(), fit, data, FitConfig(epochs=4, optimizer="lm", early_stopping=False), seed=0)
+        be.fit(w, be.new_opt(), fit, data, FitConfig(epochs=3 + k % 4, optimizer="lm", early_stopping=False), seed=0)
         torch.cuda.synchronize()
         got = current_weights(spec, w)
         st = be._lm_buffers()["state"].cpu().numpy()
         best = int(st[L.LMS_BEST])
         wb = st[L.LMS_W + best * L.LM_NPMAX:][:spec.nparams]
         hidden = spec.offsets["W3"]
-        from_trial = not np.allclose(got[:hidden], wb[:hidden].astype(np.float32))
-        branches.add(from_trial)
+        branches.add(not np.allclose(got[:hidden], wb[:hidden].astype(np.float32)))
         X = (torch.stack([f.double() for f in feats], 1) - torch.tensor(data.fmu, dtype=torch.float64)) * \
             torch.tensor(data.fisd, dtype=torch.float64)
         Pm = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
@@ -291,6 +289,8 @@ def test_out_step_from_rejected_last_trial():
             return float((e ** 2).mean())
 
         lg, lb = loss(got), loss(wb)
-        assert lg <= lb * (1 + 1e-6), (seed, lg, lb)
-        assert abs(float(fit[L.F_BEST].item()) - lg) <= 0.05 * max(lb - lg, 0.0) + 1e-5 * lb, (seed, fit[L.F_BEST], lg, lb)
+        assert lg <= lb * (1 + 1e-6), (k, lg, lb)
+        assert abs(float(fit[L.F_BEST].item()) - lg) <= 0.05 * max(lb - lg, 0.0) + 1e-5 * lb, (k, fit[L.F_BEST], lg, lb)
+        if branches == {False, True}:
+            break
     assert branches == {False, True}, branches

@@ -51,6 +51,9 @@ def run(n_log2=20, nin=1, passes=40, og=False):
                                 "panel0": (s1[1] - s1[0]) / 100.0, "wait_panel1": (s1[2] - s1[1]) / 100.0,
                                 "panel1": (s1[3] - s1[2]) / 100.0, "wait_last": (s1[4] - s1[3]) / 100.0,
                                 "last_panel": (s1[5] - s1[4]) / 100.0,
+                                "last_panel_load": (s1[6] - s1[4]) / 100.0 if s1[6] else None,
+                                "last_panel_columns": (s1[7] - s1[6]) / 100.0 if s1[6] and s1[7] else None,
+                                "last_panel_writeback": (s1[5] - s1[7]) / 100.0 if s1[7] else None,
                                 "factor_total": (s1[5] - s1[0]) / 100.0,
                                 "backward": (st[7] - st[6]) / 100.0 if st[6] and st[7] else None,
                                 "total_kernel": (st[5] - st[0]) / 100.0 if st[5] else None}
