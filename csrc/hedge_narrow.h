@@ -367,19 +367,27 @@ struct NarrowPairBody {
         for (int f = 0; f < NIN; ++f) acc = nb_fma(x[f], nb_s(Wi[S::OW1 + f * H + j]), acc);
         a1[j] = nb_lrelu(acc, alpha);
       }
+      // layer 2 with the row index outer: H independent accumulator chains
+      // (a dependent v_pk_fma_f32 pair costs a hazard wait state and the
+      // result latency; one wave per SIMD has nothing to fill them with)
 #pragma unroll
-      for (int j = 0; j < H; ++j) {
-        nb_f2 acc = nb_s(Wi[S::OB2 + j]);
+      for (int j = 0; j < H; ++j) a2[j] = nb_s(Wi[S::OB2 + j]);
 #pragma unroll
-        for (int i = 0; i < H; ++i) acc = nb_fma(a1[i], nb_s(Wi[S::OW2 + i * H + j]), acc);
-        a2[j] = nb_lrelu(acc, alpha);
-      }
+      for (int i = 0; i < H; ++i)
+#pragma unroll
+        for (int j = 0; j < H; ++j) a2[j] = nb_fma(a1[i], nb_s(Wi[S::OW2 + i * H + j]), a2[j]);
+#pragma unroll
+      for (int j = 0; j < H; ++j) a2[j] = nb_lrelu(a2[j], alpha);
+      // output layer: NO x 2 chains (even / odd hidden units)
 #pragma unroll
       for (int k = 0; k < NO; ++k) {
-        nb_f2 acc = nb_s(Wi[S::OB3 + k]);
+        nb_f2 acc0 = nb_s(Wi[S::OB3 + k]), acc1 = nb_s(0.f);
 #pragma unroll
-        for (int j = 0; j < H; ++j) acc = nb_fma(a2[j], nb_s(Wi[S::OW3 + j * NO + k]), acc);
-        o[k] = acc;
+        for (int j = 0; j < H; j += 2) {
+          acc0 = nb_fma(a2[j], nb_s(Wi[S::OW3 + j * NO + k]), acc0);
+          acc1 = nb_fma(a2[j + 1], nb_s(Wi[S::OW3 + (j + 1) * NO + k]), acc1);
+        }
+        o[k] = acc0 + acc1;
       }
       nb_f2 V;
       if (HEAD == HEAD_COMPLEMENT) {  // psi = 1 - phi
@@ -480,13 +488,14 @@ struct NarrowPairBody {
       }
 #pragma unroll
       for (int i = 0; i < H; ++i) {
-        nb_f2 da = nb_s(0.f);
+        nb_f2 da0 = nb_s(0.f), da1 = nb_s(0.f);  // two chains (even / odd j)
 #pragma unroll
         for (int j = 0; j < H; ++j) {
           if constexpr (!MGM) g[S::OW2 + i * H + j] = nb_acc(g[S::OW2 + i * H + j], a1[i], dz2[j]);
-          da = nb_fma(nb_s(Wi[S::OW2 + i * H + j]), dz2[j], da);
+          if (j & 1) da1 = nb_fma(nb_s(Wi[S::OW2 + i * H + j]), dz2[j], da1);
+          else da0 = nb_fma(nb_s(Wi[S::OW2 + i * H + j]), dz2[j], da0);
         }
-        const nb_f2 dz1 = nb_lrelu_bwd(a1[i], da, alpha);
+        const nb_f2 dz1 = nb_lrelu_bwd(a1[i], da0 + da1, alpha);
         g[S::OB1 + i] += dz1.x + dz1.y;
 #pragma unroll
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = nb_acc(g[S::OW1 + f * H + i], x[f], dz1);
