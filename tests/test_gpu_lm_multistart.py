@@ -309,5 +309,5 @@ def test_out_step_from_rejected_last_trial():
             tb.fit(wc, tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
             want = current_weights(spec, wc)
             assert np.allclose(want[:hidden], wb[:hidden].astype(np.float32)) != from_trial, (k, lam0)
-            assert loss(want) == pytest.approx(lg, rel=2e-2)
+            assert loss(want) == pytest.approx(lg, rel=5e-2)
     assert branches == {False, True}, branches
