@@ -462,7 +462,7 @@ def main(argv=None):
                    "lm_damping": a.lm_damping if lm else None,
                    "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
                    "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None,
-                   "lm_lam0_first": (a.lm_lam0_first or None) if lm else None, "init": a.init,
+                   "lm_lam0_first": (a.lm_lam0_first or None) if lm else None, "init": a.init, "seed": a.seed,
                    "lm_stop": [a.lm_stop_tol, a.lm_stop_min] if (lm and a.lm_stop_tol > 0) else None,
                    "lm_lam_carry": (a.lm_lam_carry or None) if lm else None,
                    "lm_renorm": bool(a.lm_renorm) if lm else None,
