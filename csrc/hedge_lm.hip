@@ -413,120 +413,89 @@ RPH_INLINE void lm_static_for(F&& f) {
 #include "lm_chol.h"
 namespace rph {
 
-// Exact Newton step on the OUTPUT block (the value is linear in the output
-// layer's N = out_n parameters [P - N, P), so the loss is exactly quadratic
-// in them): (2 G_oo (1 + mu) + ridge) d = -g_o with the FULL-BATCH output Gram
-// matrix gog (packed upper triangle, built on the matrix cores by the fit's
-// last pass), the full-batch gradient, a Marquardt damping out_mu (relative,
-// on the diagonal) and a ridge of lm.ridge x mean diagonal.  ONE wave, no
-// workgroup barrier: lane i holds row i of the system in registers (NM >= N
-// compile-time slots; rows / columns >= N are the identity), the LDL^T
-// elimination broadcasts column k by v_readlane, the triangular solves run
-// by v_readlane too (L^T's columns come back through LDS), d -> out[0, N).
-// *dl = the exact full-batch loss change g_o.d + d.G_oo d.  False (nothing to
+// Exact Newton step on the OUTPUT block at the best point (the value is
+// linear in the output layer's N = out_n parameters [P - N, P), so the loss
+// is exactly quadratic in them): 2 G_oo d = -g_o with the FULL-BATCH output
+// Gram matrix gog (packed upper triangle, built on the matrix cores by the
+// fit's last passes), the full-batch gradient, a Marquardt damping out_mu
+// (relative, on the diagonal) and a ridge of lm.ridge x mean diagonal.  The
+// N x N system goes to LDS, the whole workgroup eliminates it (LDL^T, one
+// barrier per column), wave 0 runs both triangular solves by v_readlane (lane
+// i owns entry i, N <= 64), d -> out[0, N).  *dl = the exact full-batch loss
+// change g_o.d + d.G_oo d (< 0 for any positive damping).  False (nothing to
 // apply) when a pivot is not positive.  Called by workgroup 0 of the final
-// pass only; every thread of the workgroup calls it (wave 0 computes).
+// pass only.
 RPH_INLINE double lm_og(const double* gog, int N, int i, int j) {
   const int lo = i < j ? i : j, hi = i < j ? j : i;
   return gog[lo * N - lo * (lo - 1) / 2 + (hi - lo)];
 }
 
-template <int NM>
-RPH_INLINE bool lm_out_newton_wave(const double* gog, const double* go, const int N, const float ridge,
-                                   const float mu, double* lt, double* out, double* dl) {
-#pragma clang fp contract(off)
-  const int lane = threadIdx.x & 63;
-  const bool row = lane < N;
-  double r[NM];
-#pragma unroll
-  for (int j = 0; j < NM; ++j) {
-    const int jc = j < N ? j : N - 1, ic = row ? lane : 0;
-    const double v = 2.0 * lm_og(gog, N, ic, jc);  // (every load in bounds; masked below)
-    r[j] = (row && j < N) ? v : (lane == j ? 1.0 : 0.0);
-  }
-  // damping on the diagonal: a (1 + mu) + ridge x mean diagonal
-  double dg = 0.0;
-#pragma unroll
-  for (int j = 0; j < NM; ++j)
-    if (j == lane && row) dg = r[j];
-  double sd = dg;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sd += __shfl_xor(sd, o, 64);
-  const double rid = (double)ridge * sd / (double)N;
-#pragma unroll
-  for (int j = 0; j < NM; ++j)
-    if (j == lane && row) r[j] = (r[j] + r[j] * (double)mu) + rid;
-  // LDL^T, right-looking: step k subtracts A_ik A_jk / A_kk from A_ij (i, j > k);
-  // afterwards r[k] = L_ik = A_ik / D_k (lanes i > k), D_k kept by lane k
-  bool ok = true;
-  double dk_own = 1.0;
-#pragma unroll
-  for (int k = 0; k < NM; ++k) {
-    if (k < N) {
-      const double dk = lmc_readlane(r[k], k);
-      ok = ok && dk > 0.0;
-      const double inv = lm_rcp(dk);
-      if (lane == k) dk_own = dk;
-      const double aik = r[k];
-#pragma unroll
-      for (int j = k + 1; j < NM; ++j) {
-        if (j < N) {
-          const double ajk = lmc_readlane(aik, j);  // A_jk (column k of lane j)
-          if (lane > k) r[j] -= (aik * ajk) * inv;
-        }
-      }
-      if (lane > k) r[k] = aik * inv;
-    }
-  }
-  // L (strictly lower) -> LDS rows for the backward solve's column reads
-#pragma unroll
-  for (int j = 0; j < NM; ++j)
-    if (j < N && row) lt[lane * NM + j] = j < lane ? r[j] : 0.0;
-  lmc_wave_sync();
-  // L z = -g, y = z / D, L^T d = y (lane i holds entry i)
-  const double gi = row ? go[lane] : 0.0;
-  double b = -gi;
-#pragma unroll
-  for (int k = 0; k < NM; ++k) {
-    if (k < N) {
-      const double zk = lmc_readlane(b, k);
-      if (lane > k) b -= r[k] * zk;
-    }
-  }
-  b *= lm_rcp(dk_own);
-#pragma unroll
-  for (int k = NM - 1; k >= 0; --k) {
-    if (k < N) {
-      const double dk = lmc_readlane(b, k);
-      if (lane < k) b -= lt[k * NM + lane] * dk;
-    }
-  }
-  if (!row) b = 0.0;
-  if (row) out[lane] = b;
-  // exact loss change of the quadratic: g.d + d.G d (G undamped, full batch)
-  double gd = 0.0;
-#pragma unroll
-  for (int j = 0; j < NM; ++j)
-    if (j < N) gd += (row ? lm_og(gog, N, lane, j) : 0.0) * lmc_readlane(b, j);
-  double t = b * (gi + gd);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
-  if (lane == 0) *dl = t;
-  return ok;
-}
-
 template <int P>
 RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, const float ridge, const float mu,
                               double* A, double* out, double* dl) {
-  __shared__ int s_ok;
-  if (threadIdx.x < 64) {
-    const double* go = g + (P - N);
-    const bool ok = N <= 32 ? lm_out_newton_wave<32>(gog, go, N, ridge, mu, A, out, dl)
-                            : lm_out_newton_wave<64>(gog, go, N, ridge, mu, A, out, dl);
-    if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
+#pragma clang fp contract(off)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int o0 = P - N, LDA = 65;
+  __shared__ double s_rid;
+  for (int e = tid; e < N * N; e += 256) {
+    const int i = e / N, j = e % N;
+    A[i * LDA + j] = 2.0 * lm_og(gog, N, i, j);
   }
   __syncthreads();
-  return s_ok != 0;
+  if (tid < 64) {
+    double dg = lane < N ? A[lane * LDA + lane] : 0.0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dg += __shfl_xor(dg, o, 64);
+    if (lane == 0) s_rid = (double)ridge * dg / (double)N;
+  }
+  __syncthreads();
+  if (tid < N) {
+    const double a = A[tid * LDA + tid];
+    A[tid * LDA + tid] = (a + a * (double)mu) + s_rid;
+  }
+  __syncthreads();
+  // LDL^T elimination over the whole workgroup (lower triangle): step k
+  // subtracts A_ik A_jk / A_kk from every (i, j), k < j <= i; D_k = A_kk
+  bool ok = true;
+  for (int k = 0; k < N; ++k) {
+    const double akk = A[k * LDA + k];
+    ok = ok && akk > 0.0;
+    const double inv = lm_rcp(akk);
+    const int m = N - k - 1;
+    for (int e = tid; e < m * m; e += 256) {
+      const int i = k + 1 + e / m, j = k + 1 + e % m;
+      if (j <= i) A[i * LDA + j] -= (A[i * LDA + k] * A[j * LDA + k]) * inv;
+    }
+    __syncthreads();
+  }
+  if (tid < 64) {
+    // L z = b (L_ik = A_ik / D_k), z / D, L^T d = z: lane i holds entry i and
+    // 1 / D_i (v_rcp_f64 + one Newton step, as lm_rcp)
+    const double di = lane < N ? A[lane * LDA + lane] : 1.0;
+    const double ri = lm_rcp(di);
+    const double gi = lane < N ? g[o0 + lane] : 0.0;
+    double b = -gi;
+    for (int k = 0; k < N; ++k) {
+      const double zk = lmc_readlane(b, k) * lmc_readlane(ri, k);  // L_ik z_k = A_ik (z_k / D_k)
+      if (lane > k && lane < N) b -= A[lane * LDA + k] * zk;
+    }
+    b *= ri;
+    for (int k = N - 1; k >= 0; --k) {
+      const double dk = lmc_readlane(b, k);
+      if (lane < k) b -= (A[k * LDA + lane] * ri) * dk;
+    }
+    if (lane >= N) b = 0.0;
+    if (lane < N) out[lane] = b;
+    // exact loss change of the quadratic: g.d + d.G d (G undamped, full batch)
+    double gd = 0.0;
+    for (int j = 0; j < N; ++j) gd += (lane < N ? lm_og(gog, N, lane, j) : 0.0) * lmc_readlane(b, j);
+    double t = b * (gi + gd);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) *dl = t;
+  }
+  __syncthreads();
+  return ok;
 }
 
 // Solve kernel, LM_SPEC workgroups.  Every workgroup takes the same
