@@ -308,6 +308,8 @@ def test_out_step_from_rejected_last_trial():
             wc = tb.new_weights(w1)
             tb.fit(wc, tb.new_opt(), tb.new_fit(), cd, fc, seed=0)
             want = current_weights(spec, wc)
-            assert np.allclose(want[:hidden], wb[:hidden].astype(np.float32)) != from_trial, (k, lam0)
+            wt = st[L.LMS_W + (1 - best) * L.LM_NPMAX:][:spec.nparams]  # the GPU's last trial
+            near_trial = np.abs(want[:hidden] - wt[:hidden]).max() < np.abs(want[:hidden] - wb[:hidden]).max()
+            assert near_trial == from_trial, (k, lam0)
             assert loss(want) == pytest.approx(lg, rel=5e-2)
     assert branches == {False, True}, branches
