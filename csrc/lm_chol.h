@@ -66,9 +66,18 @@ struct TileGrid {
 RPH_INLINE int tg_off(int r, int c) { return r * 16 + (c ^ ((r >> 1) << 1)); }
 
 // fp64 reciprocal square root: v_rsq_f64 (rel. err 5.2e-8) + one Newton step
+// (RPH_LMC_FAST_RSQ A/B: the hardware estimate alone - three dependent fp64
+// operations fewer on the panel's per-column pivot chain)
+#ifndef RPH_LMC_FAST_RSQ
+#define RPH_LMC_FAST_RSQ 0
+#endif
 RPH_INLINE double lmc_rsq(double x) {
   const double y = __builtin_amdgcn_rsq(x);
+#if RPH_LMC_FAST_RSQ
+  return y;
+#else
   return y * __builtin_fma(-0.5 * x * y, y, 1.5);
+#endif
 }
 
 RPH_INLINE double lmc_readlane(double v, int l) {
