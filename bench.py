@@ -154,6 +154,8 @@ def parse(argv=None):
                     help="later dates: warm start re-expressed for the date's input standardisation")
     ap.add_argument("--lm-explore-passes", type=int, default=None, help="trial points of every exploration fit")
     ap.add_argument("--lm-explore-log2", type=int, default=None, help="exploration fits on 2^this local paths")
+    ap.add_argument("--lm-explore-one", type=int, default=None, choices=[0, 1],
+                    help="lm_starts 1: the one start still explores on the path prefix first (warm-up)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
@@ -178,7 +180,7 @@ def parse(argv=None):
                     ("lm_damping", "simple"), ("lm_lam0", 1e-3), ("lm_lam_up", 4.0), ("lm_lam_down", 1.0 / 3.0),
                     ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam0_first", 0.0),
                     ("lm_lam_carry", 0.0),
-                    ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16), ("lm_renorm", 0), ("lm_out_fix", 0),
+                    ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16), ("lm_explore_one", 0), ("lm_renorm", 0), ("lm_out_fix", 0),
                     ("lm_out_mu", 1e-5)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
@@ -202,7 +204,8 @@ def build_run(a, world: int):
                         lm_stop_min=a.lm_stop_min, lm_lam0_rest=a.lm_lam0_rest, lm_lam0_first=a.lm_lam0_first,
                         init=a.init,
                         lm_lam_carry=a.lm_lam_carry, lm_starts=a.lm_starts, lm_explore_passes=a.lm_explore_passes,
-                        lm_explore_log2=a.lm_explore_log2, lm_renorm=bool(a.lm_renorm), lm_out_fix=bool(a.lm_out_fix),
+                        lm_explore_log2=a.lm_explore_log2, lm_explore_one=bool(a.lm_explore_one),
+                        lm_renorm=bool(a.lm_renorm), lm_out_fix=bool(a.lm_out_fix),
                         lm_out_mu=a.lm_out_mu)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
@@ -411,7 +414,7 @@ def main(argv=None):
     res = run.collect()
     ms = 1000.0 * dt / max(a.steps, 1)
     lm_stats = lm_fit_stats(res.induction) if a.optimizer == "lm" else None
-    if lm_stats is not None and a.lm_starts > 1:
+    if lm_stats is not None and (a.lm_starts > 1 or a.lm_explore_one):
         lm_stats["multistart"] = multistart_record(run, a, world)
     memory = None
     if gpu:
@@ -477,7 +480,7 @@ def main(argv=None):
                    "lm_out_fix": bool(a.lm_out_fix) if lm else None,
                    "lm_multistart": ({"starts_per_rank": a.lm_starts, "explore_passes": a.lm_explore_passes,
                                       "explore_paths_per_rank": 1 << a.lm_explore_log2}
-                                     if (lm and a.lm_starts > 1) else None),
+                                     if (lm and (a.lm_starts > 1 or a.lm_explore_one)) else None),
                    "steps_per_epoch": None if lm else run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,
                    "step_schedule": None if lm else (run.backend.step_mode() if hasattr(run.backend, "step_mode")

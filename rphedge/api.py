@@ -287,6 +287,7 @@ class HedgeRun:
                                lm_lam_carry=float(tr.lm_lam_carry), lm_starts=int(tr.lm_starts),
                                lm_renorm=bool(tr.lm_renorm),
                                lm_explore_passes=int(tr.lm_explore_passes), lm_explore_log2=int(tr.lm_explore_log2),
+                               lm_explore_one=bool(getattr(tr, "lm_explore_one", False)),
                                init_spread=str(getattr(tr, "init", "reference")) == "spread",
                                init_shared_stream=bool(pf.shared_initializer),
                                mean_refit=bool(tr.mean_refit) and not pf.keras_fit_only)

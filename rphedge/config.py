@@ -113,6 +113,8 @@ class TrainingParams:
     lm_explore_passes: int = 45      # ... trial points of every exploration fit
     lm_explore_log2: int = 16        # ... on the first 2^this local paths; the best start over all ranks is
                                      # then polished for lm_passes_first passes on every path
+    lm_explore_one: bool = False     # lm_starts = 1: the one start still explores first (a warm-up of
+                                     # lm_explore_passes on the 2^lm_explore_log2 path prefix)
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
     lm_damping: str = "simple"       # LM damping update: simple (x1/3 / x4) | nielsen (gain ratio)
     lm_lam0: float = 1e-3            # LM initial damping of every fit

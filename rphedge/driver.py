@@ -72,6 +72,9 @@ class InductionConfig:
     lm_starts: int = 1
     lm_explore_passes: int = 45
     lm_explore_log2: int = 16
+    # lm_starts = 1: still run the exploration machinery with the one start
+    # (a first-date warm-up of lm_explore_passes on the path prefix)
+    lm_explore_one: bool = False
     # the extra start points use the run's initialiser (TrainingParams.init,
     # ParityFlags.shared_initializer), so candidate 0 is not the odd one out
     init_spread: bool = False
@@ -168,7 +171,7 @@ class BackwardInduction:
         # initial weights, the others the reference initialiser at seeds
         # seed + 1000 c (same data-dependent output bias); every rank holds all
         self.lm_w0s = None
-        if icfg.optimizer == "lm" and icfg.lm_starts > 1:
+        if icfg.optimizer == "lm" and (icfg.lm_starts > 1 or icfg.lm_explore_one):
             from .models import hedge_mlp as hm
             o = spec.offsets
             b3 = np.asarray(w0, np.float32)[o["b3"]:o["P"]]
@@ -214,7 +217,7 @@ class BackwardInduction:
     def _fcfg(self, first: bool, loss: int, t: int | None = None) -> FitConfig:
         c = self.cfg
         if c.optimizer == "lm" and loss == L.LOSS_MSE:
-            ms = first and c.lm_starts > 1
+            ms = first and (c.lm_starts > 1 or c.lm_explore_one)
             # the warm start was fitted at date t + 1 (its standardisation)
             ren = (self.norms[t + 1] if (c.lm_renorm and not first and c.warm_start and t is not None and self.norms
                                          and t + 1 < len(self.norms)) else None)

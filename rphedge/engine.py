@@ -730,7 +730,7 @@ class HipBackend:
             for i in range(len(mu)):
                 lm.ren_mu[i], lm.ren_isd[i] = float(mu[i]), float(isd[i])
             lm.renorm = 1
-        if int(fcfg.lm_starts) > 1 and int(fcfg.lm_explore_passes) > 0:
+        if int(fcfg.lm_starts) >= 1 and int(fcfg.lm_explore_passes) > 0:
             self._lm_explore(d, fcfg)
             lm.lam_carry = 1.0  # the polish starts at the chosen exploration's damping
         if self.world <= 1 and not self.tcfg.lm_split:
@@ -1226,7 +1226,7 @@ class TorchBackend:
         if float(fcfg.lm_lam_carry) > 0.0:
             lam = max(self._lm_lam_last * float(np.float32(fcfg.lm_lam_carry)), float(np.float32(t.lm_lam_min)))
         K = int(fcfg.lm_starts)
-        if K > 1 and int(fcfg.lm_explore_passes) > 0:
+        if K >= 1 and int(fcfg.lm_explore_passes) > 0:
             # multi-start exploration (k_lm_select): rank-local fits on a path prefix
             want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else self.n_local
             nsub = int(max(256, min(self.n_local, want) // 256 * 256))
