@@ -71,8 +71,13 @@ PRESETS = {
                    batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="lm",
                    # first date: start at the damping of the first trial the round-3 sequence
                    # (lam0 1e-3, x4 per rejection) could accept, fp32(1e-3) x 4^7: its 7
-                   # rejected trials are skipped, the rest of the trajectory is unchanged
-                   lm_lam0_first=LAM0_FIRST, lm_passes_first=73,
+                   # rejected trials are skipped, the rest of the trajectory is unchanged.
+                   # Its first 33 passes run on the 2^16-path prefix (the exploration
+                   # machinery with one start: latency-bound passes, ~14 us cheaper each),
+                   # then 35 on every path (8 seeds: 8.58 vs 8.85 ms at P&L 0.906 vs 0.908,
+                   # profiles/r4/seeds_explore_one.jsonl)
+                   lm_lam0_first=LAM0_FIRST, lm_explore_one=1, lm_explore_passes=33, lm_explore_log2=16,
+                   lm_passes_first=35,
                    lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
     # the flagship with a multi-start first date (4 starts x 45 passes on 2^16
