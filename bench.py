@@ -94,7 +94,10 @@ PRESETS = {
     "heston30": dict(model="heston", dates=30, substeps=10, paths_log2=20, epochs_first=1024, epochs_rest=16,
                      batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1,
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
-                     optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                     optimizer="lm", lm_passes_first=35, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                     # first date: 45 passes on the 2^16-path prefix, then 35 on every path
+                     # (3 seeds: 12.5 vs 12.8 ms, P&L 2.419 vs 2.423 mean; profiles/r4/presets_explore_one.jsonl)
+                     lm_explore_one=1, lm_explore_passes=45, lm_explore_log2=16,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
@@ -103,7 +106,10 @@ PRESETS = {
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
                     extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
-                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                    optimizer="lm", lm_passes_first=40, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                    # first date: 40 passes on the 2^16-path prefix, then 40 on every path
+                    # (2 seeds: 333 vs 340 ms, P&L 0.359 vs 0.374 mean; profiles/r4/presets_explore_one.jsonl)
+                    lm_explore_one=1, lm_explore_passes=40, lm_explore_log2=16,
                     label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
     "euro30_mfma": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-3, lr_rest=1e-3, lr_decay=0.1, hidden=32,
