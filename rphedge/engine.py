@@ -461,9 +461,11 @@ class HipBackend:
         self.lag = torch.zeros(2, L.LAG_FLOATS, dtype=torch.float32, device=dev)
         self._acc_clean = False  # acc_fit known zero (set by a lagged fit's finalize)
         self.stamps = None  # set to an int64 [num_wgs, 8] tensor for phase diagnostics
-        # eval epilogue (k_hedge_eval): weights read from LDS, 2-4 resident waves
-        # per SIMD, each thread walks its paths with a 4-deep load ring
-        ewg = int(os.environ.get("RPH_EVAL_WGS", "512"))
+        # eval epilogue (k_hedge_eval): weights read from LDS, up to 4 resident
+        # waves per SIMD, each thread walks its paths with a 4-deep load ring;
+        # 2048 workgroups (2 paths per thread at 2^20): euro30 8.42 -> 8.28 ms
+        # against 512 (profiles/r4/eval_wgs_sweep.txt)
+        ewg = int(os.environ.get("RPH_EVAL_WGS", "2048"))
         self.eval_wgs = int(max(1, min(ewg, (self.n_local + 255) // 256)))
         self._cache = _Cache()
         self._lm_same_gram = True  # the last LM fit built the world-invariant Gram (exchange: gradient region only)
