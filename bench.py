@@ -96,8 +96,11 @@ PRESETS = {
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
                      optimizer="lm", lm_passes_first=35, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                      # first date: 45 passes on the 2^16-path prefix, then 35 on every path
-                     # (3 seeds: 12.5 vs 12.8 ms, P&L 2.419 vs 2.423 mean; profiles/r4/presets_explore_one.jsonl)
-                     lm_explore_one=1, lm_explore_passes=45, lm_explore_log2=16,
+                     # (3 seeds: 12.5 vs 12.8 ms, P&L 2.419 vs 2.423 mean; profiles/r4/presets_explore_one.jsonl),
+                     # the prefix's 7 initial rejections at lam0 1e-3 skipped (the same P&L bit
+                     # for bit on 3 seeds, 12.41 ms; profiles/r4/lam0_warmup_presets.jsonl; basket5's
+                     # prefix has another rejection count: skipping 7 there diverges one seed)
+                     lm_lam0_first=LAM0_FIRST, lm_explore_one=1, lm_explore_passes=38, lm_explore_log2=16,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
