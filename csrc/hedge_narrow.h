@@ -313,6 +313,77 @@ struct NarrowPairBody {
     return __builtin_bit_cast(nb_bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 
+  // one 128-path iteration of the output-layer Gram: u of both paths
+  // (masked) -> the [path][unit] image (bf16 hi / lo halves, 64 rows per
+  // half-iteration) -> hi hi^T + hi lo^T + lo hi^T on the matrix cores
+  RPH_INLINE static void og_accum(unsigned char* img, nb_f32x16 (&oacc)[NBO], const nb_f2 (&a2)[H],
+                                  const nb_f2 (&pr)[NHOLD], const nb_f2 m, const int lane) {
+    nb_f2 c[NO];
+    if (HEAD == HEAD_COMPLEMENT) {
+      c[0] = (pr[0] - pr[1]) * m;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NO; ++k) c[k] = pr[k] * m;
+    }
+    float ua[(NU + 3) / 4 * 4], ub[(NU + 3) / 4 * 4];
+#pragma unroll
+    for (int j = 0; j < H; ++j)
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        const nb_f2 v = a2[j] * c[k];
+        ua[j * NO + k] = v.x;
+        ub[j * NO + k] = v.y;
+      }
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      ua[H * NO + k] = c[k].x;
+      ub[H * NO + k] = c[k].y;
+    }
+#pragma unroll
+    for (int e = NU; e < (NU + 3) / 4 * 4; ++e) ua[e] = ub[e] = 0.f;
+    constexpr int LO = NUP / 32;  // unit block of the lo half
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      og_wave_sync();  // the previous half's fragment reads are done
+#pragma unroll
+      for (int c0 = 0; c0 < NU; c0 += 4) {
+        if (h2) og_put(img, lane, c0, ub[c0], ub[c0 + 1], ub[c0 + 2], ub[c0 + 3]);
+        else og_put(img, lane, c0, ua[c0], ua[c0 + 1], ua[c0 + 2], ua[c0 + 3]);
+      }
+      og_wave_sync();
+#pragma unroll
+      for (int s2 = 0; s2 < OG_ROWS / 16; ++s2) {
+        const nb_bf16x8 h0 = og_frag(img, s2, 0, lane), l0 = og_frag(img, s2, LO, lane);
+        oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h0, oacc[0], 0, 0, 0);
+        oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l0, oacc[0], 0, 0, 0);
+        oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h0, oacc[0], 0, 0, 0);
+        if constexpr (NBO == 3) {
+          const nb_bf16x8 h1 = og_frag(img, s2, 1, lane), l1 = og_frag(img, s2, LO + 1, lane);
+          oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h1, oacc[1], 0, 0, 0);
+          oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l1, oacc[1], 0, 0, 0);
+          oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h1, oacc[1], 0, 0, 0);
+          oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, h1, oacc[2], 0, 0, 0);
+          oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, l1, oacc[2], 0, 0, 0);
+          oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l1, h1, oacc[2], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // the four waves' output-Gram tiles -> this workgroup's og_out (fixed order);
+  // og_lds is reused (every wave's last fragment reads are done)
+  RPH_INLINE static void og_finish(unsigned char* og_lds, const nb_f32x16 (&oacc)[NBO], float* __restrict__ og_out) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
+    float* ot = reinterpret_cast<float*>(og_lds);
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NBO; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) ot[(wid * NBO + b) * 1024 + q * 64 + lane] = oacc[b][q];
+    __syncthreads();
+    for (int e = t; e < NBO * 1024; e += 256)
+      og_out[e] = (ot[e] + ot[NBO * 1024 + e]) + (ot[2 * NBO * 1024 + e] + ot[3 * NBO * 1024 + e]);
+  }
+
   // og_lds: OG_LDS bytes of LDS (the OG instantiation), og_out: this
   // workgroup's NBO x 1024 output-Gram floats (MFMA register layout)
   RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
@@ -408,59 +479,7 @@ struct NarrowPairBody {
       g[P + 2] += ape.x + ape.y;
       g[P + 3] += m.x + m.y;
       if constexpr (OGM) {
-        if (og) {
-          // u of both paths (masked) -> image rows lane, 64 + lane
-          nb_f2 c[NO];
-          if (HEAD == HEAD_COMPLEMENT) {
-            c[0] = (pr[0] - pr[1]) * m;
-          } else {
-#pragma unroll
-            for (int k = 0; k < NO; ++k) c[k] = pr[k] * m;
-          }
-          float ua[(NU + 3) / 4 * 4], ub[(NU + 3) / 4 * 4];
-#pragma unroll
-          for (int j = 0; j < H; ++j)
-#pragma unroll
-            for (int k = 0; k < NO; ++k) {
-              const nb_f2 v = a2[j] * c[k];
-              ua[j * NO + k] = v.x;
-              ub[j * NO + k] = v.y;
-            }
-#pragma unroll
-          for (int k = 0; k < NO; ++k) {
-            ua[H * NO + k] = c[k].x;
-            ub[H * NO + k] = c[k].y;
-          }
-#pragma unroll
-          for (int e = NU; e < (NU + 3) / 4 * 4; ++e) ua[e] = ub[e] = 0.f;
-          constexpr int LO = NUP / 32;  // unit block of the lo half
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            og_wave_sync();  // the previous half's fragment reads are done
-#pragma unroll
-            for (int c0 = 0; c0 < NU; c0 += 4) {
-              if (h2) og_put(img, lane, c0, ub[c0], ub[c0 + 1], ub[c0 + 2], ub[c0 + 3]);
-              else og_put(img, lane, c0, ua[c0], ua[c0 + 1], ua[c0 + 2], ua[c0 + 3]);
-            }
-            og_wave_sync();
-#pragma unroll
-            for (int s2 = 0; s2 < OG_ROWS / 16; ++s2) {
-              const nb_bf16x8 h0 = og_frag(img, s2, 0, lane), l0 = og_frag(img, s2, LO, lane);
-              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h0, oacc[0], 0, 0, 0);
-              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l0, oacc[0], 0, 0, 0);
-              oacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h0, oacc[0], 0, 0, 0);
-              if constexpr (NBO == 3) {
-                const nb_bf16x8 h1 = og_frag(img, s2, 1, lane), l1 = og_frag(img, s2, LO + 1, lane);
-                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, h1, oacc[1], 0, 0, 0);
-                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, l1, oacc[1], 0, 0, 0);
-                oacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l0, h1, oacc[1], 0, 0, 0);
-                oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, h1, oacc[2], 0, 0, 0);
-                oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, l1, oacc[2], 0, 0, 0);
-                oacc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(l1, h1, oacc[2], 0, 0, 0);
-              }
-            }
-          }
-        }
+        if (og) og_accum(img, oacc, a2, pr, m, lane);
       }
       const nb_f2 dV = e * m * two_inv;
 
