@@ -262,97 +262,6 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 }
 
 // ---------------------------------------------------------------------------
-// Output-Gram kernel (the last pass of an lm_out_fix fit, RPH_LM_OG_SIDE):
-// the full-batch output-layer Gram of the trial point on its own, launched on
-// a side stream beside the plain pass kernel.  It needs only the forward to
-// a2 (no loss, no backward), 150 VGPRs and 35 KB of LDS, so its workgroups
-// co-reside with the pass kernel's (one 296-register wave per SIMD leaves room
-// for one more) and its LDS / matrix-core work fills the pass's stall cycles.
-// Writes the same per-workgroup slab_o tiles k_lm_reduce sums.
-// ---------------------------------------------------------------------------
-template <class B>
-__global__ __launch_bounds__(256) void k_lm_og(const TrainDesc d, const LmDesc lm, const int pass) {
-  constexpr int P = B::P;
-  constexpr int NIN = B::NIN_, H = B::H_, NBO = B::NBO;
-  using S = typename B::S;
-  __shared__ __attribute__((aligned(16))) float wl[P + 4];
-  __shared__ __attribute__((aligned(16))) unsigned char og_img[B::OG_LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int inst = blockIdx.y;
-  const double* st = lm.state + (size_t)inst * LMS_FLOATS;
-  const double* sl = st + LMS_SLOTS + LM_SLOT * (pass & 1);
-  if (pass > 0 && sl[LSS_STOP] != 0.0) return;  // adaptive budget spent (the reduce returns too)
-  // the trial point, exactly as k_lm_pass loads it
-  const int trial = pass == 0 ? 0 : 1 - (int)sl[LSS_BEST];
-  for (int i = tid; i < P; i += 256) {
-    float w;
-    if (pass == 0) {
-      const float* w0p = lm.w0 != nullptr ? lm.w0 + inst * LM_NPMAX : d.wts->w[0];
-      w = w0p[i];
-      if (lm.renorm) {
-        if (i >= S::OW1 && i < S::OW1 + NIN * H) {
-          const int f = (i - S::OW1) / H;
-          w = (float)((double)w * ((double)lm.ren_isd[f] / (double)d.fisd[f]));
-        } else if (i >= S::OB1 && i < S::OB1 + H) {
-          double acc = (double)w;
-#pragma unroll
-          for (int f = 0; f < NIN; ++f)
-            acc += (double)w0p[S::OW1 + f * H + (i - S::OB1)] * (double)lm.ren_isd[f] *
-                   ((double)d.fmu[f] - (double)lm.ren_mu[f]);
-          w = (float)acc;
-        }
-      }
-    } else {
-      w = (float)st[LMS_W + trial * LM_NPMAX + i];
-    }
-    wl[i] = w;
-  }
-  __syncthreads();
-  nb_f32x16 oacc[NBO];
-#pragma unroll
-  for (int b = 0; b < NBO; ++b) oacc[b] = nb_f32x16{};
-  unsigned char* const img = og_img + wid * B::OG_ROWS * B::OG_PITCH;
-  {
-    constexpr int NU4 = (B::NU + 3) / 4 * 4;
-#pragma unroll
-    for (int c0 = NU4; c0 < B::NUP; c0 += 4) B::og_put(img, lane, c0, 0.f, 0.f, 0.f, 0.f);
-  }
-  const Perm perm = make_perm(1u, 0u, 0u, false);
-  const long long nblk = (d.batch + 127) / 128;
-  const long long TW = (long long)gridDim.x * 4;
-  typename B::Pre cur;
-  long long b = (long long)blockIdx.x * 4 + wid;
-  if (b < nblk) B::load(d, 0, perm, b * 128, lane, cur);
-  for (; b < nblk; b += TW) {
-    nb_f2 x[NIN], pr[B::NHOLD];
-#pragma unroll
-    for (int f = 0; f < NIN; ++f) x[f] = (cur.x[f] - d.fmu[f]) * d.fisd[f];
-#pragma unroll
-    for (int k = 0; k < B::NHOLD; ++k) pr[k] = cur.pr[k];
-    const nb_f2 m = cur.m;
-    if (b + TW < nblk) B::load(d, 0, perm, (b + TW) * 128, lane, cur);
-    nb_f2 a1[H], a2[H];
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-      nb_f2 acc = nb_s(wl[S::OB1 + j]);
-#pragma unroll
-      for (int f = 0; f < NIN; ++f) acc = nb_fma(x[f], nb_s(wl[S::OW1 + f * H + j]), acc);
-      a1[j] = nb_lrelu(acc, d.alpha);
-    }
-#pragma unroll
-    for (int j = 0; j < H; ++j) a2[j] = nb_s(wl[S::OB2 + j]);
-#pragma unroll
-    for (int i = 0; i < H; ++i)
-#pragma unroll
-      for (int j = 0; j < H; ++j) a2[j] = nb_fma(a1[i], nb_s(wl[S::OW2 + i * H + j]), a2[j]);
-#pragma unroll
-    for (int j = 0; j < H; ++j) a2[j] = nb_lrelu(a2[j], d.alpha);
-    B::og_accum(img, oacc, a2, pr, m, lane);
-  }
-  B::og_finish(og_img, oacc, lm.slab_o + ((size_t)inst * lm.num_wgs + blockIdx.x) * 3 * 1024);
-}
-
-// ---------------------------------------------------------------------------
 // Reduce kernel: red[e] = fixed-order sums of the slabs.
 // ---------------------------------------------------------------------------
 // workgroups of the output-Gram part of k_lm_reduce (64 packed entries each)
@@ -958,30 +867,6 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   return 0;
 }
 
-// side stream + fork / join events of the output-Gram kernel (created once;
-// RPH_LM_OG_SIDE=0 keeps the output Gram inside the pass kernel)
-struct LmSide {
-  hipStream_t stream = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-static LmSide& lm_side() {
-  static LmSide sd = [] {
-    LmSide x;
-    (void)hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking);
-    (void)hipEventCreateWithFlags(&x.fork, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&x.join, hipEventDisableTiming);
-    return x;
-  }();
-  return sd;
-}
-static bool lm_og_side() {
-  static const bool on = [] {
-    const char* e = getenv("RPH_LM_OG_SIDE");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
 template <int A, int B, int C, int E>
 static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const double* red_new, hipStream_t s) {
   using K = LmKernels<A, B, C, E>;
@@ -1002,20 +887,6 @@ static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const 
   if constexpr (K::BodyOG::OGM) {
     // the last LM_OUTG_TAIL evaluations of an lm_out_fix fit build the output Gram
     if (og) {
-      if (lm_og_side()) {
-        // on a side stream beside the plain pass (fork / join by events: also
-        // inside a hipGraph capture), k_lm_reduce reads its tiles after the join
-        LmSide& sd = lm_side();
-        if (hipEventRecord(sd.fork, s) != hipSuccess || hipStreamWaitEvent(sd.stream, sd.fork, 0) != hipSuccess)
-          return (int)hipGetLastError();
-        hipLaunchKernelGGL((k_lm_og<typename K::BodyOG>), dim3(lm->num_wgs, lm->inst), dim3(256), 0, sd.stream, *d,
-                           *lm, pass);
-        hipLaunchKernelGGL((k_lm_pass<typename K::Body>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
-                           red_new);
-        if (hipEventRecord(sd.join, sd.stream) != hipSuccess || hipStreamWaitEvent(s, sd.join, 0) != hipSuccess)
-          return (int)hipGetLastError();
-        return (int)hipGetLastError();
-      }
       hipLaunchKernelGGL((k_lm_pass<typename K::BodyOG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
                          red_new);
       return (int)hipGetLastError();
@@ -1284,7 +1155,6 @@ extern "C" int rph_lm_shape(int nin, int h, int nout, int head, int* p, int* r, 
     *r = K::S::R;                                                        \
     *nblk = LmShape<K::S::P>::NBLK;                                      \
     *two_per_cu = K::TWO ? 1 : 0;                                        \
-    if (lm_og_side()) (void)lm_side(); /* side stream: outside any capture */ \
     return 0;                                                            \
   }
   RPH_LM_SHAPES(X)
