@@ -369,20 +369,6 @@ struct NarrowPairBody {
       }
     }
   }
-  // the four waves' output-Gram tiles -> this workgroup's og_out (fixed order);
-  // og_lds is reused (every wave's last fragment reads are done)
-  RPH_INLINE static void og_finish(unsigned char* og_lds, const nb_f32x16 (&oacc)[NBO], float* __restrict__ og_out) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
-    float* ot = reinterpret_cast<float*>(og_lds);
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NBO; ++b)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) ot[(wid * NBO + b) * 1024 + q * 64 + lane] = oacc[b][q];
-    __syncthreads();
-    for (int e = t; e < NBO * 1024; e += 256)
-      og_out[e] = (ot[e] + ot[NBO * 1024 + e]) + (ot[2 * NBO * 1024 + e] + ot[3 * NBO * 1024 + e]);
-  }
 
   // og_lds: OG_LDS bytes of LDS (the OG instantiation), og_out: this
   // workgroup's NBO x 1024 output-Gram floats (MFMA register layout)
