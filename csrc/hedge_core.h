@@ -18,7 +18,13 @@ namespace rph {
 #define RPH_STAMP(k)                                                                    \
   do {                                                                                  \
     if (d.stamps != nullptr && threadIdx.x == 0)                                        \
-      d.stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
+      d.stamps[(size_t)blockIdx.x * 8 + (k)] = rph_stamp_clock();                       \
+  } while (0)
+// the bodies' "path loop done" stamp (the bodies also run in k_lm_pass, whose
+// workgroups 0 and 1 leave stamp rows 0 and 1 to k_lm_solve)
+#define RPH_STAMP_BODY(k)                                                               \
+  do {                                                                                  \
+    if (blockIdx.x >= 2) RPH_STAMP(k);                                                  \
   } while (0)
 
 template <int NIN, int H, int NO, int HEAD>

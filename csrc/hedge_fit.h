@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void k_hedge_fit(const TrainDesc d, const int 
   // diagnostic stamps of the most recent step: 0 start, 1 partial done, 2 adds
   // drained, 3 all arrived (thread 0), 4 sums read, 5 update done
 #define FIT_STAMP(k) \
-  if (d.stamps != nullptr && tid == 0) d.stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+  if (d.stamps != nullptr && tid == 0) d.stamps[(size_t)blockIdx.x * 8 + (k)] = rph_stamp_clock()
   uint32_t gstep = 0;  // steps started (rotating buffers, barrier targets)
   uint32_t done = 0;   // steps completed (DP sequence)
   bool bad = false;

@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const bool stamp_on = d.stamps != nullptr && m == 0 && blockIdx.y == 0 && tid == 0;
 #define RPH_STAMPS(k)                                        \
   do {                                                       \
-    if (stamp_on) ts[(k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (stamp_on) ts[(k)] = rph_stamp_clock();                \
   } while (0)
   RPH_STAMPS(0);
 #ifdef RPH_LDS_POISON
@@ -545,20 +545,44 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const double* sin = st + LMS_SLOTS + LM_SLOT * (pass & 1);  // read by every workgroup
   double* sout = st + LMS_SLOTS + LM_SLOT * ((pass + 1) & 1);  // written by workgroup 0
   // ---- scalars of this pass ------------------------------------------------------
-  const int best_old = pass == 0 ? 1 : (int)sin[LSS_BEST];
+  // Every load of the prologue is unconditional (clamped indices, both
+  // outcomes of the acceptance test), so all of them are in flight at once: a
+  // load under a condition waits out its own round trip, and the solve's
+  // setup was a chain of them
+  const double sv_best = sin[LSS_BEST], sv_lbest = sin[LSS_LBEST], sv_stop = sin[LSS_STOP];
+  const double sv_lam = sin[LSS_LAM], sv_nu = sin[LSS_NU], sv_pred = sin[LSS_PRED], sv_sidx = sin[LSS_SPEC_IDX];
+  // the trial's packet statistics [loss, |e|, ape, count]
+  const double t_loss = red_new[LM_GBLK_MAX + LM_NPMAX], cnt = red_new[LM_GBLK_MAX + LM_NPMAX + 3];
+  double sp_lam[LM_SPEC], sp_ok[LM_SPEC], sp_pred[LM_SPEC];
+#pragma unroll
+  for (int k = 0; k < LM_SPEC; ++k) {
+    sp_lam[k] = st[LMS_SPEC_LAM + k];
+    sp_ok[k] = st[LMS_SPEC_OK + k];
+    sp_pred[k] = st[LMS_SPEC_PRED + k];
+  }
+  // per-parameter values of a full solve, for either best point
+  constexpr int NDS = (P + 63) / 64;  // diagonal entries per lane (the damping scale)
+  const int tc = tid < P ? tid : P - 1;
+  const double w_slot0 = st[LMS_W + tc], w_slot1 = st[LMS_W + LM_NPMAX + tc];
+  const double g_new = red_new[LM_GBLK_MAX + tc], g_old = best_red[LM_GBLK_MAX + tc];
+  const double d_new = lmc_gram<TileGrid<P>::NBG>(red_new, tc, tc), d_old = lmc_gram<TileGrid<P>::NBG>(best_red, tc, tc);
+  double ds_new[NDS], ds_old[NDS];
+#pragma unroll
+  for (int k = 0; k < NDS; ++k) {
+    const int i = lane + 64 * k < P ? lane + 64 * k : P - 1;
+    ds_new[k] = lmc_gram<TileGrid<P>::NBG>(red_new, i, i);
+    ds_old[k] = lmc_gram<TileGrid<P>::NBG>(best_red, i, i);
+  }
+  const int best_old = pass == 0 ? 1 : (int)sv_best;
   const int trial = 1 - best_old;
-  auto pkt = [&](int i) -> double {  // packet entries of the trial: [g (P) | loss, |e|, ape, count]
-    return i < P ? red_new[LM_GBLK_MAX + i] : red_new[LM_GBLK_MAX + LM_NPMAX + i - P];
-  };
-  const double cnt = pkt(P + 3);
-  const double Lt = pkt(P + 0) / fmax(cnt, 1.0);
-  const double Lb = pass == 0 ? INFINITY : sin[LSS_LBEST];
+  const double Lt = t_loss / fmax(cnt, 1.0);
+  const double Lb = pass == 0 ? INFINITY : sv_lbest;
   // adaptive budget spent at an earlier solve: the trial block is stale
-  const bool stopped = pass > 0 && sin[LSS_STOP] != 0.0;
+  const bool stopped = pass > 0 && sv_stop != 0.0;
   const bool accept = !stopped && (pass == 0 || (Lt == Lt && Lt < Lb));
-  double lam = sin[LSS_LAM], nu = sin[LSS_NU];
-  const double pred_prev = sin[LSS_PRED];
-  const int sidx = (int)sin[LSS_SPEC_IDX];
+  double lam = sv_lam, nu = sv_nu;
+  const double pred_prev = sv_pred;
+  const int sidx = (int)sv_sidx;
   int best = best_old;
   if (stopped) {
   } else if (accept) {
@@ -581,9 +605,17 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   const bool final_pass = pass == lm.passes;
   // a rejection whose step the last full solve precomputed (same damping,
   // same best point: rejections do not move it)
-  const bool spec = !final_pass && !accept && pass > 0 && sidx >= 1 && sidx < LM_SPEC && st[LMS_SPEC_LAM + sidx] == lam;
-  const int spec_ok = spec ? (st[LMS_SPEC_OK + sidx] != 0.0) : 0;
-  const double spec_pred = spec ? st[LMS_SPEC_PRED + sidx] : 0.0;
+  double sl = 0.0, so = 0.0, sq = 0.0;
+#pragma unroll
+  for (int k = 1; k < LM_SPEC; ++k)
+    if (k == sidx) {
+      sl = sp_lam[k];
+      so = sp_ok[k];
+      sq = sp_pred[k];
+    }
+  const bool spec = !final_pass && !accept && pass > 0 && sidx >= 1 && sidx < LM_SPEC && sl == lam;
+  const int spec_ok = spec ? (so != 0.0) : 0;
+  const double spec_pred = spec ? sq : 0.0;
   // the damping of this workgroup's system: m further rejections
   double lam_m = lam, nu_m = nu;
   for (int k = 0; k < m; ++k) {
@@ -720,12 +752,19 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   unsigned* pub = reinterpret_cast<unsigned*>(lds + TG::OFF_FLAGS);
   unsigned* fac = pub + TG::NT + 1;
   static_assert(P <= 256, "one parameter per thread");
-  const double gi = tid < P ? g[tid] : 0.0;
-  const double wbest = tid < P ? st[LMS_W + best * LM_NPMAX + tid] : 0.0;  // for the final update
-  const double a_ii = tid < P ? 2.0 * lmc_gram<TG::NBG>(src, tid, tid) : 0.0;
+  const double gi = tid < P ? (accept ? g_new : g_old) : 0.0;
+  const double wbest = tid < P ? (best == 0 ? w_slot0 : w_slot1) : 0.0;  // for the final update
+  const double a_ii = tid < P ? 2.0 * (accept ? d_new : d_old) : 0.0;
+  // the Gram block into the tile store with coalesced loads, in flight
+  // across the damping setup below (up to 16 tiles per owner wave: the larger
+  // nets' owners load their tiles from the Gram block after the setup)
+  constexpr bool STAGED = TG::TPW <= 16;
+  if constexpr (STAGED) lmc_stage<P>(T, src, gi);
   if (wid == 0) {
     double s = 0.0;
-    for (int i = lane; i < P; i += 64) s += 2.0 * lmc_gram<TG::NBG>(src, i, i);
+#pragma unroll
+    for (int k = 0; k < NDS; ++k)
+      if (lane + 64 * k < P) s += 2.0 * (accept ? ds_new[k] : ds_old[k]);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
     if (lane == 0) {
@@ -755,9 +794,9 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       lmc_backward<P>(T, lds + TG::OFF_RDG, vec);
       RPH_STAMPS(7);
       break;
-    case 1: LmcOwner<P, 0>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
-    case 2: LmcOwner<P, 1>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
-    default: LmcOwner<P, 2>::run(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+    case 1: LmcOwner<P, 0>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+    case 2: LmcOwner<P, 1>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+    default: LmcOwner<P, 2>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
   }
   __syncthreads();
   RPH_STAMPS(3);

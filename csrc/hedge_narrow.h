@@ -153,7 +153,7 @@ struct NarrowBody {
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
       }
     }
-    RPH_STAMP(5);  // path loop done
+    RPH_STAMP_BODY(5);  // path loop done
     // ---- in-wave reduce-scatter, cross-wave LDS sum ------------------------
     wave_reduce_scatter<R>(g, lane);
     constexpr int PER = R / 64;
@@ -538,7 +538,7 @@ struct NarrowPairBody {
         }
       }
     }
-    RPH_STAMP(5);  // path loop done
+    RPH_STAMP_BODY(5);  // path loop done
     wave_reduce_scatter<R>(g, lane);
     constexpr int PER = R / 64;
 #pragma unroll

@@ -119,6 +119,40 @@ RPH_INLINE bool lmc_wait(const unsigned* flag, unsigned target) {
   return false;
 }
 
+// The whole workgroup copies the strictly lower Gram entries (x2) and the rhs
+// row -g into the tile store before the setup barrier: the Gram block is read
+// in its own order (each 64-lane load one contiguous 512-byte run), where the
+// owners' accumulator-order loads touch 16 cache lines per instruction
+template <int P>
+RPH_INLINE void lmc_stage(double* T, const double* src, double g_tid) {
+  using TG = TileGrid<P>;
+  constexpr int NBG = TG::NBG, NBLK = NBG * (NBG + 1) / 2;
+  constexpr int NIT = NBLK * 4;  // 256 threads x 4 = one 32 x 32 block
+  constexpr int CH = NIT;        // every load in flight before the first store (one round trip)
+  const int tid = threadIdx.x;
+  lm_static_for<(NIT + CH - 1) / CH>([&](auto cc) {
+    constexpr int I0 = decltype(cc)::value * CH;
+    double v[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (I0 + u < NIT) v[u] = src[(I0 + u) * 256 + tid];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int it = I0 + u;
+      if (it < NIT) {
+        const int b = it >> 2, e = (it & 3) * 256 + tid;
+        int mb = 0, rem = b;  // block b -> (mb, nb), upper triangle row-major (lmc_gram)
+        while (rem >= NBG - mb) rem -= NBG - mb++;
+        const int nb = mb + rem;
+        const int q = e >> 6, h = (e >> 5) & 1;
+        const int lo = 32 * mb + (q & 3) + 4 * h + 8 * (q >> 2), hi = 32 * nb + (e & 31);
+        if (lo < hi && hi < P) T[TG::tidx(hi >> 4, lo >> 4) * 256 + tg_off(hi & 15, lo & 15)] = 2.0 * v[u];
+      }
+    }
+  });
+  if (tid < P) T[TG::tidx(P >> 4, tid >> 4) * 256 + tg_off(P & 15, tid & 15)] = -g_tid;
+}
+
 // Owner wave O (0..2): its tiles are t = O + 3 j (compile-time), so every
 // register index is static.
 template <int P, int O>
@@ -142,6 +176,28 @@ struct LmcOwner {
           double v;
           if (i < P && c < P) v = i == c ? dg : (c < i ? 2.0 * gv : 0.0);
           else if (i == P && c < P) v = -gr;
+          else v = i == c ? 1.0 : 0.0;
+          C[j][r] = v;
+        }
+      }
+    });
+  }
+
+  // the same tiles from the store, where lmc_stage put the strictly lower
+  // Gram entries (x2) and the rhs row: LDS reads only
+  RPH_INLINE static void load_staged(lmc_d4* C, const double* T, const double* diag, int lr, int lq) {
+    lm_static_for<TPW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, t = O + 3 * j;
+      if constexpr (t < TG::NTILE) {
+        constexpr int ib = TG::trow(t), jb = TG::tcol(t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * ib + lq + 4 * r, c = 16 * jb + lr;
+          const int ic = i < P ? i : P - 1;
+          const double tv = T[t * 256 + tg_off(lq + 4 * r, lr)], dg = diag[ic];
+          double v;
+          if (i < P && c < P) v = i == c ? dg : (c < i ? tv : 0.0);
+          else if (i == P && c < P) v = tv;
           else v = i == c ? 1.0 : 0.0;
           C[j][r] = v;
         }
@@ -182,11 +238,14 @@ struct LmcOwner {
     });
   }
 
+  // STAGED: the tiles from the store (lmc_stage), else from the Gram block
+  template <bool STAGED>
   RPH_INLINE static void run(const double* src, const double* diag, const double* g, double* T, unsigned* pub,
                              const unsigned* fac, int* s_fail) {
     const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
     lmc_d4 C[TPW];
-    load(C, src, diag, g, lr, lq);
+    if constexpr (STAGED) load_staged(C, T, diag, lr, lq);
+    else load(C, src, diag, g, lr, lq);
     publish(C, T, 0, lr, lq);
     lmc_signal(&pub[0]);
     for (int K = 0; K + 1 < TG::NK; ++K) {
@@ -209,7 +268,7 @@ struct LmcOwner {
 // 4/5 last panel, 6 its rows loaded, 7 its columns factored
 #define LMC_STAMP(k)                                                                    \
   do {                                                                                  \
-    if (stamps != nullptr && lane == 0) stamps[k] = __builtin_amdgcn_s_memrealtime();  \
+    if (stamps != nullptr && lane == 0) stamps[k] = rph_stamp_clock();               \
   } while (0)
 
 template <int P>

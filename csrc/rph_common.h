@@ -26,6 +26,16 @@
 
 namespace rph {
 
+// diagnostic clock (s_memrealtime, 100 MHz) read where the program puts it:
+// a volatile asm keeps its place among the other side-effecting instructions
+// (the builtin may be scheduled freely, which let phase stamps of the solve
+// land out of program order), and the wait makes the value ready at once
+RPH_INLINE unsigned long long rph_stamp_clock() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+
 // Pull the kernel-argument segment (the by-value launch descriptor, up to 10
 // 64-byte lines) into the scalar cache with every miss in flight at once.
 // Without it the compiler's own kernarg loads form a chain of 4-6 dependent
