@@ -751,6 +751,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   double* vec = lds + TG::OFF_D;  // the solution d
   unsigned* pub = reinterpret_cast<unsigned*>(lds + TG::OFF_FLAGS);
   unsigned* fac = pub + TG::NT + 1;
+  unsigned* xdone = fac + TG::NT + 1;  // owner waves done inverting the diagonal blocks
   static_assert(P <= 256, "one parameter per thread");
   const double gi = tid < P ? (accept ? g_new : g_old) : 0.0;
   const double wbest = tid < P ? (best == 0 ? w_slot0 : w_slot1) : 0.0;  // for the final update
@@ -772,7 +773,7 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       s_fail = 0;
     }
   }
-  if (tid < 2 * (TG::NT + 1)) pub[tid] = 0u;
+  if (tid < 2 * (TG::NT + 1) + 1) pub[tid] = 0u;  // pub, fac, xdone
   __syncthreads();
   double dmp = 0.0;  // this parameter's damping term lam 2G_ii + ridge (for the predicted reduction)
   if (tid < P) {
@@ -791,12 +792,21 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       lmc_panels<P>(T, lds + TG::OFF_RDG, lds + TG::OFF_BC, pub, fac, &s_fail, stp);
     }
       RPH_STAMPS(6);
-      lmc_backward<P>(T, lds + TG::OFF_RDG, vec);
+      lmc_backward<P>(T, lds + TG::OFF_RDG, vec, lds + TG::OFF_X, xdone, &s_fail);
       RPH_STAMPS(7);
       break;
-    case 1: LmcOwner<P, 0>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
-    case 2: LmcOwner<P, 1>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
-    default: LmcOwner<P, 2>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail); break;
+    case 1:
+      LmcOwner<P, 0>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail, lds + TG::OFF_RDG,
+                                             lds + TG::OFF_X, xdone);
+      break;
+    case 2:
+      LmcOwner<P, 1>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail, lds + TG::OFF_RDG,
+                                             lds + TG::OFF_X, xdone);
+      break;
+    default:
+      LmcOwner<P, 2>::template run<STAGED>(src, lds + TG::OFF_DIAG, g, T, pub, fac, &s_fail, lds + TG::OFF_RDG,
+                                             lds + TG::OFF_X, xdone);
+      break;
   }
   __syncthreads();
   RPH_STAMPS(3);

@@ -46,7 +46,11 @@ struct TileGrid {
   static constexpr int OFF_DIAG = OFF_D;
   static constexpr int OFF_RDG = OFF_D + PT;
   static constexpr int OFF_BC = OFF_RDG + PT;
-  static constexpr int OFF_FLAGS = OFF_BC + 32;  // (as unsigned) pub[NT + 1], fac[NT + 1]
+  // the inverses of the diagonal blocks 0..NK-2 of L (owners, after their
+  // last update), for the backward solve - the nets with up to 48 tiles
+  static constexpr int NX = NTILE <= 48 ? NK - 1 : 0;
+  static constexpr int OFF_X = OFF_BC + 32;
+  static constexpr int OFF_FLAGS = OFF_X + NX * 256;  // (as unsigned) pub[NT + 1], fac[NT + 1], xdone
   static constexpr int LDS_BYTES = OFF_FLAGS * 8 + 2 * (NT + 1) * 4 + 16;
   // lower tile t (column-major) <-> (row block, column block)
   static constexpr int tidx(int ib, int jb) { return jb * NT - jb * (jb - 1) / 2 + (ib - jb); }
@@ -238,25 +242,59 @@ struct LmcOwner {
     });
   }
 
+  // the inverse of the diagonal blocks K = O + 3 s (< NX) of L: lanes 16 s + c
+  // compute column c by forward substitution (in-lane chains, the L entries
+  // as LDS broadcasts) -> X[K][i][c]
+  RPH_INLINE static void invert(const double* T, const double* rdg, double* X, int lane) {
+#pragma clang fp contract(off)
+    const int s = lane >> 4, c = lane & 15, K = O + 3 * s;
+    if (K < TG::NX) {
+      const double* Lt = T + TG::tidx(K, K) * 256;
+      double x[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        double s0 = i == c ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < i; ++k) {
+          const double l = Lt[tg_off(i, k)];
+          if (k & 1) s1 = __builtin_fma(-l, x[k], s1);
+          else s0 = __builtin_fma(-l, x[k], s0);
+        }
+        x[i] = (s0 + s1) * rdg[16 * K + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) X[K * 256 + i * 16 + c] = x[i];
+    }
+  }
+
   // STAGED: the tiles from the store (lmc_stage), else from the Gram block
   template <bool STAGED>
   RPH_INLINE static void run(const double* src, const double* diag, const double* g, double* T, unsigned* pub,
-                             const unsigned* fac, int* s_fail) {
+                             const unsigned* fac, int* s_fail, const double* rdg, double* X, unsigned* xdone) {
     const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
     lmc_d4 C[TPW];
     if constexpr (STAGED) load_staged(C, T, diag, lr, lq);
     else load(C, src, diag, g, lr, lq);
     publish(C, T, 0, lr, lq);
     lmc_signal(&pub[0]);
+    bool ok = true;
     for (int K = 0; K + 1 < TG::NK; ++K) {
       if (!lmc_wait(&fac[K], 1u)) {
         *s_fail = 2;
-        return;
+        ok = false;
+        break;
       }
       update(C, T, K, K + 1, K + 1, lr, lq);  // look-ahead: the next panel's column block
       publish(C, T, K + 1, lr, lq);
       lmc_signal(&pub[K + 1]);
       update(C, T, K, K + 2, TG::NT - 1, lr, lq);
+    }
+    // idle from here (the last panel is the panel wave's): the diagonal blocks'
+    // inverses for the backward solve (signalled even after a failure, so the
+    // backward never waits out its bound)
+    if constexpr (TG::NX > 0) {
+      if (ok) invert(T, rdg, X, lane);
+      lmc_signal(xdone);
     }
   }
 };
@@ -377,7 +415,8 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
 // = (column, row residue mod 4), reduced by shuffles), then the 16 x 16
 // triangular block by a readlane chain.  d -> dv[0, P).
 template <int P>
-RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv) {
+RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv, const double* X, const unsigned* xdone,
+                             int* s_fail) {
 #pragma clang fp contract(off)
   using TG = TileGrid<P>;
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
@@ -403,18 +442,34 @@ RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv) {
     z += __shfl_xor(z, 32, 64);
     const double y = col < P ? T[TG::tidx(P >> 4, K) * 256 + tg_off(P & 15, c)] : 0.0;
     z = y - z;
-    // column c of the diagonal tile: L[16K + j][16K + c], j = 0..15
-    double lc[16];
-    const double* td = T + TG::tidx(K, K) * 256;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) lc[j] = td[tg_off(j, c)];
-    const double rd = col < P ? rdg[col] : 0.0;
     double dk = 0.0;
+    if constexpr (K < TG::NX) {
+      // an inverted block (owners): d = X^T z, X = L_KK^-1 - independent
+      // broadcasts instead of a dependent 16-step chain
+      if constexpr (K == TG::NX - 1)
+        if (!lmc_wait(xdone, 3u)) *s_fail = 2;
+      const double* xk = X + K * 256 + c;
+      double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-    for (int j = NC - 1; j >= 0; --j) {
-      const double dj = lmc_readlane(z * rd, j);  // d[16K + j] (final in lane j)
-      if (c == j) dk = dj;
-      z = __builtin_fma(-lc[j], dj, z);  // lanes c < j
+      for (int i = 0; i < 16; ++i) {
+        const double zi = lmc_readlane(z, i);
+        if (i & 1) a1 = __builtin_fma(xk[i * 16], zi, a1);
+        else a0 = __builtin_fma(xk[i * 16], zi, a0);
+      }
+      dk = a0 + a1;
+    } else {
+      // column c of the diagonal tile: L[16K + j][16K + c], j = 0..15
+      double lc[16];
+      const double* td = T + TG::tidx(K, K) * 256;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) lc[j] = td[tg_off(j, c)];
+      const double rd = col < P ? rdg[col] : 0.0;
+#pragma unroll
+      for (int j = NC - 1; j >= 0; --j) {
+        const double dj = lmc_readlane(z * rd, j);  // d[16K + j] (final in lane j)
+        if (c == j) dk = dj;
+        z = __builtin_fma(-lc[j], dj, z);  // lanes c < j
+      }
     }
     if (q == 0 && col < P) dv[col] = dk;
     lmc_wave_sync();
