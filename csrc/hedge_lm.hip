@@ -42,6 +42,34 @@ struct LmShape {
   static_assert(NP <= LM_NPMAX && NBLK * 1024 <= LM_GBLK_MAX, "network too large for the LM solver");
 };
 
+// compile-time unrolled loop: f(std::integral_constant<int, j>) for j in [0, N)
+template <class F, int... J>
+RPH_INLINE void lm_static_for(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, class F>
+RPH_INLINE void lm_static_for(F&& f) {
+  lm_static_for(f, std::make_integer_sequence<int, N>{});
+}
+
+}  // namespace rph
+#include "lm_chol.h"
+namespace rph {
+
+// The solve's tile-store image of the Gram (strictly lower entries x2, at
+// their tile-store offsets), written by k_lm_reduce beside the 32 x 32 blocks
+// in the unused tail of the Gram region: the solve then stages it with
+// contiguous loads of 56 KB instead of gathering from 80 KB of blocks
+// (nets whose blocks and image fit the region, up to 48 tiles)
+template <int P>
+struct LmTPack {
+  using TG = TileGrid<P>;
+  static constexpr int OFF = LmShape<P>::NBLK * 1024;  // image offset in the reduced block
+  static constexpr int LEN = TG::NTILE * 256;
+  static constexpr bool ON = TG::NX > 0 && OFF + LEN <= LM_GBLK_MAX;
+  static constexpr int COPY = ON ? LEN : 0;  // doubles the best-block copy adds
+};
+
 // upper-triangular block b -> (mb, nb), mb <= nb, row-major
 RPH_INLINE void lm_blk(int b, int NB, int& mb, int& nb) {
   int m = 0;
@@ -134,7 +162,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     // the previous solve accepted its trial: best block := that trial's
     // reduced block (G, g, stats), spread over the grid; red_new is rewritten
     // only by this pass's reduce kernel, which runs after this one
-    constexpr int NG = LmShape<P>::NBLK * 1024;
+    constexpr int NG = LmShape<P>::NBLK * 1024 + LmTPack<P>::COPY;  // blocks (+ the tile-store image)
     // g | stats | output Gram (its entry 0 is -1 when the trial's pass did not build it)
     constexpr int NGR = LM_RED_OUTG - LM_GBLK_MAX + (B::NU <= LM_OG_MAX ? B::NU * (B::NU + 1) / 2 : 1);
     double* best_red = st + LMS_RED;
@@ -267,6 +295,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 // workgroups of the output-Gram part of k_lm_reduce (64 packed entries each)
 constexpr int lm_og_wgs(int NU) { return NU <= LM_OG_MAX ? (NU * (NU + 1) / 2 + 63) / 64 : 0; }
 
+
 template <int P, int R, int NU>
 __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
   using LS = LmShape<P>;
@@ -349,7 +378,19 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
         a += part[q * 64 + l];
         b += part[(q + 1) * 64 + l];
       }
-      red[e] = (a + b) * (double)lm.inv_ns;
+      const double v = (a + b) * (double)lm.inv_ns;
+      red[e] = v;
+      if constexpr (LmTPack<P>::ON) {
+        // this entry's place in the solve's tile store (strictly lower only)
+        using TG = TileGrid<P>;
+        const int b = e >> 10, f = e & 1023;
+        int mb = 0, rem = b;
+        while (rem >= TG::NBG - mb) rem -= TG::NBG - mb++;
+        const int q = f >> 6, h = (f >> 5) & 1;
+        const int lo = 32 * mb + (q & 3) + 4 * h + 8 * (q >> 2), hi = 32 * (mb + rem) + (f & 31);
+        if (lo < hi && hi < P)
+          red[LmTPack<P>::OFF + TG::tidx(hi >> 4, lo >> 4) * 256 + tg_off(hi & 15, lo & 15)] = 2.0 * v;
+      }
     }
     return;
   }
@@ -399,19 +440,6 @@ RPH_INLINE double lm_rsq(double x) {
   return y * __builtin_fma(-0.5 * x * y, y, 1.5);
 }
 
-// compile-time unrolled loop: f(std::integral_constant<int, j>) for j in [0, N)
-template <class F, int... J>
-RPH_INLINE void lm_static_for(F&& f, std::integer_sequence<int, J...>) {
-  (f(std::integral_constant<int, J>{}), ...);
-}
-template <int N, class F>
-RPH_INLINE void lm_static_for(F&& f) {
-  lm_static_for(f, std::make_integer_sequence<int, N>{});
-}
-
-}  // namespace rph
-#include "lm_chol.h"
-namespace rph {
 
 // Exact Newton step on the OUTPUT block at the best point (the value is
 // linear in the output layer's N = out_n parameters [P - N, P), so the loss
@@ -760,7 +788,20 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   // across the damping setup below (up to 16 tiles per owner wave: the larger
   // nets' owners load their tiles from the Gram block after the setup)
   constexpr bool STAGED = TG::TPW <= 16;
-  if constexpr (STAGED) lmc_stage<P>(T, src, gi);
+  if constexpr (LmTPack<P>::ON) {
+    // the reduce kernel's tile-store image: a contiguous copy (every load
+    // in flight before the first store)
+    static_assert(LmTPack<P>::LEN % 256 == 0, "whole tiles");
+    constexpr int NQ = LmTPack<P>::LEN / 256;  // loads per thread
+    const double* s1 = src + LmTPack<P>::OFF;
+    double v[NQ];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) v[u] = s1[u * 256 + tid];
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) T[u * 256 + tid] = v[u];
+  } else if constexpr (STAGED) {
+    lmc_stage<P>(T, src);
+  }
   if (wid == 0) {
     double s = 0.0;
 #pragma unroll
@@ -782,6 +823,9 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     // still gets damped, so growing lam always shortens its step
     dmp = fmax(a_ii, (double)lm.diag_floor * s_diag) * lam_m + (double)lm.ridge * s_diag;
     lds[TG::OFF_DIAG + tid] = a_ii + dmp;
+    // the rhs row -g into the staged store (after the setup barrier: the image
+    // copy above writes these places too)
+    if constexpr (STAGED) T[TG::tidx(P >> 4, tid >> 4) * 256 + tg_off(P & 15, tid & 15)] = -gi;
   }
   RPH_STAMPS(2);
   __syncthreads();  // the damped diagonal is in place

@@ -123,12 +123,12 @@ RPH_INLINE bool lmc_wait(const unsigned* flag, unsigned target) {
   return false;
 }
 
-// The whole workgroup copies the strictly lower Gram entries (x2) and the rhs
-// row -g into the tile store before the setup barrier: the Gram block is read
+// The whole workgroup copies the strictly lower Gram entries (x2) into the
+// tile store before the setup barrier (the rhs row follows it): the Gram block is read
 // in its own order (each 64-lane load one contiguous 512-byte run), where the
 // owners' accumulator-order loads touch 16 cache lines per instruction
 template <int P>
-RPH_INLINE void lmc_stage(double* T, const double* src, double g_tid) {
+RPH_INLINE void lmc_stage(double* T, const double* src) {
   using TG = TileGrid<P>;
   constexpr int NBG = TG::NBG, NBLK = NBG * (NBG + 1) / 2;
   constexpr int NIT = NBLK * 4;  // 256 threads x 4 = one 32 x 32 block
@@ -154,7 +154,6 @@ RPH_INLINE void lmc_stage(double* T, const double* src, double g_tid) {
       }
     }
   });
-  if (tid < P) T[TG::tidx(P >> 4, tid >> 4) * 256 + tg_off(P & 15, tid & 15)] = -g_tid;
 }
 
 // Owner wave O (0..2): its tiles are t = O + 3 j (compile-time), so every

@@ -291,6 +291,45 @@ def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
 LM_PAIR_WPS = 1  # csrc/hedge_lm.hip RPH_LM_PAIR_WPS default (one pass workgroup per CU)
 
 
+def lm_tpack_len(P: int, nblk: int) -> int:
+    """Doubles of the solve's tile-store image of the Gram that k_lm_reduce
+    writes after the 32 x 32 blocks (csrc/hedge_lm.hip LmTPack: nets with up
+    to 48 tiles whose blocks and image fit the Gram region), else 0.  A Gram
+    all-reduce over the ranks carries it with the blocks."""
+    nt = (P + 1 + 15) // 16
+    ntile = nt * (nt + 1) // 2
+    nx = (P + 15) // 16 - 1 if ntile <= 48 else 0
+    ln = ntile * 256
+    return ln if nx > 0 and nblk * 1024 + ln <= L.LM_GBLK_MAX else 0
+
+
+def lm_tpack_image(blocks, P: int, nblk: int):
+    """The tile-store image k_lm_reduce writes at red[nblk * 1024:] (strictly
+    lower Gram entries x2 at their csrc/lm_chol.h tile-store offsets) from the
+    32 x 32 blocks red[:nblk * 1024], for code that builds a reduced block on
+    the host (tests); None when the net has no image (lm_tpack_len 0)."""
+    import numpy as np
+    ln = lm_tpack_len(P, nblk)
+    if ln == 0:
+        return None
+    nbg, nt = (P + 31) // 32, (P + 1 + 15) // 16
+    e = np.arange(nblk * 1024)
+    b, f = e >> 10, e & 1023
+    starts = np.cumsum([0] + [nbg - m for m in range(nbg)])
+    mb = np.searchsorted(starts, b, side="right") - 1
+    nb = mb + (b - starts[mb])
+    q, h = f >> 6, (f >> 5) & 1
+    lo = 32 * mb + (q & 3) + 4 * h + 8 * (q >> 2)
+    hi = 32 * nb + (f & 31)
+    ok = (lo < hi) & (hi < P)
+    ib, jb, r, c = hi >> 4, lo >> 4, hi & 15, lo & 15
+    t = jb * nt - jb * (jb - 1) // 2 + (ib - jb)
+    off = t * 256 + r * 16 + (c ^ ((r >> 1) << 1))
+    img = np.zeros(ln)
+    img[off[ok]] = 2.0 * np.asarray(blocks, dtype=np.float64)[:nblk * 1024][ok]
+    return img
+
+
 def lm_two_per_cu(spec) -> bool:
     """csrc/hedge_lm.hip LmKernels::TWO for a net shape (no native library
     needed; tests/test_lm_cpu.py checks it against native.lm_shape)."""
@@ -679,7 +718,7 @@ class HipBackend:
         if self.world <= 1:
             return 0
         P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
-        return 8 * self._lm_greg(False) if self._lm_same_gram else 8 * (nblk * 1024 + L.LM_RED - L.LM_GBLK_MAX)
+        return 8 * self._lm_greg(False) if self._lm_same_gram else 8 * (nblk * 1024 + lm_tpack_len(P, nblk) + L.LM_RED - L.LM_GBLK_MAX)
 
     def _lm_greg(self, og: bool) -> int:
         """Doubles of the gradient region a pass exchanges (even: 16-byte
@@ -830,7 +869,7 @@ class HipBackend:
         if self.lm_mailbox is not None:
             x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
             if gram:
-                self.native.lm_dp_exchange(x, red, nblk * 1024, P, self.stream)
+                self.native.lm_dp_exchange(x, red, nblk * 1024 + lm_tpack_len(P, nblk), P, self.stream)
             else:
                 self.native.lm_dp_exchange(x, red, 0, self._lm_greg(og), self.stream)
             return

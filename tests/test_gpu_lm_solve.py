@@ -16,6 +16,8 @@ import numpy as np
 import pytest
 import torch
 
+from rphedge.engine import lm_tpack_image
+
 pytestmark = pytest.mark.gpu
 
 # (shape, P)
@@ -52,6 +54,9 @@ def make_block(L, G, g, loss_mean, count=1000.0):
     enc = encode_gram(G)
     red[:enc.size] = enc
     P = G.shape[0]
+    img = lm_tpack_image(enc, P, enc.size // 1024)  # what k_lm_reduce writes beside the blocks
+    if img is not None:
+        red[enc.size:enc.size + img.size] = img
     red[L.LM_GBLK_MAX:L.LM_GBLK_MAX + P] = g
     s = L.LM_GBLK_MAX + L.LM_NPMAX
     red[s:s + 4] = [loss_mean * count, 0.5, 0.25, count]
