@@ -103,8 +103,6 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   __shared__ __attribute__((aligned(16))) float jt[LM_TILE * JP];
   // the output-Gram image of the OG instantiation (the last passes of an lm_out_fix fit)
   __shared__ __attribute__((aligned(16))) unsigned char og_img[B::OGM ? B::OG_LDS : 16];
-  // the gradient-outer-product images of the MG instantiation (A/B, LmDesc.mfma_grad)
-  __shared__ __attribute__((aligned(16))) float mg_img[B::MGM ? B::MG_LDS / 4 : 4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   prefetch_kernarg_end(kat);
   // diagnostic phase stamps of every workgroup but 0 and 1 (tools/stamp_lm.py;
@@ -197,7 +195,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     B::make_frags(wl + S::OW2, fr);
     float val[NR];
     B::partial(d, 0, perm, wl, fr, scratch, pre, val, sc, lm.out_gram != 0, og_img,
-               lm.slab_o + ((size_t)inst * lm.num_wgs + blockIdx.x) * 3 * 1024, mg_img);
+               lm.slab_o + ((size_t)inst * lm.num_wgs + blockIdx.x) * 3 * 1024);
 #pragma unroll
     for (int j = 0; j < NR; ++j)
       if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
@@ -229,6 +227,30 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     pr[NHOLD - 1] = d.bond;
     float z1[H], a1[H], z2[H], a2[H], hold[NHOLD];
     net_forward<NIN, H, NO, HEAD>(wl, x, d.alpha, z1, a1, z2, a2, hold);
+    // pinball fits (IRLS Gauss-Newton): the Gram is the curvature of the
+    // pinball loss's quadratic majoriser at this point, mean_p w_p J_p J_p^T / 2
+    // with w_p = 1 / (2 max(|r_p|, delta)) (r = V - y), i.e. the row scaled by
+    // 1 / (2 sqrt(max(|r_p|, delta))); delta = max(q_delta, q_kappa x the mean
+    // |r| of this 64-path tile) keeps the weights of the small residuals
+    // bounded (a near-zero residual would otherwise dominate the step).  The
+    // shard-subsample Gram only (the host keeps pinball fits off the simulated
+    // subsample, which has no targets)
+    float wq = 1.f;
+    if (d.loss == LOSS_PINBALL && !lm.gram_side) {
+      const long long p = (slot / lm.gram_blk) * lm.gram_blk_stride + slot % lm.gram_blk;
+      float V = 0.f;
+#pragma unroll
+      for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
+      const float ra = ok ? fabsf(V - d.target[ok ? p : 0]) : 0.f;
+      float sa = ra, sc = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        sa += __shfl_xor(sa, o, 64);
+        sc += __shfl_xor(sc, o, 64);
+      }
+      const float dl = fmaxf(lm.q_delta, lm.q_kappa * sa / fmaxf(sc, 1.f));
+      wq = 0.5f * __builtin_amdgcn_rsqf(fmaxf(ra, dl));
+    }
     // J_p = dV_p / dtheta  (dV = 1)
     float dout[NO];
     if (HEAD == HEAD_COMPLEMENT) {
@@ -238,7 +260,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
       for (int k = 0; k < NO; ++k) dout[k] = pr[k];
     }
     float* row = jt + lane * JP;
-    const float m = ok ? 1.f : 0.f;  // paths beyond the shard contribute nothing
+    const float m = ok ? wq : 0.f;  // paths beyond the shard contribute nothing
 #pragma unroll
     for (int k = 0; k < NO; ++k) row[S::OB3 + k] = m * dout[k];
     float dz2[H];
@@ -906,20 +928,12 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
 // ---------------------------------------------------------------------------
 template <int NIN, int H, int NO, int HEAD>
 struct LmKernels {
-  // the 1-3 input nets could run two pass workgroups per CU (measured slower:
-  // one wave per SIMD with the packed two-path body is the default)
-#ifndef RPH_LM_PAIR_WPS
-#define RPH_LM_PAIR_WPS 1
-#endif
-  static constexpr bool TWO = RPH_LM_PAIR_WPS == 2 && NIN <= 3 && NetShape<NIN, H, NO, HEAD>::R <= 128;
-  using Body = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1>;  // two paths per lane, packed fp32
+  // one pass workgroup per CU, two paths per lane, packed fp32 (two
+  // workgroups per CU spill: BENCHMARKS.md round 4)
+  using Body = NarrowPairBody<NIN, H, NO, HEAD>;
   // the same body + the full-batch output-layer Gram on the matrix cores (the
   // last LM_OUTG_TAIL passes of an lm_out_fix fit)
-  using BodyOG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true>;
-  // A/B (LmDesc.mfma_grad): the W2 / W3 gradient outer products on the matrix cores
-  using BodyMG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, false, true>;
-  using BodyMGOG = NarrowPairBody<NIN, H, NO, HEAD, TWO ? 2 : 1, true, true>;
-  static constexpr bool HAS_MG = BodyMG::MGM && NIN <= 3;
+  using BodyOG = NarrowPairBody<NIN, H, NO, HEAD, true>;
   using S = NetShape<NIN, H, NO, HEAD>;
   // the tile store + vectors + hand-off counters (lm_chol.h)
   static constexpr int smem() { return TileGrid<S::P>::LDS_BYTES; }
@@ -950,8 +964,10 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   }
   if (lm->red_wgs != nblk * 1024 / 64 + R / 4 + lm_og_wgs(nu)) return rph_report("rph_lm", "bad red_wgs");
   if (lm->out_gram && (!lm->slab_o || nu > LM_OG_MAX)) return rph_report("rph_lm", "output Gram needs slab_o (<= 64 output parameters)");
-  if (lm->mfma_grad && !(d->h == 8 && d->nin <= 3 && (d->head == HEAD_COMPLEMENT || d->nout <= 8)))
-    return rph_report("rph_lm", "mfma_grad: 8-unit nets with up to 3 inputs only");
+  if (d->loss != LOSS_MSE && d->loss != LOSS_PINBALL) return rph_report("rph_lm", "LM fits: MSE or pinball loss");
+  if (d->loss == LOSS_PINBALL && (lm->gram_side || lm->out_gram || lm->out_n > 0 || lm->bias_index >= 0 ||
+                                  !(lm->q_delta > 0.f)))
+    return rph_report("rph_lm", "pinball LM fits: shard Gram subsample, no output / bias step, q_delta > 0");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   if (lm->inst < 1 || lm->inst > LM_SEL_MAX) return rph_report("rph_lm", "bad instance count");
   if (lm->inst > 1 && !lm->explore) return rph_report("rph_lm", "several instances are exploration fits only");
@@ -966,17 +982,6 @@ static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const 
   // path workgroups + Gram-only workgroups past them (Gram subsample > 64 x path grid)
   const unsigned grid = (unsigned)(lm->gram_wgs > lm->num_wgs ? lm->gram_wgs : lm->num_wgs);
   const bool og = lm->out_gram && pass > lm->passes - LM_OUTG_TAIL;
-  if constexpr (K::HAS_MG) {
-    if (lm->mfma_grad) {
-      if (og && K::BodyMGOG::OGM)
-        hipLaunchKernelGGL((k_lm_pass<typename K::BodyMGOG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
-                           red_new);
-      else
-        hipLaunchKernelGGL((k_lm_pass<typename K::BodyMG>), dim3(grid, lm->inst), dim3(256), 0, s, *d, *lm, pass,
-                           red_new);
-      return (int)hipGetLastError();
-    }
-  }
   if constexpr (K::BodyOG::OGM) {
     // the last LM_OUTG_TAIL evaluations of an lm_out_fix fit build the output Gram
     if (og) {
@@ -1247,7 +1252,7 @@ extern "C" int rph_lm_shape(int nin, int h, int nout, int head, int* p, int* r, 
     *p = K::S::P;                                                        \
     *r = K::S::R;                                                        \
     *nblk = LmShape<K::S::P>::NBLK;                                      \
-    *two_per_cu = K::TWO ? 1 : 0;                                        \
+    *two_per_cu = 0;                                                     \
     return 0;                                                            \
   }
   RPH_LM_SHAPES(X)

@@ -196,9 +196,9 @@ typedef short nb_s16x4 __attribute__((ext_vector_type(4)));
 typedef short nb_s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) nb_s16x4 nb_lds_s16x4;
 
-template <int NIN, int H, int NO, int HEAD, int WPS = 2, bool OG = false, bool MG = false>
+template <int NIN, int H, int NO, int HEAD, bool OG = false>
 struct NarrowPairBody {
-  static constexpr int WAVES_PER_SIMD = WPS;  // 2: two workgroups per CU (the 512-workgroup LM pass grid)
+  static constexpr int WAVES_PER_SIMD = 1;  // one pass workgroup per CU (256 VGPRs + AGPRs per lane)
   static constexpr int NIN_ = NIN, H_ = H, NO_ = NO, HEAD_ = HEAD;
   using S = NetShape<NIN, H, NO, HEAD>;
   static constexpr int P = S::P;
@@ -231,17 +231,6 @@ struct NarrowPairBody {
   static constexpr bool OGM = OG && NU <= 64;
   static_assert(!OG || NU <= 64, "output-layer Gram: at most 64 output parameters");
   static_assert(4 * NBO * 1024 * 4 <= OG_LDS, "the waves' output-Gram tiles reuse the image LDS");
-  // MG (A/B variant, LmDesc.mfma_grad): the two largest weight-gradient outer
-  // products, sum_p a1 (x) dz2 (W2, H x H) and sum_p a2 (x) dout (W3, H x NO),
-  // on v_mfma_f32_16x16x4_f32 (exact fp32 products) instead of the VALU: per
-  // 128-path iteration each lane writes rows [a1 | a2] and [dz2 | dout] of its
-  // two paths to fp32 [path][16] LDS images, 32 MFMAs (K = 4 paths) read one
-  // operand element per lane from each, the 16 x 16 tile (rows a1 | a2,
-  // columns dz2 | dout) stays in 4 accumulator registers per lane and joins
-  // the packet after the loop
-  static constexpr int NOH = HEAD == HEAD_FREE ? NO : 1;
-  static constexpr bool MGM = MG && H == 8 && NOH <= 8;
-  static constexpr int MG_LDS = 4 * 2 * 128 * 16 * 4;  // per wave: L and R images, 128 rows x 16 floats
   struct Frags {};
   struct Pre {
     nb_f2 x[NIN], pr[NHOLD], y;
@@ -375,7 +364,7 @@ struct NarrowPairBody {
   RPH_INLINE static void partial(const TrainDesc& d, int step, const Perm& perm, const float* __restrict__ W,
                                  const Frags&, float* lds, Pre& pre, float (&val)[NR], const Sched& sc,
                                  const bool og = false, unsigned char* og_lds = nullptr,
-                                 float* __restrict__ og_out = nullptr, float* mg_lds = nullptr) {
+                                 float* __restrict__ og_out = nullptr) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long long stride = sc.bstep * 128;
     const long long jend = sc.bend * 128 < d.batch ? sc.bend * 128 : d.batch;
@@ -384,13 +373,11 @@ struct NarrowPairBody {
     for (int i = 0; i < R; ++i) g[i] = 0.f;
     const float alpha = d.alpha;
     const float two_inv = 2.f * d.inv_batch;
+    const bool pinball = d.loss == LOSS_PINBALL;
+    const float q = d.quantile;
     Pre cur = pre;
     nb_f32x16 oacc[NBO];
     unsigned char* const img = og_lds + wid * OG_ROWS * OG_PITCH;
-    typedef float mg_f4 __attribute__((ext_vector_type(4)));
-    mg_f4 macc = {0.f, 0.f, 0.f, 0.f};
-    float* const mgL = mg_lds + wid * 2 * 128 * 16;  // [path][a1 | a2]
-    float* const mgR = mgL + 128 * 16;              // [path][dz2 | dout | 0]
     if constexpr (OGM) {
 #pragma unroll
       for (int b = 0; b < NBO; ++b) oacc[b] = nb_f32x16{};
@@ -456,7 +443,19 @@ struct NarrowPairBody {
       }
       // MSE loss statistics and dL/dV (mean over the global batch)
       const nb_f2 e = V - y;
-      const nb_f2 le = e * e * m;
+      // per-path loss and dL/dV: MSE, or the reference's pinball loss
+      // (Replicating_Portfolio.py:138-145; uniform branch on the descriptor)
+      nb_f2 le, dV;
+      if (pinball) {
+        float lx, ly, gx, gy;
+        path_loss(LOSS_PINBALL, q, V.x, y.x, lx, gx);
+        path_loss(LOSS_PINBALL, q, V.y, y.y, ly, gy);
+        le = nb_f2{lx, ly} * m;
+        dV = nb_f2{gx, gy} * m * d.inv_batch;
+      } else {
+        le = e * e * m;
+        dV = e * m * two_inv;
+      }
       const nb_f2 ae = nb_f2{fabsf(e.x), fabsf(e.y)} * m;
       const nb_f2 ape = ae * nb_f2{__builtin_amdgcn_rcpf(fmaxf(fabsf(y.x), 1e-7f)),
                                    __builtin_amdgcn_rcpf(fmaxf(fabsf(y.y), 1e-7f))};
@@ -467,7 +466,6 @@ struct NarrowPairBody {
       if constexpr (OGM) {
         if (og) og_accum(img, oacc, a2, pr, m, lane);
       }
-      const nb_f2 dV = e * m * two_inv;
 
       // backward
       nb_f2 dout[NO];
@@ -485,7 +483,7 @@ struct NarrowPairBody {
         nb_f2 da = nb_s(0.f);
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
-          if constexpr (!MGM) g[S::OW3 + j * NO + k] = nb_acc(g[S::OW3 + j * NO + k], a2[j], dout[k]);
+          g[S::OW3 + j * NO + k] = nb_acc(g[S::OW3 + j * NO + k], a2[j], dout[k]);
           da = nb_fma(nb_s(Wi[S::OW3 + j * NO + k]), dout[k], da);
         }
         dz2[j] = nb_lrelu_bwd(a2[j], da, alpha);
@@ -496,7 +494,7 @@ struct NarrowPairBody {
         nb_f2 da0 = nb_s(0.f), da1 = nb_s(0.f);  // two chains (even / odd j)
 #pragma unroll
         for (int j = 0; j < H; ++j) {
-          if constexpr (!MGM) g[S::OW2 + i * H + j] = nb_acc(g[S::OW2 + i * H + j], a1[i], dz2[j]);
+          g[S::OW2 + i * H + j] = nb_acc(g[S::OW2 + i * H + j], a1[i], dz2[j]);
           if (j & 1) da1 = nb_fma(nb_s(Wi[S::OW2 + i * H + j]), dz2[j], da1);
           else da0 = nb_fma(nb_s(Wi[S::OW2 + i * H + j]), dz2[j], da0);
         }
@@ -505,50 +503,12 @@ struct NarrowPairBody {
 #pragma unroll
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = nb_acc(g[S::OW1 + f * H + i], x[f], dz1);
       }
-      if constexpr (MGM) {
-        // rows of both paths -> the L / R images, then sum_p L_p R_p^T over
-        // the 128 paths on the matrix cores (K = 4 paths per instruction)
-        typedef float mg_f4v __attribute__((ext_vector_type(4)));
-        og_wave_sync();  // the previous iteration's operand reads are done
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const int row = lane + 64 * h2;
-          auto pick = [&](nb_f2 v) { return h2 ? v.y : v.x; };
-          float* Lr = mgL + row * 16;
-          float* Rr = mgR + row * 16;
-          *(mg_f4v*)(Lr + 0) = mg_f4v{pick(a1[0]), pick(a1[1]), pick(a1[2]), pick(a1[3])};
-          *(mg_f4v*)(Lr + 4) = mg_f4v{pick(a1[4]), pick(a1[5]), pick(a1[6]), pick(a1[7])};
-          *(mg_f4v*)(Lr + 8) = mg_f4v{pick(a2[0]), pick(a2[1]), pick(a2[2]), pick(a2[3])};
-          *(mg_f4v*)(Lr + 12) = mg_f4v{pick(a2[4]), pick(a2[5]), pick(a2[6]), pick(a2[7])};
-          *(mg_f4v*)(Rr + 0) = mg_f4v{pick(dz2[0]), pick(dz2[1]), pick(dz2[2]), pick(dz2[3])};
-          *(mg_f4v*)(Rr + 4) = mg_f4v{pick(dz2[4]), pick(dz2[5]), pick(dz2[6]), pick(dz2[7])};
-          float r8[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) r8[k] = k < NOH ? pick(dout[k < NOH ? k : 0]) : 0.f;
-          *(mg_f4v*)(Rr + 8) = mg_f4v{r8[0], r8[1], r8[2], r8[3]};
-          *(mg_f4v*)(Rr + 12) = mg_f4v{r8[4], r8[5], r8[6], r8[7]};
-        }
-        og_wave_sync();
-        const int col = lane & 15, kq = lane >> 4;
-#pragma unroll
-        for (int s4 = 0; s4 < 32; ++s4) {
-          const float av = mgL[(4 * s4 + kq) * 16 + col];
-          const float bv = mgR[(4 * s4 + kq) * 16 + col];
-          macc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, macc, 0, 0, 0);
-        }
-      }
     }
     RPH_STAMP_BODY(5);  // path loop done
     wave_reduce_scatter<R>(g, lane);
     constexpr int PER = R / 64;
 #pragma unroll
     for (int i = 0; i < PER; ++i) lds[wid * R + lane * PER + i] = g[i];
-    if constexpr (MGM) {
-      // each wave's 16 x 16 tile (C[4 (lane / 16) + r][lane % 16]) -> LDS
-      __syncthreads();  // every wave's last operand reads are done
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mg_lds[wid * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)] = macc[r];
-    }
     if constexpr (OGM) {
       if (og) {
         // the four waves' output-Gram tiles -> one workgroup tile (fixed order)
@@ -563,13 +523,6 @@ struct NarrowPairBody {
     __syncthreads();
     const int t = threadIdx.x;
     val[0] = (t < R) ? (lds[t] + lds[R + t]) + (lds[2 * R + t] + lds[3 * R + t]) : 0.f;
-    if constexpr (MGM) {
-      // the W2 / W3 entries come from the four waves' tiles (fixed order)
-      int e = -1;
-      if (t >= S::OW2 && t < S::OW2 + H * H) e = ((t - S::OW2) / H) * 16 + (t - S::OW2) % H;
-      else if (t >= S::OW3 && t < S::OW3 + H * NOH) e = (8 + (t - S::OW3) / NOH) * 16 + 8 + (t - S::OW3) % NOH;
-      if (e >= 0) val[0] = (mg_lds[e] + mg_lds[256 + e]) + (mg_lds[512 + e] + mg_lds[768 + e]);
-    }
     if constexpr (OGM) {
       if (og) {
         const float* ot = reinterpret_cast<const float*>(og_lds);

@@ -70,18 +70,9 @@ struct TileGrid {
 RPH_INLINE int tg_off(int r, int c) { return r * 16 + (c ^ ((r >> 1) << 1)); }
 
 // fp64 reciprocal square root: v_rsq_f64 (rel. err 5.2e-8) + one Newton step
-// (RPH_LMC_FAST_RSQ A/B: the hardware estimate alone - three dependent fp64
-// operations fewer on the panel's per-column pivot chain)
-#ifndef RPH_LMC_FAST_RSQ
-#define RPH_LMC_FAST_RSQ 0
-#endif
 RPH_INLINE double lmc_rsq(double x) {
   const double y = __builtin_amdgcn_rsq(x);
-#if RPH_LMC_FAST_RSQ
-  return y;
-#else
   return y * __builtin_fma(-0.5 * x * y, y, 1.5);
-#endif
 }
 
 RPH_INLINE double lmc_readlane(double v, int l) {
@@ -308,21 +299,49 @@ struct LmcOwner {
     if (stamps != nullptr && lane == 0) stamps[k] = rph_stamp_clock();               \
   } while (0)
 
+// row_newbcast:J (gfx90a+ 64-bit DPP): every lane of each 16-lane row gets
+// lane J of that row's v - one v_mov_b64_dpp, no SGPR or LDS round trip
+template <int J>
+RPH_INLINE double lmc_bcast(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xF, 0xF, true);
+}
+
+// A 16-row tile row (16 doubles) from the store / to the store (swizzled columns)
+RPH_INLINE void lmc_load_row(double (&a)[16], const double* tr, int r) {
+  const int sw = (r >> 1) << 1;
+#pragma unroll
+  for (int c = 0; c < 16; c += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(tr + (c ^ sw));
+    a[c] = v.x;
+    a[c + 1] = v.y;
+  }
+}
+
 template <int P>
 RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* pub, unsigned* fac, int* s_fail,
                            unsigned long long* stamps) {
 #pragma clang fp contract(off)
   using TG = TileGrid<P>;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, li = lane & 15;
+  (void)bc;
   bool ok = true, alive = true;
-  // every panel is its own straight-line code (static column count, static
+  // Register layout of panel K: every 16-lane DPP row holds a replica of the
+  // diagonal tile (lane 16 r + i: its row i in dk[]), and the panel rows
+  // below it are spread over all 64 lanes (row 16K + 16 + lane + 64 s in
+  // a[s][]).  Column c's entries L[16K + j][16K + c] of the diagonal tile are
+  // then one row_newbcast:j away from every lane (lmc_bcast): the pivot, the
+  // column scale and every trailing update of the panel are in-register -
+  // no v_readlane / SGPR hazard and no LDS round trip per column.  The fma
+  // sequence applied to every entry is the same as a serial right-looking
+  // Cholesky (bitwise the previous readlane / LDS-broadcast panel).
+  // Every panel is its own straight-line code (static column count, static
   // row slots): the column chain of one panel is a single basic block, so the
-  // next column's pivot chain overlaps this column's trailing updates
+  // next column's pivot chain overlaps this column's trailing updates.
   lm_static_for<TG::NK>([&](auto kc) {
     constexpr int K = decltype(kc)::value;
     constexpr int NC = P - 16 * K < 16 ? P - 16 * K : 16;  // factored columns
-    constexpr int ROWS = TG::PT - 16 * K;                  // rows of the panel (tile rows K..NT-1)
-    constexpr int NS = (ROWS + 63) / 64;                   // row slots per lane
+    constexpr int OFF = TG::PT - 16 * K - 16;              // panel rows below the diagonal tile
+    constexpr int NS = (OFF + 63) / 64;                    // their row slots per lane
     if (!alive) return;
     if (!lmc_wait(&pub[K], 3u)) {
       *s_fail = 2;
@@ -331,74 +350,86 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
     }
     if constexpr (K < 2) LMC_STAMP(2 * K);
     else if constexpr (K == TG::NK - 1) LMC_STAMP(4);
-    double a[NS][16];
+    double dk[16];
+    lmc_load_row(dk, T + TG::tidx(K, K) * 256 + li * 16, li);
+    // (a lane past the last panel row duplicates row o % OFF: it computes and
+    // stores exactly that row's values, so loads and stores need no branch -
+    // a conditional store would let the compiler sink the row updates into
+    // it, keeping every broadcast alive until then)
+    double a[NS > 0 ? NS : 1][16];
+    int arow[NS > 0 ? NS : 1];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const int row = 16 * K + lane + 64 * s;
-      if (s + 1 < NS || lane + 64 * s < ROWS) {
-        const double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
-        const int sw = ((row & 15) >> 1) << 1;
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-          const double2 v = *reinterpret_cast<const double2*>(tr + (c ^ sw));
-          a[s][c] = v.x;
-          a[s][c + 1] = v.y;
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) a[s][c] = 0.0;
-      }
+      const int o = lane + 64 * s;
+      arow[s] = 16 * K + 16 + (o < OFF ? o : o % (OFF > 0 ? OFF : 1));
+      lmc_load_row(a[s], T + TG::tidx(arow[s] >> 4, K) * 256 + (arow[s] & 15) * 16, arow[s] & 15);
     }
     if constexpr (K == TG::NK - 1) LMC_STAMP(6);
-    // the lane's own diagonal entry (lanes 0..15: row 16K + lane of the diagonal
-    // tile), updated with its OWN L entries - the same fma sequence the column
-    // updates apply to it - so the pivot chain never waits for a broadcast
-    double dg = lane < 16 ? T[TG::tidx(K, K) * 256 + tg_off(lane, lane)] : 1.0;
+    // column c's block: scale column c, update column c + 1 and start the
+    // pivot chain of c + 1, then the remaining updates of column c (which
+    // hide that chain's latency); a scheduling barrier closes every block, so
+    // only one column's broadcasts are live at a time (no spills)
+    double piv = lmc_bcast<0>(dk[0]);
+    double rl = lmc_rsq(piv);
+    double myrl = 0.0;  // lane i < NC of every DPP row: 1 / L[16K + i][16K + i]
     lm_static_for<NC>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
-      const double piv = lmc_readlane(dg, c);
       ok = ok && piv > 0.0;
-      const double rl = lmc_rsq(piv);
+      dk[c] *= rl;  // lane i: L[16K + i][16K + c] (i >= c)
 #pragma unroll
       for (int s = 0; s < NS; ++s) a[s][c] *= rl;
-      if (lane == c) rdg[16 * K + c] = rl;
-      // look-ahead: the next column first (its L entry by v_readlane), so the
-      // next pivot and scale wait for nothing but this column's arithmetic
+      myrl = li == c ? rl : myrl;
+      double piv_n = 1.0, rl_n = 1.0;
       if constexpr (c + 1 < NC) {
-        const double l1 = lmc_readlane(a[0][c], c + 1);  // L[16K + c + 1][16K + c]
+        const double l1 = lmc_bcast<c + 1>(dk[c]);  // L[16K + c + 1][16K + c]
+        dk[c + 1] = __builtin_fma(-dk[c], l1, dk[c + 1]);
 #pragma unroll
         for (int s = 0; s < NS; ++s) a[s][c + 1] = __builtin_fma(-a[s][c], l1, a[s][c + 1]);
+        // the next pivot: lane c + 1's diagonal, final after this update
+        piv_n = lmc_bcast<c + 1>(dk[c + 1]);
+        rl_n = lmc_rsq(piv_n);
       }
-      dg = __builtin_fma(-a[0][c], a[0][c], dg);  // lanes > c: their diagonal's column-c update
-      // the remaining columns: L[16K + j][16K + c] through an LDS broadcast
-      // (double-buffered by column parity: no write-after-read wait)
-      if constexpr (c + 2 < NC) {
-        double* b = bc + 16 * (c & 1);
-        if (lane < 16) b[lane] = a[0][c];
-        lmc_wave_sync();  // the other lanes' stores: no load may be forwarded across
-#pragma unroll
-        for (int j = c + 2; j < NC; ++j) {
-          const double lj = b[j];
+      lm_static_for<NC>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j > c + 1) {
+          const double lj = lmc_bcast<j>(dk[c]);  // L[16K + j][16K + c]
+          dk[j] = __builtin_fma(-dk[c], lj, dk[j]);
 #pragma unroll
           for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
         }
-      }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      piv = piv_n;
+      rl = rl_n;
     });
+    rdg[16 * K + li] = myrl;  // (every DPP row the same value; entries >= P unused)
     if constexpr (K == TG::NK - 1) LMC_STAMP(7);
-    // write L back (the diagonal tile's upper triangle as zeros)
+    // write L back: the rows below the diagonal tile first (same basic block
+    // as their updates), then the diagonal tile
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const int row = 16 * K + lane + 64 * s;
-      if (s + 1 < NS || lane + 64 * s < ROWS) {
-        double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
-        const int sw = ((row & 15) >> 1) << 1;
+      const int row = arow[s];
+      double* tr = T + TG::tidx(row >> 4, K) * 256 + (row & 15) * 16;
+      const int sw = ((row & 15) >> 1) << 1;
 #pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-          double2 v;
-          v.x = (s == 0 && c > lane) ? 0.0 : a[s][c];
-          v.y = (s == 0 && c + 1 > lane) ? 0.0 : a[s][c + 1];
-          *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
-        }
+      for (int c = 0; c < 16; c += 2) {
+        double2 v;
+        v.x = a[s][c];
+        v.y = a[s][c + 1];
+        *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
+      }
+    }
+    {
+      // the diagonal tile, its upper triangle as zeros (every DPP row stores
+      // the same values to the same places: no branch)
+      double* tr = T + TG::tidx(K, K) * 256 + li * 16;
+      const int sw = (li >> 1) << 1;
+#pragma unroll
+      for (int c = 0; c < 16; c += 2) {
+        double2 v;
+        v.x = c > li ? 0.0 : dk[c];
+        v.y = c + 1 > li ? 0.0 : dk[c + 1];
+        *reinterpret_cast<double2*>(tr + (c ^ sw)) = v;
       }
     }
     lmc_signal(&fac[K]);

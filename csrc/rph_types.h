@@ -300,7 +300,11 @@ struct LmDesc {
   const float* gfeat[MAXIN];
   const float* gprice[MAXIN];
   int gram_side;
-  int mfma_grad;                 // A/B: the W2 / W3 gradient outer products on the matrix cores (NarrowPairBody MG)
+  // pinball fits (TrainDesc.loss == LOSS_PINBALL): IRLS Gram weights
+  // 1 / (2 max(|r|, delta)), delta = max(q_delta, q_kappa x the mean |r| of
+  // the path's 64-path Gram tile) (target units)
+  float q_delta;
+  float q_kappa;
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)

@@ -281,6 +281,12 @@ class HedgeRun:
                                poll_every=tr.poll_every, seed=tr.seed,
                                feature_norm="none" if pf.raw_features else tr.feature_norm,
                                optimizer=str(tr.optimizer).lower(), lm_passes_first=int(tr.lm_passes_first),
+                               q99_optimizer=str(getattr(tr, "q99_optimizer", "adam")).lower(),
+                               lm_q_passes_first=int(getattr(tr, "lm_q_passes_first", 40)),
+                               lm_q_passes_rest=int(getattr(tr, "lm_q_passes_rest", 4)),
+                               lm_q_delta=float(getattr(tr, "lm_q_delta", 1e-4)),
+                               lm_q_kappa=float(getattr(tr, "lm_q_kappa", 3.0)),
+                               lm_q_start=str(getattr(tr, "lm_q_start", "mse")),
                                lm_passes_rest=int(tr.lm_passes_rest), lm_stop_tol=float(tr.lm_stop_tol),
                                lm_stop_min=int(tr.lm_stop_min), lm_lam0_rest=float(tr.lm_lam0_rest),
                                lm_lam0_first=float(tr.lm_lam0_first),

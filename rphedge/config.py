@@ -90,7 +90,18 @@ class TrainingParams:
     variant: int = -1                # narrow lag-kernel variant (-1: engine default; see engine.TrainConfig)
     concurrent_q99: bool = True      # two networks: run the pinball fit concurrently with the MSE fit (GPU)
     optimizer: str = "adam"          # MSE fits: "adam" (Keras-Adam minibatches, the reference) | "lm" (full-batch
-                                     # Levenberg-Marquardt on the GPU: csrc/hedge_lm.hip; pinball fits stay Adam)
+                                     # Levenberg-Marquardt on the GPU: csrc/hedge_lm.hip)
+    q99_optimizer: str = "adam"      # pinball (Q99) fits: "adam" | "lm" (IRLS Gauss-Newton in the same LM
+                                     # kernels: Gram weighted by 1 / (2 max(|r|, delta)), exact pinball loss
+                                     # for the accept test; two networks only - the shared Q1 net stays Adam)
+    lm_q_passes_first: int = 40      # pinball LM trial points, first date
+    lm_q_passes_rest: int = 4        # ... later dates
+    lm_q_delta: float = 1e-4         # IRLS weight floor, relative to the mean |terminal value|
+    lm_q_kappa: float = 3.0          # IRLS weight cap: |r| below lm_q_kappa x the mean |r| of its 64-path Gram
+                                     # tile counts as that (a near-zero residual would dominate the step)
+    lm_q_start: str = "mse"          # each pinball LM fit starts from: "mse" (the date's fitted MSE net, the
+                                     # reference's alternate training of one net, Q1) | "warm" (the previous
+                                     # date's Q99 net, Q18)
     lm_passes_first: int = 80        # LM trial points on the first date (from the random init)
     lm_passes_rest: int = 3          # LM trial points on later dates (warm start, Q18)
     lm_stop_tol: float = 0.0         # later dates: adaptive pass budget, lm_passes_rest = the cap; an accepted

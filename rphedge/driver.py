@@ -57,6 +57,12 @@ class InductionConfig:
     # pooled over all fitted dates, "date" = per-date mean/std
     feature_norm: str = "none"
     optimizer: str = "adam"              # MSE fits: adam | lm (engine.FitConfig.optimizer)
+    q99_optimizer: str = "adam"          # pinball fits (two networks): adam | lm (IRLS Gauss-Newton LM)
+    lm_q_passes_first: int = 40
+    lm_q_passes_rest: int = 4
+    lm_q_delta: float = 1e-4             # IRLS weight floor, relative to the mean |terminal value|
+    lm_q_kappa: float = 3.0              # IRLS weight cap relative to the Gram tile's mean |r|
+    lm_q_start: str = "mse"              # pinball LM start point: mse (the date's MSE net) | warm (Q18)
     lm_passes_first: int = 80
     lm_passes_rest: int = 3
     lm_stop_tol: float = 0.0             # later dates: adaptive LM pass budget (engine.FitConfig)
@@ -194,6 +200,18 @@ class BackwardInduction:
         self.lr_rest = geometric_lr_schedule(icfg.lr_rest or icfg.lr, icfg.epochs_rest, icfg.lr_decay) \
             if (icfg.lr_rest > 0 or icfg.lr_decay != 1.0) else None
         self.norms = feature_norms(paths, icfg.feature_norm, world)
+        # pinball LM fits: the IRLS floor in target units (one sync at build time)
+        self.q_lm = icfg.q99 and not icfg.shared_q99_model and str(icfg.q99_optimizer).lower() == "lm"
+        self.q_delta = 0.0
+        if self.q_lm:
+            vs = torch.stack([v_terminal.double().abs().sum(),
+                              torch.tensor(float(v_terminal.numel()), dtype=torch.float64, device=dev)])
+            if world > 1:
+                from .parallel import dist as D
+
+                D.all_reduce_(vs)
+            vs = vs.cpu().numpy()
+            self.q_delta = float(icfg.lm_q_delta) * float(vs[0] / max(vs[1], 1.0))
         # self-financing P&L scan inputs (device tables built once, outside any capture)
         nd, nin = self.n_dates, spec.nin
         fmu = np.zeros((nd, MAXIN), np.float32)
@@ -216,6 +234,13 @@ class BackwardInduction:
 
     def _fcfg(self, first: bool, loss: int, t: int | None = None) -> FitConfig:
         c = self.cfg
+        if loss == L.LOSS_PINBALL and self.q_lm:
+            # IRLS Gauss-Newton LM on the pinball loss (engine / hedge_lm.hip)
+            return FitConfig(epochs=c.lm_q_passes_first if first else c.lm_q_passes_rest, loss=loss,
+                             quantile=c.quantile, optimizer="lm", early_stopping=False,
+                             lm_lam0=(c.lm_lam0_first if (first and c.lm_lam0_first > 0) else None),
+                             lm_lam_carry=0.0 if first else c.lm_lam_carry, lm_q_delta=self.q_delta,
+                             lm_q_kappa=c.lm_q_kappa)
         if c.optimizer == "lm" and loss == L.LOSS_MSE:
             ms = first and (c.lm_starts > 1 or c.lm_explore_one)
             # the warm start was fitted at date t + 1 (its standardisation)
@@ -270,7 +295,8 @@ class BackwardInduction:
             f_m, f_q = self.fits[t]
             s_m, s_q = self.stats[t]
             join = None
-            if self.backend_q is not None:  # fork: Q99 fit on the side stream
+            q_from_mse = self.q_lm and str(c.lm_q_start).lower() == "mse"
+            if self.backend_q is not None and not q_from_mse:  # fork: Q99 fit on the side stream
                 main = torch.cuda.current_stream(self.values.device)
                 if self._side is None:
                     self._side = torch.cuda.Stream(self.values.device)
@@ -293,6 +319,8 @@ class BackwardInduction:
                 if join is not None:
                     torch.cuda.current_stream(self.values.device).wait_event(join)
                 else:
+                    if q_from_mse:
+                        self.w_q.copy_(self.w_mse)  # (the date's fitted MSE net: Q1's alternate training)
                     be.fit(self.w_q, self.opt_q, f_q, data, self._fcfg(first, L.LOSS_PINBALL),
                            seed=fit_seed(c.seed, t, 1), poll_every=c.poll_every)
                 be.eval(self.w_mse, data, s_q, wts_b=self.w_q, g_base=self.gbuf, blend_c=c.cost_of_capital,

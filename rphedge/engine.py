@@ -110,6 +110,11 @@ class FitConfig:
     lm_explore_passes: int = 0
     lm_explore_paths: int = 0
     lm_w0s: object = None
+    # pinball LM fits (loss = LOSS_PINBALL): IRLS Gram weights
+    # 1 / (2 max(|r|, delta)), delta = max(lm_q_delta, lm_q_kappa x the mean |r|
+    # of the path's 64-path Gram tile) (target units; lm_q_delta 0: 1e-6)
+    lm_q_delta: float = 0.0
+    lm_q_kappa: float = 3.0
 
     def key(self):
         return (self.epochs, self.patience if self.early_stopping else 1 << 30, self.restore_best,
@@ -150,9 +155,6 @@ class TrainConfig:
     # without it).  0 = plain Marquardt scaling (the presets: 1e-6 moved the
     # euro30 8-seed P&L 0.890 -> 0.897 in tools/lm_lab.py, 1e-9 changed nothing)
     lm_diag_floor: float = 0.0
-    # A/B of the LM pass body: the two largest weight-gradient outer products
-    # (W2, W3) on v_mfma_f32_16x16x4_f32 instead of the packed-fp32 VALU
-    lm_mfma_grad: bool = False
     # damping update: "simple" (x lam_down on accept, x lam_up on reject) or
     # "nielsen" (gain ratio rho of actual / predicted reduction: accept
     # x max(1/3, 1 - (2 rho - 1)^3), reject x nu with nu doubling)
@@ -637,7 +639,12 @@ class HipBackend:
     def lm_supported(self) -> bool:
         return self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head) is not None
 
-    def _lm_buffers(self):
+    def _lm_buffers(self, loss: int = L.LOSS_MSE):
+        """LM state, reduced block, slabs and descriptor of this backend's fits
+        of one loss (MSE and pinball fits keep separate states: each carries
+        its own damping across dates)."""
+        pin = int(loss) == L.LOSS_PINBALL
+
         def make():
             shp = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             if shp is None:
@@ -676,18 +683,17 @@ class HipBackend:
             lm.lam0, lm.lam_up, lm.lam_down = t.lm_lam0, t.lm_lam_up, t.lm_lam_down
             lm.lam_min, lm.lam_max, lm.ridge = t.lm_lam_min, t.lm_lam_max, t.lm_ridge
             lm.diag_floor = float(t.lm_diag_floor)
-            # A/B: W2 / W3 gradient outer products on the matrix cores (RPH_LM_MFMA_GRAD=1 overrides)
-            lm.mfma_grad = int(os.environ.get("RPH_LM_MFMA_GRAD", "1" if t.lm_mfma_grad else "0"))
-            lm.bias_index = _lm_bias_index(self.spec, t)
-            lm.out_n, lm.out_mu = _lm_out_n(self.spec, t), float(t.lm_out_mu)
+            # (pinball fits: no output-layer / bias Newton step - the loss is not quadratic)
+            lm.bias_index = -1 if pin else _lm_bias_index(self.spec, t)
+            lm.out_n, lm.out_mu = (0 if pin else _lm_out_n(self.spec, t)), float(t.lm_out_mu)
             lm.out_gram = 1 if lm.out_n > 0 else 0
             lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
             lm.gram_skip = int(os.environ.get("RPH_LM_GRAM_SKIP", t.lm_gram_skip))  # (env: tuning sweeps)
             bufs["desc"] = lm
             return bufs
-        return self._cache.get(("lm",), make)
+        return self._cache.get(("lm",) if not pin else ("lm", L.LOSS_PINBALL), make)
 
-    def _lm_gram_mode(self, lm, data: DateData) -> bool:
+    def _lm_gram_mode(self, lm, data: DateData, allow_side: bool = True) -> bool:
         """Set the Gram subsample of ``lm`` for a fit on ``data``; returns True
         when every rank builds the same Gram matrix (the exchange then carries
         only the gradient region).  One rank reads the subsample from its shard
@@ -695,7 +701,7 @@ class HipBackend:
         data parallel, the simulated subsample is required for the small exchange
         (without it: this rank's part of the subsample, Gram summed over ranks)."""
         g = self._lm_buffers()["gram"]
-        side = data.gram_feats is not None and data.gram_prices_next is not None
+        side = allow_side and data.gram_feats is not None and data.gram_prices_next is not None
         if side:
             gw, blk, stride, inv = g["side"]
             if data.gram_feats[0].numel() != gw * L.LM_TILE:
@@ -751,18 +757,26 @@ class HipBackend:
         stats | out-means] (2.1 KB) is all-reduced between reduce and solve
         (every rank builds the same Gram matrix from the simulated global
         subsample; without it the whole reduced block travels)."""
-        if fcfg.loss != L.LOSS_MSE:
-            raise ValueError("Levenberg-Marquardt fits minimise the MSE loss only")
-        b = self._lm_buffers()
+        pin = int(fcfg.loss) == L.LOSS_PINBALL
+        if int(fcfg.loss) not in (L.LOSS_MSE, L.LOSS_PINBALL):
+            raise ValueError(f"no Levenberg-Marquardt fit for loss {fcfg.loss}")
+        if pin and int(fcfg.lm_starts) >= 1 and int(fcfg.lm_explore_passes) > 0:
+            raise ValueError("pinball LM fits have no multi-start exploration")
+        b = self._lm_buffers(fcfg.loss)
         lm = b["desc"]
-        self._lm_same_gram = self._lm_gram_mode(lm, data)
+        # (pinball: the Gram weights need the targets of the subsample paths,
+        # which the simulated global subsample does not carry: shard subsample)
+        self._lm_same_gram = self._lm_gram_mode(lm, data, allow_side=not pin)
+        lm.q_delta = float(fcfg.lm_q_delta) if float(fcfg.lm_q_delta) > 0.0 else 1e-6
+        lm.q_kappa = float(fcfg.lm_q_kappa)
         lm.passes = int(fcfg.epochs)
         lm.stop_tol, lm.stop_min = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
         lm.lam0 = float(self.tcfg.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
         d = self._train_desc(wts, opt, fit, data, fcfg, 0, None)
         d.batch, d.steps_per_epoch, d.shuffle = self.n_local, 1, 0
         d.inv_batch = 1.0 / float(self.n_local * max(self.world, 1))
-        d.loss = L.LOSS_MSE
+        d.loss = int(fcfg.loss)
+        d.quantile = float(fcfg.quantile)
         n = self.native
         lm.lam_carry = float(fcfg.lm_lam_carry)
         lm.renorm = 0
@@ -1088,7 +1102,7 @@ class TorchBackend:
         self.batch_local, self.steps_per_epoch = _steps(self.n_local, tcfg, world)
         self.eval_wgs = 1
         self._order_cache = {}
-        self._lm_lam_last = 0.0  # the last LM fit's final damping (FitConfig.lm_lam_carry)
+        self._lm_lam_last = {}  # loss -> the last LM fit's final damping (FitConfig.lm_lam_carry)
 
     new_weights = HipBackend.new_weights
     new_opt = HipBackend.new_opt
@@ -1129,6 +1143,10 @@ class TorchBackend:
         spec, t = self.spec, self.tcfg
         P = spec.nparams
         dt = torch.float64
+        pin = int(fcfg.loss) == L.LOSS_PINBALL
+        q = float(np.float32(fcfg.quantile))
+        q_delta = float(np.float32(fcfg.lm_q_delta if float(fcfg.lm_q_delta) > 0.0 else 1e-6))
+        q_kappa = float(np.float32(fcfg.lm_q_kappa))
         X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)
         pr = torch.stack([p.to(dt) for p in data.prices_next] +
                          [torch.full_like(data.target, float(data.bond_next), dtype=dt)], dim=1)
@@ -1139,7 +1157,7 @@ class TorchBackend:
             return (torch_forward(spec, w, x[None])[0] * p).sum()
 
         side = None
-        if data.gram_feats is not None and data.gram_prices_next is not None:
+        if data.gram_feats is not None and data.gram_prices_next is not None and not pin:
             # the simulated global Gram subsample (identical on every rank)
             Xs = _normalise(torch.stack([f.to(dt) for f in data.gram_feats], dim=1), data)
             ps = torch.stack([p.to(dt) for p in data.gram_prices_next] +
@@ -1160,10 +1178,10 @@ class TorchBackend:
                 ns, blk, bstride = gram_subsample(n_loc * world, t.lm_gram_paths)
                 inv_ns = 1.0 / float(ns)
                 if side is not None:
-                    Xg, pg = side
+                    Xg, pg, yg = side[0], side[1], None
                 else:
                     sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
-                    Xg, pg = Xn[sub], prn[sub]
+                    Xg, pg, yg = Xn[sub], prn[sub], yn[sub]
             else:
                 nw = lm_pass_wgs(n_loc, lm_two_per_cu(spec))
                 ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // world, n_loc))
@@ -1172,14 +1190,31 @@ class TorchBackend:
                 inv_ns = 1.0 / float(ns * world)
                 blk, bstride = lm_gram_geometry(n_loc, ns, world)
                 sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
-                Xg, pg = Xn[sub], prn[sub]
+                Xg, pg, yg = Xn[sub], prn[sub], yn[sub]
 
             def evaluate(w):
                 wg = w.detach().clone().requires_grad_(True)
                 e = (torch_forward(spec, wg, Xn) * prn).sum(1) - yn
-                lsum = (e * e).sum()
-                (lsum / n_glob).backward()
+                if pin:
+                    # pinball loss of y - V (Replicating_Portfolio.py:138-145), its
+                    # subgradient (path_loss), the IRLS Gram weights of its
+                    # quadratic majoriser (k_lm_pass)
+                    ed = e.detach()
+                    pos = -q * ed >= (q - 1.0) * (-ed)
+                    lvec = torch.where(pos, -q * ed, (q - 1.0) * (-ed))
+                    lsum = lvec.sum()
+                    dV = torch.where(pos, torch.full_like(ed, -q), torch.full_like(ed, 1.0 - q))
+                    ((dV * (torch_forward(spec, wg, Xn) * prn).sum(1)).sum() / n_glob).backward()
+                else:
+                    lsum = (e * e).sum()
+                    (lsum / n_glob).backward()
                 J = vmap(jacrev(v_one), in_dims=(None, 0, 0))(w.detach(), Xg, pg)
+                if pin:
+                    rg = (torch_forward(spec, w.detach(), Xg) * pg).sum(1) - yg
+                    ra = rg.abs()
+                    # per 64-path tile: delta = max(q_delta, kappa x mean |r| of the tile)
+                    dl = torch.clamp_min(q_kappa * ra.view(-1, L.LM_TILE).mean(1, keepdim=True), q_delta)
+                    J = J * (0.5 / torch.sqrt(torch.maximum(ra.view(-1, L.LM_TILE), dl).reshape(-1)))[:, None]
                 G = (J.T @ J).reshape(-1) * inv_ns
                 rest = torch.cat([wg.grad.detach(),
                                   torch.stack([lsum.detach(), e.detach().abs().sum(),
@@ -1265,7 +1300,8 @@ class TorchBackend:
                     w_best[o["W1"] + f * spec.hidden + j] = f32(float(w32[o["W1"] + f * spec.hidden + j]) * r)
         lam = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
         if float(fcfg.lm_lam_carry) > 0.0:
-            lam = max(self._lm_lam_last * float(np.float32(fcfg.lm_lam_carry)), float(np.float32(t.lm_lam_min)))
+            lam = max(self._lm_lam_last.get(int(fcfg.loss), 0.0) * float(np.float32(fcfg.lm_lam_carry)),
+                      float(np.float32(t.lm_lam_min)))
         K = int(fcfg.lm_starts)
         if K >= 1 and int(fcfg.lm_explore_passes) > 0:
             # multi-start exploration (k_lm_select): rank-local fits on a path prefix
@@ -1291,9 +1327,9 @@ class TorchBackend:
         tol, kmin = float(fcfg.lm_stop_tol), max(1, int(fcfg.lm_stop_min))
         w_best, G, g, stb, Lb, lam, hist = run(w_best, make_eval(self.n_local, W, main=True), int(fcfg.epochs), lam,
                                                tol, kmin)
-        self._lm_lam_last = lam
-        bi = _lm_bias_index(spec, t)
-        n_out, out_ok = _lm_out_n(spec, t), False
+        self._lm_lam_last[int(fcfg.loss)] = lam
+        bi = -1 if pin else _lm_bias_index(spec, t)
+        n_out, out_ok = (0 if pin else _lm_out_n(spec, t)), False
 
         def out_step(wp, gp):
             """lm_out_newton at point wp (gradient gp): the full-batch output-layer
@@ -1386,8 +1422,8 @@ class TorchBackend:
         spec, dt = self.spec, self.dtype
         P = spec.nparams
         if fcfg.optimizer == "lm":
-            if fcfg.loss != L.LOSS_MSE:
-                raise ValueError("Levenberg-Marquardt fits minimise the MSE loss only")
+            if int(fcfg.loss) not in (L.LOSS_MSE, L.LOSS_PINBALL):
+                raise ValueError(f"no Levenberg-Marquardt fit for loss {fcfg.loss}")
             return self._lm_fit(wts, fit, data, fcfg)
         fit.copy_(fit_template(fcfg, self.device))
         X = _normalise(torch.stack([f.to(dt) for f in data.feats], dim=1), data)

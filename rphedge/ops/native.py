@@ -93,7 +93,7 @@ class LmDesc(C.Structure):
         ("renorm", C.c_int), ("pad1", C.c_int), ("ren_mu", C.c_float * MAXIN), ("ren_isd", C.c_float * MAXIN),
         ("out_n", C.c_int), ("out_mu", C.c_float), ("out_gram", C.c_int), ("pad3", C.c_int),
         ("slab_o", VP),
-        ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("mfma_grad", C.c_int),
+        ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("q_delta", C.c_float), ("q_kappa", C.c_float),
     ]
 
     def __init__(self, *a, **kw):

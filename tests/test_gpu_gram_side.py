@@ -81,45 +81,3 @@ def test_gram_only_workgroups_match_fp64(side):
     G_ref = (J.T @ J).numpy() / ns
     G = decode_gram(red, spec.nparams)
     assert np.linalg.norm(G - G_ref) / np.linalg.norm(G_ref) < 2e-5
-
-
-@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (1, 8, 1, 1), (3, 8, 2, 0)])
-@pytest.mark.parametrize("og", [False, True])
-def test_mfma_gradient_variant_matches_fp64(shape, og):
-    """A/B pass body (LmDesc.mfma_grad): the W2 / W3 gradient outer products
-    on v_mfma_f32_16x16x4_f32 - the packet's gradient vs fp64 autograd, and
-    equal to the VALU body's to fp32 rounding (with and without the output
-    Gram of the fit's last passes)."""
-    from rphedge.engine import FitConfig, HipBackend, TrainConfig
-    from rphedge.models.hedge_mlp import torch_forward
-    from rphedge.ops import layout as L
-
-    dev = torch.device("cuda", 0)
-    n = 1 << 15
-    spec, feats, pr, y, data, w0 = _setup(shape, n, dev)
-    reds = []
-    for mg in (0, 1):
-        be = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=4096, lm_out_fix=og), device=dev)
-        b = be._lm_buffers()
-        w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
-        d = be._train_desc(w, o, f, data, FitConfig(), 0, None)
-        d.batch, d.steps_per_epoch, d.shuffle, d.inv_batch = n, 1, 0, 1.0 / n
-        lm = b["desc"]
-        lm.passes, lm.mfma_grad = 1, mg
-        be.native.lm_eval(d, lm, b["red"], 0, None)  # (pass 0 of 1 is an output-Gram pass when og)
-        torch.cuda.synchronize()
-        reds.append(b["red"].cpu().numpy().copy())
-    P = spec.nparams
-    X = (torch.stack(feats, 1).double() - 0.1) * 1.5
-    if spec.head == L.HEAD_FREE:
-        Pm = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
-    else:
-        Pm = torch.stack([pr[0].double(), torch.full((n,), 1.01, dtype=torch.float64)], 1)
-    wt = torch.tensor(np.asarray(w0, np.float64), requires_grad=True)
-    e = (torch_forward(spec, wt, X) * Pm).sum(1) - y.double()
-    ((e * e).sum() / n).backward()
-    g_ref = wt.grad.numpy()
-    g_v, g_m = (r[L.LM_GBLK_MAX:L.LM_GBLK_MAX + P] for r in reds)
-    assert np.linalg.norm(g_m - g_ref) / np.linalg.norm(g_ref) < 2e-5
-    np.testing.assert_allclose(g_m, g_v, rtol=1e-4, atol=1e-6 * np.abs(g_ref).max())
-    np.testing.assert_array_equal(reds[0][:L.LM_GBLK_MAX], reds[1][:L.LM_GBLK_MAX])  # the Gram is untouched

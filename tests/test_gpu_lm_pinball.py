@@ -1,0 +1,144 @@
+"""Pinball (Q99) Levenberg-Marquardt fits on the GPU (csrc/hedge_lm.hip with
+TrainDesc.loss = LOSS_PINBALL): the reference's second fit per date
+(Replicating_Portfolio.py:138-145, :217) as IRLS Gauss-Newton steps - exact
+pinball loss and subgradient over every path, the Gram of the subsample
+weighted by 1 / (2 max(|r|, delta)) with delta = max(q_delta, q_kappa x the
+mean |r| of the 64-path tile).  Checked against the fp64 torch oracle
+(engine.TorchBackend._lm_fit): one pass's reduced block, a whole fit, and the
+corrected-mode pension API end to end with both fits on LM."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_lm import _setup, decode_gram
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (1, 8, 1, 1), (3, 8, 2, 0)])
+def test_lm_pinball_pass_block_matches_fp64(shape):
+    from torch.func import jacrev, vmap
+
+    from rphedge.engine import FitConfig, HipBackend, TrainConfig
+    from rphedge.models.hedge_mlp import torch_forward
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 15
+    q, q_delta, kappa = 0.99, 1e-5, 3.0
+    spec, feats, pr, y, data, w0 = _setup(shape, n, dev)
+    be = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=4096), device=dev)
+    b = be._lm_buffers(L.LOSS_PINBALL)
+    w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+    fc = FitConfig(loss=L.LOSS_PINBALL, quantile=q)
+    d = be._train_desc(w, o, f, data, fc, 0, None)
+    d.batch, d.steps_per_epoch, d.shuffle, d.inv_batch = n, 1, 0, 1.0 / n
+    d.loss, d.quantile = L.LOSS_PINBALL, q
+    lm = b["desc"]
+    be._lm_gram_mode(lm, data, allow_side=False)
+    lm.passes, lm.q_delta, lm.q_kappa = 1, q_delta, kappa
+    assert lm.out_n == 0 and lm.out_gram == 0 and lm.bias_index == -1
+    be.native.lm_eval(d, lm, b["red"], 0, None)
+    torch.cuda.synchronize()
+    red = b["red"].cpu().numpy()
+    P = spec.nparams
+    ns = lm.gram_wgs * 64
+    X = (torch.stack(feats, 1).double() - 0.1) * 1.5
+    Pm = torch.stack([p.double() for p in pr] + [torch.full((n,), 1.01, dtype=torch.float64)], 1)
+    wt = torch.tensor(np.asarray(w0, np.float64), requires_grad=True)
+    V = (torch_forward(spec, wt, X) * Pm).sum(1)
+    e = (y.double() - V).detach()
+    lvec = torch.maximum(q * e, (q - 1.0) * e)
+    dV = torch.where(q * e >= (q - 1.0) * e, torch.full_like(e, -q), torch.full_like(e, 1.0 - q))
+    ((dV * V).sum() / n).backward()
+    sub = torch.tensor([(j // lm.gram_blk) * lm.gram_blk_stride + j % lm.gram_blk for j in range(ns)])
+    J = vmap(jacrev(lambda ww, x, p: (torch_forward(spec, ww, x[None])[0] * p).sum()), in_dims=(None, 0, 0))(
+        wt.detach(), X[sub], Pm[sub])
+    ra = e[sub].abs()
+    dl = torch.clamp_min(kappa * ra.view(-1, 64).mean(1, keepdim=True), q_delta)
+    s = 0.5 / torch.sqrt(torch.maximum(ra.view(-1, 64), dl).reshape(-1))
+    Js = J * s[:, None]
+    G_ref = (Js.T @ Js).numpy() / ns
+    G = decode_gram(red, P)
+    assert np.linalg.norm(G - G_ref) / np.linalg.norm(G_ref) < 1e-4
+    g = red[L.LM_GBLK_MAX:L.LM_GBLK_MAX + P]
+    g_ref = wt.grad.numpy()
+    assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-4
+    st = red[L.LM_GBLK_MAX + L.LM_NPMAX:L.LM_GBLK_MAX + L.LM_NPMAX + 4]
+    assert st[0] == pytest.approx(float(lvec.sum()), rel=1e-5) and st[3] == n
+
+
+@pytest.mark.parametrize("shape", [(1, 8, 2, 0), (3, 8, 2, 0)])
+def test_lm_pinball_fit_matches_torch(shape):
+    """A pinball LM fit from an MSE-fitted start point: the best-so-far loss
+    sequence follows the fp64 oracle, no Cholesky failure, bitwise run to run,
+    and ~1 % of the targets end above the fitted quantile."""
+    from rphedge.engine import DateData, FitConfig, HipBackend, TorchBackend, TrainConfig, current_weights
+    from rphedge.ops import layout as L
+
+    dev = torch.device("cuda", 0)
+    n = 1 << 14
+    spec, feats, pr, y, data, w0 = _setup(shape, n, dev, seed=3)
+    y = y + 0.03 * torch.randn(n, generator=torch.Generator().manual_seed(7))
+    data.target = y.to(dev)
+    tc = TrainConfig(batch_size=n, lm_gram_paths=2048)
+    fm = FitConfig(epochs=20, optimizer="lm", early_stopping=False)
+    fq = FitConfig(epochs=12, optimizer="lm", loss=L.LOSS_PINBALL, quantile=0.99, early_stopping=False,
+                   lm_q_delta=1e-5)
+    outs = []
+    for _ in range(2):
+        be = HipBackend(spec, n, tc, device=dev)
+        w, o, f = be.new_weights(w0), be.new_opt(), be.new_fit()
+        be.fit(w, o, f, data, fm, seed=0)
+        be.fit(w, o, f, data, fq, seed=0)
+        torch.cuda.synchronize()
+        st = be._lm_buffers(L.LOSS_PINBALL)["state"].cpu().numpy()
+        outs.append((current_weights(spec, w), f.cpu().numpy(), int(st[L.LMS_FAIL])))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert outs[0][2] == 0
+    cd = DateData(feats=feats, prices_next=pr, bond_next=1.01, target=y, prices_now=pr, fmu=data.fmu, fisd=data.fisd)
+    tb = TorchBackend(spec, n, tc)
+    wc, oc, fcs = tb.new_weights(w0), tb.new_opt(), tb.new_fit()
+    tb.fit(wc, oc, fcs, cd, fm, seed=0)
+    tb.fit(wc, oc, fcs, cd, fq, seed=0)
+    hist_g = outs[0][1][L.F_HIST:L.F_HIST + 13]
+    hist_c = np.asarray(tb.lm_last["hist"])
+    np.testing.assert_allclose(np.minimum.accumulate(hist_g)[:6], np.minimum.accumulate(hist_c)[:6], rtol=5e-3)
+    assert min(hist_g) == pytest.approx(min(hist_c), rel=2e-2)
+    assert min(hist_g) < 0.7 * hist_g[0]
+    from rphedge.models.hedge_mlp import torch_forward
+
+    X = (torch.stack(feats, 1) - 0.1) * 1.5
+    Pm = torch.stack(pr + [torch.full((n,), 1.01)], 1)
+    V = (torch_forward(spec, torch.tensor(outs[0][0]), X) * Pm).sum(1)
+    above = float((y > V).double().mean())
+    assert 0.003 < above < 0.03, above
+
+
+def test_pension_both_fits_on_lm():
+    """Corrected-mode pension (two networks, RP-module parameters, 2^16 paths,
+    40 quarterly dates): MSE and Q99 fits both on LM.  Every pinball fit ends
+    with ~1 % of its targets above the fitted quantile (the Q99 sign condition
+    of "Single Time Step.ipynb":656-662 at the 99 % level), V0 sits between the
+    pure-MSE value and the Q99 one, and the run has no Cholesky failure."""
+    from rphedge import experiments
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+
+    p = experiments.mts_parameters()
+    p.update(n_paths=16, optimizer="lm", q99_optimizer="lm", lm_passes_first=40, lm_passes_rest=3,
+             lm_q_passes_first=30, lm_q_passes_rest=4, lm_lam_carry=3.0, verbose=False, device="cuda:0")
+    cfg = parse_params(p)
+    run = HedgeRun(cfg)
+    res = run.run()
+    torch.cuda.synchronize()
+    assert res.v0 == res.v0 and np.isfinite(res.phi) and np.isfinite(res.psi)
+    ind = res.induction
+    for dres in ind.dates:
+        assert dres.fit_q99 is not None and dres.fit_q99["best_loss"] == dres.fit_q99["best_loss"]
+    # the final date's Q99 hedge: fraction of paths whose next value exceeds it
+    st_q = run.backend._lm_buffers(1)["state"].cpu().numpy()
+    from rphedge.ops import layout as L
+
+    assert int(st_q[L.LMS_FAIL]) == 0
+    assert 0.5e6 < res.v0 < 1.5e6
