@@ -341,19 +341,19 @@ def lm_exchange_record(run, passes: int, world: int) -> dict:
 
 def multistart_record(run, a, world: int) -> dict:
     """First-date multi-start exploration: every candidate's final best loss on
-    its exploration prefix (all ranks), the pick, and the exploration's work
-    in full passes over the local paths."""
+    the global exploration prefix (every rank runs the same candidates), the
+    pick, and the exploration's work in full passes over the local paths."""
     from rphedge.ops import layout as L
 
     be = run.backend
     x = getattr(be, "lm_explore_last", None)
-    rec = {"starts": a.lm_starts * world, "explore_passes": a.lm_explore_passes}
-    nsub = min(run.n_local, 1 << a.lm_explore_log2)
-    rec["explore_paths_per_rank"] = nsub
+    rec = {"starts": a.lm_starts, "explore_passes": a.lm_explore_passes}
+    nsub = min(run.n_total, 1 << a.lm_explore_log2)
+    rec["explore_paths_global"] = nsub
     rec["full_pass_equivalents"] = a.lm_starts * (a.lm_explore_passes + 1) * nsub / run.n_local
-    if isinstance(x, dict) and "sel" in x:
-        sel = x["sel"].double().cpu().numpy()
-        losses = [float(sel[c * L.LM_SEL_W]) for c in range(a.lm_starts * world)]
+    if isinstance(x, dict) and "state" in x:
+        st = x["state"].double().cpu().numpy()
+        losses = [float(st[k, L.LMS_LFIN]) for k in range(a.lm_starts)]
     elif isinstance(x, dict):
         losses = [float(v) for v in x["losses"]]
     else:
@@ -492,8 +492,8 @@ def main(argv=None):
                    "lm_lam_carry": (a.lm_lam_carry or None) if lm else None,
                    "lm_renorm": bool(a.lm_renorm) if lm else None,
                    "lm_out_fix": bool(a.lm_out_fix) if lm else None,
-                   "lm_multistart": ({"starts_per_rank": a.lm_starts, "explore_passes": a.lm_explore_passes,
-                                      "explore_paths_per_rank": 1 << a.lm_explore_log2}
+                   "lm_multistart": ({"starts": a.lm_starts, "explore_passes": a.lm_explore_passes,
+                                      "explore_paths_global": 1 << a.lm_explore_log2}
                                      if (lm and (a.lm_starts > 1 or a.lm_explore_one)) else None),
                    "steps_per_epoch": None if lm else run.backend.steps_per_epoch, "graph": use_graph,
                    "backend": run.backend_kind,

@@ -789,7 +789,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
       publish(lam, spec_pred, (double)(sidx + 1));
     } else {  // not positive definite at this damping: as the serial solve's failure branch
       publish(fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max), pred_prev, (double)LM_SPEC);
-      if (tid == 0) st[LMS_FAIL] += 1.0;
+      if (tid == 0) {
+        st[LMS_FAIL] += 1.0;
+        st[LMS_FAILTOT] += 1.0;
+      }
     }
     return;
   }
@@ -912,7 +915,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     // more damping (trial := best)
     if (tid < P) st[LMS_W + (1 - best) * LM_NPMAX + tid] = wbest;
     publish(fmin(lam * lm.lam_up * lm.lam_up, (double)lm.lam_max), pred_prev, (double)LM_SPEC);
-    if (tid == 0) st[LMS_FAIL] += 1.0;
+    if (tid == 0) {
+      st[LMS_FAIL] += 1.0;
+      st[LMS_FAILTOT] += 1.0;
+    }
     return;
   }
   RPH_STAMPS(5);

@@ -205,6 +205,7 @@ enum LmState : int {
   LMS_NACC,                          // accepted steps of the current fit
   LMS_FAIL,                          // Cholesky failures (non-positive pivot)
   LMS_LFIN,                          // the fit's final best loss (written by the last solve)
+  LMS_FAILTOT,                       // Cholesky failures of every fit on this state (never reset)
   LMS_SPEC_LAM = LMS_FAIL + 8,       // [LM_SPEC] damping of precomputed reject-branch step m
   LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC,  // [LM_SPEC] its predicted reduction
   LMS_SPEC_OK = LMS_SPEC_PRED + LM_SPEC,   // [LM_SPEC] 1: positive definite (step valid)

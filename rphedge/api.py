@@ -88,6 +88,7 @@ class HedgeRun:
         self.spec = self._spec()
         self.paths = None
         self.gpaths = None  # LM Gram subsample paths (engine.gram_subsample), simulated on every rank
+        self.xpaths = None  # LM multi-start exploration: (global prefix paths, their terminal values)
         self.induction = None
         self.graph = None
 
@@ -133,18 +134,30 @@ class HedgeRun:
         vt_out = self.v_terminal if into is not None else None
         with self.timer.phase("simulate"):
             p = self._simulate_paths(self.n_local, self.offset, None, into)
-            if self.kind == "european":
-                v_t = P.payoff(c.option_type.lower(), p, c.K / c.Y, stream=self.stream, out=vt_out)
-            elif self.kind == "basket":
-                w = c.basket_weights or tuple([1.0 / c.n_assets] * c.n_assets)
-                v_t = P.payoff("basket_call", p, c.K / c.Y, weights=w, stream=self.stream, out=vt_out)
-            else:
-                v_t = P.payoff("guarantee", p, c.K, stream=self.stream, out=vt_out)
-            if str(c.train.optimizer).lower() == "lm":
-                ns, blk, stride = gram_subsample(self.n_total, c.train.lm_gram_paths)
+            v_t = self._payoff(p, vt_out)
+            tr = c.train
+            if str(tr.optimizer).lower() == "lm":
+                ns, blk, stride = gram_subsample(self.n_total, tr.lm_gram_paths)
                 self.gpaths = self._simulate_paths(ns, 0, (blk, stride), self.gpaths if into is not None else None)
+                if self.di.world > 1 and (int(tr.lm_starts) > 1 or bool(getattr(tr, "lm_explore_one", False))):
+                    # the multi-start exploration's global path prefix (every
+                    # rank explores the same starts on the same paths)
+                    nx = min(1 << int(tr.lm_explore_log2), self.n_total)
+                    xp = self._simulate_paths(nx, 0, None, self.xpaths[0] if into is not None else None)
+                    xv = self._payoff(xp, self.xpaths[1] if into is not None else None)
+                    self.xpaths = (xp, xv)
         self.paths, self.v_terminal = p, v_t
         return p, v_t
+
+    def _payoff(self, p: P.Paths, out=None) -> torch.Tensor:
+        """Terminal value V_T of paths ``p`` (K7; ``out``: into that buffer)."""
+        c = self.cfg
+        if self.kind == "european":
+            return P.payoff(c.option_type.lower(), p, c.K / c.Y, stream=self.stream, out=out)
+        if self.kind == "basket":
+            w = c.basket_weights or tuple([1.0 / c.n_assets] * c.n_assets)
+            return P.payoff("basket_call", p, c.K / c.Y, weights=w, stream=self.stream, out=out)
+        return P.payoff("guarantee", p, c.K, stream=self.stream, out=out)
 
     def _simulate_paths(self, n: int, offset: int, index_map, into: P.Paths | None) -> P.Paths:
         """One model's coarse-grid paths for ``n`` paths from global index
@@ -308,7 +321,7 @@ class HedgeRun:
                 backend_q = None
         self.induction = BackwardInduction(self.paths, self.v_terminal, self.spec, self.w0, self.backend, icfg,
                                            world=self.di.world, rank=self.di.rank, backend_q=backend_q,
-                                           gram_paths=self.gpaths)
+                                           gram_paths=self.gpaths, explore_paths=self.xpaths)
         return self
 
     # ------------------------------------------------------------------ run

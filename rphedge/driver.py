@@ -146,10 +146,14 @@ class BackwardInduction:
     """Owns device buffers for one run; ``enqueue()`` is graph-capturable."""
 
     def __init__(self, paths: Paths, v_terminal: torch.Tensor, spec: NetSpec, w0: np.ndarray, backend,
-                 icfg: InductionConfig, world: int = 1, rank: int = 0, backend_q=None, gram_paths: Paths | None = None):
+                 icfg: InductionConfig, world: int = 1, rank: int = 0, backend_q=None, gram_paths: Paths | None = None,
+                 explore_paths: tuple | None = None):
         self.paths, self.spec, self.backend, self.cfg = paths, spec, backend, icfg
         # LM fits: the global Gram subsample simulated on this rank (engine.gram_subsample)
         self.gram_paths = gram_paths
+        # LM multi-start exploration: (paths, terminal values) of the global path
+        # prefix simulated on this rank (None: the shard prefix is the global one)
+        self.explore_paths = explore_paths
         # independent-network model parallelism: with two networks (corrected
         # Q1 semantics) the pinball fit of a date does not depend on that date's
         # MSE fit, so it runs on its own backend (own buffers) on a side stream,
@@ -175,7 +179,8 @@ class BackwardInduction:
         self.w_init = backend.new_weights(w0)
         # multi-start start points of the first LM fit: candidate 0 = the run's
         # initial weights, the others the reference initialiser at seeds
-        # seed + 1000 c (same data-dependent output bias); every rank holds all
+        # seed + 1000 c (same data-dependent output bias); every rank runs all
+        # of them on the same global path prefix (the same set at every world size)
         self.lm_w0s = None
         if icfg.optimizer == "lm" and (icfg.lm_starts > 1 or icfg.lm_explore_one):
             from .models import hedge_mlp as hm
@@ -184,7 +189,7 @@ class BackwardInduction:
             rows = [np.asarray(w0, np.float32)] + [hm.init_weights(spec, b3, seed=icfg.seed + 1000 * c,
                                                                    spread=icfg.init_spread,
                                                                    shared_stream=icfg.init_shared_stream)
-                                                   for c in range(1, icfg.lm_starts * max(world, 1))]
+                                                   for c in range(1, icfg.lm_starts)]
             self.lm_w0s = np.stack(rows)
         self.opt_init = backend.new_opt()
         self.fits = [[backend.new_fit(), backend.new_fit()] for _ in range(self.n_dates)]
@@ -255,11 +260,23 @@ class BackwardInduction:
                              lm_starts=c.lm_starts if ms else 1,
                              lm_explore_passes=c.lm_explore_passes if ms else 0,
                              lm_explore_paths=(1 << int(c.lm_explore_log2)) if ms else 0,
-                             lm_w0s=self.lm_w0s if ms else None, lm_renorm=ren)
+                             lm_w0s=self.lm_w0s if ms else None, lm_renorm=ren,
+                             lm_explore_data=self.explore_data(t) if (ms and t is not None) else None)
         return FitConfig(epochs=c.epochs_first if first else c.epochs_rest,
                          patience=c.patience_first if first else c.patience_rest,
                          loss=loss, quantile=c.quantile, lr_schedule=self.lr_first if first else self.lr_rest,
                          restore_best=True, restore_at_end=c.restore_best_at_end, early_stopping=c.early_stopping)
+
+    def explore_data(self, t: int) -> DateData | None:
+        """The multi-start exploration's data at date t: the global path prefix
+        simulated on this rank (FitConfig.lm_explore_data), or None when the
+        shard prefix is the global one (one rank)."""
+        if self.explore_paths is None:
+            return None
+        xp, xv = self.explore_paths
+        mu, isd = self.norms[t] if self.norms else ((), ())
+        return DateData(feats=xp.features(t), prices_next=xp.prices(t + 1), bond_next=float(xp.bond[t + 1]),
+                        target=xv, prices_now=xp.prices(t), bond_now=float(xp.bond[t]), fmu=mu, fisd=isd)
 
     def date_data(self, t: int) -> DateData:
         p = self.paths

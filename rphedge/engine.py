@@ -96,12 +96,12 @@ class FitConfig:
     # > 0: the fit starts at the previous LM fit's final damping x lm_lam_carry
     # (later dates: a warm start's curvature scale is the last fit's)
     lm_lam_carry: float = 0.0
-    # multi-start exploration (first date): lm_starts fits per rank from the
-    # start points lm_w0s[rank * lm_starts + k] ([world x starts, P]; row 0 =
-    # the run's initial weights), lm_explore_passes trial points each on the
-    # first lm_explore_paths local paths (rank-local: no exchange), then every
-    # rank takes the candidate with the lowest final loss over all ranks and
-    # ``epochs`` polish passes on every path start there (at its damping)
+    # multi-start exploration (first date): lm_starts fits from the start
+    # points lm_w0s[k] ([starts, P]; row 0 = the run's initial weights),
+    # lm_explore_passes trial points each on the first lm_explore_paths global
+    # paths (lm_explore_data; every rank runs all of them on the same data),
+    # then the candidate with the lowest final loss is the start point of the
+    # ``epochs`` polish passes on every path (at its damping)
     # (mu, isd) of the inputs the start weights were fitted on (the previous
     # date): the first layer is re-expressed for this fit's standardisation, so
     # a warm start is the previous hedge as a function of the raw state
@@ -110,6 +110,11 @@ class FitConfig:
     lm_explore_passes: int = 0
     lm_explore_paths: int = 0
     lm_w0s: object = None
+    # the exploration's data: the first lm_explore_paths GLOBAL paths of the
+    # date (DateData, simulated on every rank; None: this rank's shard prefix,
+    # the global prefix on one rank) - every rank runs the same starts on the
+    # same paths, so the pick is the same at every world size with no exchange
+    lm_explore_data: object = None
     # pinball LM fits (loss = LOSS_PINBALL): IRLS Gram weights
     # 1 / (2 max(|r|, delta)), delta = max(lm_q_delta, lm_q_kappa x the mean |r|
     # of the path's 64-path Gram tile) (target units; lm_q_delta 0: 1e-6)
@@ -798,25 +803,30 @@ class HipBackend:
             n.lm_solve(d, lm, b["red"], k, self.stream)
 
     def lm_explore_paths(self, fcfg: FitConfig) -> int:
-        """Local paths of a multi-start exploration: a prefix of the shard, a
-        multiple of 256 (one pass workgroup per 256 paths)."""
-        want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else self.n_local
-        return int(max(256, min(self.n_local, want) // 256 * 256))
+        """Paths of a multi-start exploration: the global prefix (a multiple of
+        256: one pass workgroup per 256 paths)."""
+        have = int(fcfg.lm_explore_data.target.numel()) if fcfg.lm_explore_data is not None else self.n_local
+        want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else have
+        return int(max(256, min(have, want) // 256 * 256))
 
     def _lm_explore(self, d_main, fcfg: FitConfig):
         """Multi-start exploration of a first date (graph-capturable): K
         independent LM fits in ONE launch per kernel (grid y = instance) on the
-        first lm_explore_paths local paths, rank-local; k_lm_select packs the
-        candidates, the LM exchange all-gathers them (data parallel) and every
-        rank writes the same winner into the NetWeights and its damping into
-        the main LM state (the polish fit carries it)."""
+        global path prefix (FitConfig.lm_explore_data, or this rank's shard
+        prefix when it is the global one); k_lm_select writes the winner into
+        the NetWeights and its damping into the main LM state (the polish fit
+        carries it).  Every rank runs the same fits on the same paths: the
+        pick needs no exchange and does not depend on the world size."""
         b = self._lm_buffers()
         K = int(fcfg.lm_starts)
+        xd = fcfg.lm_explore_data
+        if self.world > 1 and xd is None:
+            raise ValueError("data-parallel multi-start exploration needs lm_explore_data (the global prefix)")
         nsub = self.lm_explore_paths(fcfg)
-        if K * max(self.world, 1) > L.LM_SEL_MAX:
-            raise ValueError(f"{K} starts x {self.world} ranks exceed the {L.LM_SEL_MAX} selection candidates")
-        if fcfg.lm_w0s is None or len(fcfg.lm_w0s) < K * max(self.world, 1):
-            raise ValueError("multi-start exploration needs lm_w0s (one start point per rank and instance)")
+        if K > L.LM_SEL_MAX:
+            raise ValueError(f"{K} starts exceed the {L.LM_SEL_MAX} selection candidates")
+        if fcfg.lm_w0s is None or len(fcfg.lm_w0s) < K:
+            raise ValueError("multi-start exploration needs lm_w0s (one start point per instance)")
         P = self.P
 
         def make():
@@ -825,7 +835,7 @@ class HipBackend:
             nw = lm_pass_wgs(nsub, bool(two))
             gw = int(max(1, min(max(L.LM_TILE, min(int(t.lm_gram_paths), nsub)) // L.LM_TILE, nw)))
             w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
-            rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)[self.rank * K:(self.rank + 1) * K, :P]
+            rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)[:K, :P]
             w0[:, :P] = torch.from_numpy(np.ascontiguousarray(rows))
             bufs = dict(state=torch.zeros(K, L.LMS_FLOATS, dtype=torch.float64, device=dev),
                         red=torch.zeros(K, L.LM_RED, dtype=torch.float64, device=dev),
@@ -836,7 +846,7 @@ class HipBackend:
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
             lm.w0 = bufs["w0"].data_ptr()
             lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
-            lm.out_n, lm.out_gram, lm.gram_side = 0, 0, 0  # (rank-local fits on a shard prefix)
+            lm.out_n, lm.out_gram, lm.gram_side = 0, 0, 0  # (the prefix's own Gram subsample)
             bufs["w0_rows"] = np.ascontiguousarray(rows).tobytes()
             lm.num_wgs, lm.gram_wgs = nw, gw
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
@@ -845,32 +855,36 @@ class HipBackend:
             return bufs
         x = self._cache.get(("lm_explore", K, nsub), make)
         # this call's start points: a cached buffer must not keep an earlier
-        # fit's candidates (a new set is uploaded; not inside a graph capture)
-        rows = np.ascontiguousarray(np.asarray(fcfg.lm_w0s, dtype=np.float32)[self.rank * K:(self.rank + 1) * K, :P])
+        # fit's candidates (a new set is uploaded on the backend's stream, after
+        # the work already queued there; not inside a graph capture)
+        rows = np.ascontiguousarray(np.asarray(fcfg.lm_w0s, dtype=np.float32)[:K, :P])
         if rows.tobytes() != x["w0_rows"]:
             if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("multi-start start points changed inside a graph capture")
             w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
             w0[:, :P] = torch.from_numpy(rows)
-            x["w0"].copy_(w0)
+            if self.device.type == "cuda" and self.stream is not None:
+                with torch.cuda.stream(self.stream):  # (the launches' stream: ordered after queued fits)
+                    x["w0"].copy_(w0)
+            else:
+                x["w0"].copy_(w0)
             x["w0_rows"] = rows.tobytes()
         lm = x["desc"]
         lm.passes = int(fcfg.lm_explore_passes)
         lm.lam0 = float(self.tcfg.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
         d = type(d_main).from_buffer_copy(d_main)
+        if xd is not None:
+            for i, f in enumerate(xd.feats):
+                d.feat[i] = f.data_ptr()
+            for i, p in enumerate(xd.prices_next):
+                d.price[i] = p.data_ptr()
+            d.target = xd.target.data_ptr()
         d.n_local = d.batch = nsub
         d.inv_batch = 1.0 / float(nsub)
-        n, W = self.native, max(self.world, 1)
+        n = self.native
         n.lm_fit(d, lm, x["red"], self.stream)
-        n.lm_select(d, lm, x["sel"], b["state"], W, self.rank, P, 0, self.stream)
-        if W > 1:
-            ng = W * K * L.LM_SEL_W
-            if self.lm_mailbox is not None:
-                xd = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
-                n.lm_dp_exchange(xd, x["sel"], ng, 1, self.stream)
-            else:
-                self._lm_comm().allreduce_(x["sel"][:ng], self.stream)
-        n.lm_select(d, lm, x["sel"], b["state"], W, self.rank, P, 1, self.stream)
+        n.lm_select(d, lm, x["sel"], b["state"], 1, 0, P, 0, self.stream)
+        n.lm_select(d, lm, x["sel"], b["state"], 1, 0, P, 1, self.stream)
         self.lm_explore_last = x
 
     def _lm_allreduce(self, red: torch.Tensor, gram: bool = True, og: bool = False):
@@ -971,7 +985,8 @@ class HipBackend:
     def lm_state(self) -> dict:
         """Host view of the last LM fit (accepted steps, Cholesky failures, damping)."""
         st = self._lm_buffers()["state"].cpu().numpy()
-        return {"accepted": int(st[L.LMS_NACC]), "chol_failures": int(st[L.LMS_FAIL]), "lam": float(st[L.LMS_LAM])}
+        return {"accepted": int(st[L.LMS_NACC]), "chol_failures": int(st[L.LMS_FAIL]), "lam": float(st[L.LMS_LAM]),
+                "chol_failures_total": int(st[L.LMS_FAILTOT])}
 
     def step_mode(self, poll_every: int = 0) -> str:
         """Resolve TrainConfig.step_mode for this backend (see TrainConfig)."""
@@ -1304,20 +1319,30 @@ class TorchBackend:
                       float(np.float32(t.lm_lam_min)))
         K = int(fcfg.lm_starts)
         if K >= 1 and int(fcfg.lm_explore_passes) > 0:
-            # multi-start exploration (k_lm_select): rank-local fits on a path prefix
-            want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else self.n_local
-            nsub = int(max(256, min(self.n_local, want) // 256 * 256))
+            # multi-start exploration (k_lm_select): the same K fits on every
+            # rank, on the global path prefix (FitConfig.lm_explore_data)
+            xd = fcfg.lm_explore_data
+            have = int(xd.target.numel()) if xd is not None else self.n_local
+            want = int(fcfg.lm_explore_paths) if int(fcfg.lm_explore_paths) > 0 else have
+            nsub = int(max(256, min(have, want) // 256 * 256))
+            if xd is not None:
+                Xs_ = _normalise(torch.stack([f.to(dt) for f in xd.feats], dim=1), data)
+                ps_ = torch.stack([p.to(dt) for p in xd.prices_next] +
+                                  [torch.full((Xs_.shape[0],), float(xd.bond_next), dtype=dt)], dim=1)
+                X_main, pr_main, y_main = X, pr, y
+                X, pr, y = Xs_, ps_, xd.target.to(dt)
+            elif self.world > 1:
+                raise ValueError("data-parallel multi-start exploration needs lm_explore_data (the global prefix)")
             ev = make_eval(nsub, 1)
             rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)
             lam_x = float(t.lm_lam0 if fcfg.lm_lam0 is None else fcfg.lm_lam0)
-            sel = torch.zeros(W * K, 2 + P, dtype=dt)
+            sel = torch.zeros(K, 2 + P, dtype=dt)
             for k in range(K):
-                c = self.rank * K + k
-                wk = torch.from_numpy(rows[c, :P].copy()).to(dt)
+                wk = torch.from_numpy(rows[k, :P].copy()).to(dt)
                 wb, _, _, _, lb, lk, _ = run(wk, ev, int(fcfg.lm_explore_passes), lam_x)
-                sel[c, 0], sel[c, 1], sel[c, 2:] = lb, lk, wb
-            if self.world > 1:
-                self._allreduce(sel)
+                sel[k, 0], sel[k, 1], sel[k, 2:] = lb, lk, wb
+            if xd is not None:
+                X, pr, y = X_main, pr_main, y_main
             ls = sel[:, 0].clone()
             ls[torch.isnan(ls)] = float("inf")
             pick = int(torch.argmin(ls))  # (first index of the minimum)

@@ -75,6 +75,7 @@ LMS_LAM = LMS_BEST + 1
 LMS_NACC = LMS_BEST + 2
 LMS_FAIL = LMS_BEST + 3
 LMS_LFIN = LMS_BEST + 4             # the fit's final best loss (last solve)
+LMS_FAILTOT = LMS_BEST + 5          # Cholesky failures of every fit on this state (never reset)
 LM_SEL_W = LM_NPMAX + 2             # multi-start selection block: [loss, damping, weights] per candidate
 LM_SEL_MAX = 64
 LM_DP_WGS = 16

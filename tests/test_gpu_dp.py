@@ -163,15 +163,20 @@ def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0
     data = DateData(feats=[f], prices_next=[p1], bond_next=1.0, target=y, prices_now=[f], **gk)
     w, o, fs = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
     fc = FitConfig(epochs=passes, optimizer="lm", early_stopping=False)
-    if starts:  # multi-start exploration: rank-local starts on a 2^12-path prefix, candidates all-gathered
+    if starts:  # multi-start exploration: the same starts on the global 2^12-path prefix on every rank
         fc.lm_starts, fc.lm_explore_passes, fc.lm_explore_paths = starts, 6, 1 << 12
-        fc.lm_w0s = _ms_starts(spec, starts * world)
+        fc.lm_w0s = _ms_starts(spec, starts)
+        fa, pa, ya = _data(n if n_total is None else n_total, dev)
+        ya = ya + 0.02 * torch.sin(9 * fa)
+        nx = 1 << 12
+        fc.lm_explore_data = DateData(feats=[fa[:nx].contiguous()], prices_next=[pa[:nx].contiguous()], bond_next=1.0,
+                                      target=ya[:nx].contiguous(), prices_now=[fa[:nx].contiguous()])
     be.fit(w, o, fs, data, fc, seed=3)
     torch.cuda.synchronize()
     if starts:
         from rphedge.ops import layout as L
-        sel = be.lm_explore_last["sel"].cpu().numpy()
-        return current_weights(spec, w), [float(sel[c * L.LM_SEL_W]) for c in range(starts * world)]
+        st = be.lm_explore_last["state"].cpu().numpy()
+        return current_weights(spec, w), [float(st[k, L.LMS_LFIN]) for k in range(starts)]
     return current_weights(spec, w), be.lm_state()
 
 
@@ -266,11 +271,10 @@ def _worker_ms(rank, world, port, n, passes, out):
 
 
 def test_lm_multistart_two_ranks_one_gpu():
-    """Multi-start exploration over 2 ranks: each rank explores its own 3
-    starts on its own prefix (no exchange), k_lm_select's block is all-gathered
-    through the LM mailbox (k_lm_dp_exchange) and both ranks polish the same
-    winner: bitwise-identical replicas and candidate lists; rank 0's
-    candidates are bitwise the 1-rank exploration of the same starts."""
+    """Multi-start exploration over 2 ranks: every rank explores the same 3
+    starts on the same global 2^12-path prefix (no exchange) and both polish
+    the same winner: bitwise-identical replicas, and the candidates' losses
+    are bitwise those of the 1-rank run over the same global paths."""
     n, passes, world = 1 << 15, 4, 2
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "w")
@@ -284,7 +288,7 @@ def test_lm_multistart_two_ranks_one_gpu():
             assert p.exitcode == 0
         w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
         l0, l1 = np.load(out + ".0.losses.npy"), np.load(out + ".1.losses.npy")
-    assert np.array_equal(w0, w1) and np.array_equal(l0, l1) and len(l0) == 6
-    # 1 rank, the same global paths [0, n): its prefix is rank 0's, its 3 starts rank 0's
-    _, l_ref = _lm_fit(0, 1, n // 2, passes, torch.device("cuda", 0), starts=3, n_total=n)
-    np.testing.assert_array_equal(l0[:3], np.asarray(l_ref))
+    assert np.array_equal(w0, w1) and np.array_equal(l0, l1) and len(l0) == 3
+    # 1 rank, the same global paths [0, n): the same exploration, bit for bit
+    _, l_ref = _lm_fit(0, 1, n, passes, torch.device("cuda", 0), starts=3)
+    np.testing.assert_array_equal(l0, np.asarray(l_ref))
