@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   // than 64 x the path grid: the subsample is the same at every world size)
   const bool path_wg = (int)blockIdx.x < lm.num_wgs;
   typename B::Pre pre;
-  const typename B::Sched sc = B::sched(d, lm.num_wgs, lm.gram_wgs, lm.gram_skip);
+  const typename B::Sched sc = B::sched(d, lm.num_wgs, lm.gram_wgs, lm.gram_skip, lm.leaf_blocks);
   if (path_wg) B::load(d, 0, perm, sc.b0 * 128, lane, pre);
   for (int i = tid; i < P; i += 256) {
     float w;
@@ -170,6 +170,10 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     }
   }
   if (pass > 0 && sl[LSS_STOP] != 0.0) return;  // adaptive budget spent: nothing to evaluate
+  // fused data-parallel exchange: this pass's reduce pushes and sums under the
+  // next sequence number (every rank evaluates the same passes)
+  if (lm.dp_fused && blockIdx.x == 0 && tid == 0)
+    __hip_atomic_fetch_add(lm.dp.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (pass == 0 && blockIdx.x == 0 && tid == 0) {
     sl[LSS_BEST] = 1.0;
     // (state[LMS_LAM] = the previous fit's final damping on this state)
@@ -312,6 +316,59 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
 }
 
 // ---------------------------------------------------------------------------
+// Fused data-parallel exchange (LmDesc.dp_fused), called by wave 0 of a
+// k_lm_reduce workgroup: lane l < n holds this rank's value v of gradient-
+// region entry e (offset from LM_GBLK_MAX).  Push to every peer's mailbox row
+// (slot, me) with system-scope stores, raise flag fi (system-scope release),
+// wait for every peer's flag fi of the same sequence number (bounded acquire
+// spin -> dp.error), return the fixed rank-order sum (every rank gets the
+// bitwise-identical value).  The sequence number is the exchange counter the
+// pass kernel advanced (graph replays never see stale flags).
+// ---------------------------------------------------------------------------
+RPH_INLINE double lm_dp_sum_wave(const LmDpDesc& x, const unsigned seq, const int fi, const double v, const int e,
+                                 const bool act) {
+  const int W = x.world, me = x.rank, lane = threadIdx.x & 63;
+  const int slot = (int)(seq % DP_SLOTS);
+  if (act)
+    for (int q = 0; q < W; ++q)
+      if (q != me)
+        __hip_atomic_store(x.mbox[q] + ((size_t)slot * W + me) * x.pitch + e, v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane < W && lane != me) {
+    unsigned* fo = reinterpret_cast<unsigned*>(x.mbox[lane] + ((size_t)slot * W + me) * x.pitch + LM_RED + fi);
+    __hip_atomic_store(fo, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // (after the wave's pushes)
+    const unsigned* fin =
+        reinterpret_cast<const unsigned*>(x.mbox[me] + ((size_t)slot * W + lane) * x.pitch + LM_RED + fi);
+    unsigned it = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++it & 255u) == 0u && (__builtin_amdgcn_s_memrealtime() - t0 > DP_SPIN_TICKS ||
+                                  __hip_atomic_load(x.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+        __hip_atomic_store(x.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // every lane: the peers' rows after their flags
+  // rank order, adjacent pairs first: ((r0 + r1) + (r2 + r3)) + ... - the top
+  // of the reduce's contiguous-halves tree over the leaves
+  double a[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    a[q] = q >= W ? 0.0
+                  : q == me ? v
+                            : (act ? __hip_atomic_load(x.mbox[me] + ((size_t)slot * W + q) * x.pitch + e,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                   : 0.0);
+#pragma unroll
+  for (int st = 1; st < 8; st <<= 1)
+#pragma unroll
+    for (int q = 0; q < 8; q += 2 * st) a[q] += a[q + st];
+  return a[0];
+}
+
+// ---------------------------------------------------------------------------
 // Reduce kernel: red[e] = fixed-order sums of the slabs.
 // ---------------------------------------------------------------------------
 // workgroups of the output-Gram part of k_lm_reduce (64 packed entries each)
@@ -325,6 +382,8 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
   __shared__ double part[1024];
   const int inst = blockIdx.y;  // multi-start instance
   if (pass > 0 && lm.state[(size_t)inst * LMS_FLOATS + LMS_SLOTS + LM_SLOT * (pass & 1) + LSS_STOP] != 0.0) return;
+  // fused data-parallel exchange: the sequence number the pass kernel advanced
+  const unsigned seq = lm.dp_fused ? __hip_atomic_load(lm.dp.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   red += (size_t)inst * LM_RED;
   const float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NG;
   const float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
@@ -354,25 +413,35 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       off = b * 1024 + ((ii & 3) + 4 * (ii >> 3)) * 64 + ((ii >> 2) & 1) * 32 + jj;
     }
     const float* const slab_o = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024 + off;
-    double s0 = 0.0, s1 = 0.0;
-    if (e < NPK) {
-      int w = g;
-      for (; w + 16 < lm.num_wgs; w += 32) {
-        s0 += (double)slab_o[(size_t)w * 3 * 1024];
-        s1 += (double)slab_o[(size_t)(w + 16) * 3 * 1024];
-      }
-      if (w < lm.num_wgs) s0 += (double)slab_o[(size_t)w * 3 * 1024];
-    }
-    part[tid] = s0 + s1;
-    __syncthreads();
-    if (g == 0 && e < NPK) {
-      double a = 0.0, bb = 0.0;
+    // rows [16 g, 16 g + 16) by a pairwise tree, then the 16 groups by a
+    // pairwise tree: a contiguous-halves tree over the (<= 256) rows
+    double r[16];
 #pragma unroll
-      for (int q = 0; q < 16; q += 2) {
-        a += part[q * 64 + l];
-        bb += part[(q + 1) * 64 + l];
+    for (int u = 0; u < 16; ++u) {
+      const int w = 16 * g + u;
+      r[u] = (e < NPK && w < lm.num_wgs) ? (double)slab_o[(size_t)w * 3 * 1024] : 0.0;
+    }
+#pragma unroll
+    for (int st = 1; st < 16; st <<= 1)
+#pragma unroll
+      for (int u = 0; u < 16; u += 2 * st) r[u] += r[u + st];
+    part[tid] = r[0];
+    __syncthreads();
+    if (g == 0) {
+      double v = 0.0;
+      if (e < NPK) {
+        double c[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) c[q] = part[q * 64 + l];
+#pragma unroll
+        for (int st = 1; st < 16; st <<= 1)
+#pragma unroll
+          for (int q = 0; q < 16; q += 2 * st) c[q] += c[q + st];
+        v = c[0] * (double)lm.inv_n;
       }
-      red[LM_RED_OUTG + e] = (a + bb) * (double)lm.inv_n;
+      if (lm.dp_fused)
+        v = lm_dp_sum_wave(lm.dp, seq, R / 4 + ob, v, LM_RED_OUTG - LM_GBLK_MAX + e, e < NPK);
+      if (e < NPK) red[LM_RED_OUTG + e] = v;
     }
     return;
   }
@@ -417,30 +486,29 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     return;
   }
   // gradient packet: workgroup pw handles entries [4 pw, 4 pw + 4); thread
-  // (grp, k) sums rows grp, grp + 256, ... of entry 4 pw + k (one row per
-  // thread at 256 pass workgroups), then a fixed-order LDS tree over the 256
-  // row groups
+  // (grp, k) loads row bitrev8(grp) (<= 256 pass workgroups) of entry 4 pw + k,
+  // and the LDS tree below combines grp with grp + st: rows 2m and 2m + 1
+  // first - a contiguous-halves tree over the rows, so a rank's rows (a
+  // contiguous run of leaves, LmDesc.leaf_blocks) form a complete subtree and
+  // the sum over the ranks (lm_dp_sum_wave) finishes the same tree
   const int pw = blockIdx.x - NG / 64;
   const int k = tid & 3, grp = tid >> 2;
   const int i = pw * 4 + k;
-  double s0 = 0.0, s1 = 0.0;
-  int w = grp;
-  for (; w + 256 < lm.num_wgs; w += 512) {
-    s0 += (double)slab_b[(size_t)w * R + i];
-    s1 += (double)slab_b[(size_t)(w + 256) * R + i];
-  }
-  if (w < lm.num_wgs) s0 += (double)slab_b[(size_t)w * R + i];
-  part[tid] = s0 + s1;
+  const int row = (int)(__builtin_bitreverse32((unsigned)grp) >> 24);
+  part[tid] = row < lm.num_wgs ? (double)slab_b[(size_t)row * R + i] : 0.0;
   __syncthreads();
 #pragma unroll
   for (int st = 128; st >= 1; st >>= 1) {
     if (grp < st) part[tid] += part[tid + 4 * st];
     __syncthreads();
   }
-  if (tid < 4) {
-    const double v = part[tid];
-    if (i < P) red[LM_GBLK_MAX + i] = v;
-    else if (i < P + 4) red[LM_GBLK_MAX + LM_NPMAX + i - P] = v;
+  if (tid < 64) {
+    // entry i of the gradient region: g (i < P) or the packet statistics
+    const int e = i < P ? i : LM_NPMAX + i - P;
+    const bool act = tid < 4 && i < P + 4;
+    double v = tid < 4 ? part[tid] : 0.0;
+    if (lm.dp_fused) v = lm_dp_sum_wave(lm.dp, seq, pw, v, e, act);
+    if (act) red[LM_GBLK_MAX + e] = v;
   }
 }
 
@@ -950,8 +1018,10 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (int rc = validate_train(d, 3 /* no schedule buffers */, "rph_lm")) return rc;
   if (!lm->state || !lm->slab_b || !lm->slab_g) return rph_report("rph_lm", "null LM buffer");
   if (d->batch != d->n_local || d->steps_per_epoch != 1) return rph_report("rph_lm", "LM fits are full batch");
-  if (lm->num_wgs < 1 || lm->num_wgs > 65535 || lm->passes < 0 || lm->passes >= MAXHIST)
-    return rph_report("rph_lm", "bad num_wgs / passes");
+  if (lm->num_wgs < 1 || lm->num_wgs > 256 || lm->passes < 0 || lm->passes >= MAXHIST)
+    return rph_report("rph_lm", "bad num_wgs (1..256) / passes");
+  if (lm->leaf_blocks < 0 || (lm->leaf_blocks > 0 && (long long)lm->leaf_blocks * 128 * 4 * lm->num_wgs < d->batch))
+    return rph_report("rph_lm", "leaf_blocks: the waves' leaves must cover the shard");
   if (lm->gram_wgs < 1 || lm->gram_wgs > 65535) return rph_report("rph_lm", "bad Gram workgroup count");
   if (lm->gram_side) {
     // the subsample comes from gfeat / gprice ([gram_wgs x 64] each)
@@ -977,6 +1047,16 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   if (lm->inst < 1 || lm->inst > LM_SEL_MAX) return rph_report("rph_lm", "bad instance count");
   if (lm->inst > 1 && !lm->explore) return rph_report("rph_lm", "several instances are exploration fits only");
+  if (lm->dp_fused) {
+    const int nflags = R / 4 + lm_og_wgs(nu);
+    if (!lm->gram_side || lm->inst != 1 || lm->explore || lm->weights_only)
+      return rph_report("rph_lm", "fused DP exchange: one main fit on the shared Gram subsample only");
+    if (lm->dp.world < 2 || lm->dp.world > 8 || lm->dp.rank < 0 || lm->dp.rank >= lm->dp.world ||
+        lm->dp.pitch < LM_DP_PITCH || !lm->dp.counter || !lm->dp.error || nflags > LM_DP_FLAGS)
+      return rph_report("rph_lm", "fused DP exchange: bad mailbox descriptor");
+    for (int q = 0; q < lm->dp.world; ++q)
+      if (!lm->dp.mbox[q]) return rph_report("rph_lm", "fused DP exchange: null peer mailbox");
+  }
   if (lm->explore && lm->weights_only) return rph_report("rph_lm", "exploration fits publish nothing");
   (void)P;
   return 0;

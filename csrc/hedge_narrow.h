@@ -248,9 +248,13 @@ struct NarrowPairBody {
     long long b0, bstep, bend;
   };
   // (num_wgs: the path workgroups; a pass grid may carry Gram-only workgroups beyond them)
-  RPH_INLINE static Sched sched(const TrainDesc& d, int num_wgs, int gram_wgs, int gram_skip) {
+  RPH_INLINE static Sched sched(const TrainDesc& d, int num_wgs, int gram_wgs, int gram_skip, int leaf_blocks = 0) {
     const long long nblk = (d.batch + 127) / 128;
     const int TW = num_wgs * 4, w = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (leaf_blocks > 0) {  // contiguous leaves (LmDesc.leaf_blocks)
+      const long long b0 = (long long)w * leaf_blocks, b1 = b0 + leaf_blocks;
+      return {b0, 1, b1 < nblk ? b1 : nblk};
+    }
     const int GW = (gram_wgs < num_wgs ? gram_wgs : num_wgs) * 4;
     const long long per = nblk / TW;
     if (gram_skip <= 0 || GW >= TW || per <= 0) return {w, TW, nblk};

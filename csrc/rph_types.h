@@ -229,6 +229,25 @@ enum LmSlot : int {
   LSS_STOP,        // > 0: the fit stopped at the solve of this pass (adaptive budget)
 };
 
+// Data-parallel exchange of the LM reduced block over IPC-mapped peer
+// mailboxes (k_lm_dp_exchange): LM_DP_WGS workgroups, each owning a chunk of
+// the block; per (slot, sender) row `pitch` 8-byte entries = LM_RED data +
+// LM_DP_WGS per-workgroup flags.
+constexpr int LM_DP_WGS = 16;
+// fused exchange (LmDesc.dp_fused): k_lm_reduce's gradient-packet and
+// output-Gram workgroups push their entries of the gradient region themselves,
+// each with its own flag (<= LM_DP_FLAGS of them) after the LM_RED data entries
+constexpr int LM_DP_FLAGS = 128;
+constexpr int LM_DP_PITCH = LM_RED + LM_DP_FLAGS;  // mailbox row pitch (8-byte entries)
+struct LmDpDesc {
+  double* mbox[8];               // every rank's mailbox [DP_SLOTS][world][pitch] (own = mbox[rank])
+  unsigned* counter;             // [0] exchanges completed by this rank, [1] workgroup arrival ticket
+  unsigned* error;               // [0] set on a peer timeout
+  int world, rank;
+  int pitch;                     // entries per (slot, sender) row (>= LM_DP_PITCH)
+  int pad0;
+};
+
 struct LmDesc {
   double* state;                 // [LMS_FLOATS]
   float* slab_b;                 // [num_wgs][R] per-workgroup gradient packets
@@ -306,6 +325,21 @@ struct LmDesc {
   // the path's 64-path Gram tile) (target units)
   float q_delta;
   float q_kappa;
+  // data parallel, every rank building the same Gram (gram_side): the
+  // gradient region [g | stats | output Gram] is summed over the ranks INSIDE
+  // k_lm_reduce (its packet / output-Gram workgroups push to the peers'
+  // mailboxes, raise one flag each, wait for the peers' same flag and sum in
+  // rank order; the pass kernel advances the exchange counter): no extra
+  // launch per pass.  0: single rank, or the separate exchange kernels
+  LmDpDesc dp;
+  int dp_fused;
+  // > 0: wave w of the pass grid takes the contiguous path blocks
+  // [w leaf_blocks, (w + 1) leaf_blocks) (128 paths each; gram_skip unused):
+  // the per-wave partial sums are then the same "leaves" of the global path
+  // range at every world size (a rank's shard is a contiguous run of whole
+  // leaves), and with the reduce's contiguous-halves trees the summed
+  // gradient is bitwise independent of the world size.  0: cyclic blocks
+  int leaf_blocks;
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)
@@ -315,19 +349,6 @@ struct LmDesc {
 constexpr int LM_SEL_W = LM_NPMAX + 2;
 constexpr int LM_SEL_MAX = 64;          // candidates (world x instances)
 
-// Data-parallel exchange of the LM reduced block over IPC-mapped peer
-// mailboxes (k_lm_dp_exchange): LM_DP_WGS workgroups, each owning a chunk of
-// the block; per (slot, sender) row `pitch` 8-byte entries = LM_RED data +
-// LM_DP_WGS per-workgroup flags.
-constexpr int LM_DP_WGS = 16;
-struct LmDpDesc {
-  double* mbox[8];               // every rank's mailbox [DP_SLOTS][world][pitch] (own = mbox[rank])
-  unsigned* counter;             // [0] exchanges completed by this rank, [1] workgroup arrival ticket
-  unsigned* error;               // [0] set on a peer timeout
-  int world, rank;
-  int pitch;                     // entries per (slot, sender) row (>= LM_RED + LM_DP_WGS)
-  int pad0;
-};
 
 // Eval stats slab columns
 enum EvalStat : int {

@@ -274,7 +274,7 @@ class HedgeRun:
             kw["mailbox"] = self.mailbox
             # LM fits / mean refits: the reduced [G | g | stats] block travels
             # over its own mailbox (k_lm_dp_exchange) with the xGMI transport
-            self.lm_mailbox = D.make_mailbox(self.di, L.LM_RED + L.LM_DP_WGS, tag="rph_lmbox",
+            self.lm_mailbox = D.make_mailbox(self.di, L.LM_DP_PITCH, tag="rph_lmbox",
                                              mode=self.di.lm_dp_mode)
             kw["lm_mailbox"] = self.lm_mailbox
             kw["lm_comm"] = self.di.lm_comm

@@ -168,9 +168,17 @@ class TrainConfig:
     # (free heads), so the fitted values' mean over all paths equals the
     # target's and no mean error drifts down the backward induction
     lm_bias_fix: bool = True
-    # pass kernel load balance: the Gram workgroups' waves take this many
-    # 128-path blocks fewer than an even split (their Gram tile follows)
+    # pass kernel load balance (cyclic schedule only, lm_leaf_paths < 0): the
+    # Gram workgroups' waves take this many 128-path blocks fewer than an even
+    # split (their Gram tile follows)
     lm_gram_skip: int = 3
+    # pass kernel schedule: every wave sums one contiguous "leaf" of paths
+    # (LmDesc.leaf_blocks): 0 = auto (the shard over 4 x the pass workgroups),
+    # > 0 = this many paths per leaf (a multiple of 128: the same leaves at
+    # every world size over the same global paths - the strong-scaling
+    # rehearsal reproduces the one-rank fit bit for bit), < 0 = the cyclic
+    # block schedule with lm_gram_skip
+    lm_leaf_paths: int = 0
     # after the last pass: exact Newton step on the whole output layer (the
     # value is linear in it; 2 G_oo d = -g_o), subsuming the bias step
     lm_out_fix: bool = False
@@ -296,6 +304,27 @@ def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
 
 
 LM_PAIR_WPS = 1  # csrc/hedge_lm.hip RPH_LM_PAIR_WPS default (one pass workgroup per CU)
+
+
+def lm_pass_schedule(n_local: int, leaf_paths: int = 0) -> tuple[int, int]:
+    """(pass workgroups, leaf blocks) of an LM pass over ``n_local`` paths
+    (TrainConfig.lm_leaf_paths): auto (0) = lm_pass_wgs workgroups, the shard
+    split into 4 x that many contiguous leaves; > 0 = leaves of that many
+    paths (the workgroups to cover them, at most 256); < 0 = the cyclic
+    schedule (leaf 0)."""
+    nw = lm_pass_wgs(n_local, False)
+    nblk = (int(n_local) + 127) // 128
+    if leaf_paths < 0:
+        return nw, 0
+    if leaf_paths > 0:
+        if leaf_paths % 128:
+            raise ValueError(f"lm_leaf_paths must be a multiple of 128, got {leaf_paths}")
+        lb = leaf_paths // 128
+        nw = int(min(256, max(1, -(-nblk // (4 * lb)))))
+        if 4 * nw * lb < nblk:
+            raise ValueError(f"{leaf_paths}-path leaves need more than 256 pass workgroups for {n_local} paths")
+        return nw, lb
+    return nw, int(-(-nblk // (4 * nw)))
 
 
 def lm_tpack_len(P: int, nblk: int) -> int:
@@ -461,7 +490,7 @@ class HipBackend:
         from .ops import native
 
         self.mailbox = mailbox  # native.IpcMailbox: fused xGMI all-reduce inside the step kernel
-        self.lm_mailbox = lm_mailbox  # native.IpcMailbox (LM_RED + LM_DP_WGS pitch): LM block exchange
+        self.lm_mailbox = lm_mailbox  # native.IpcMailbox (LM_DP_PITCH pitch): LM block exchange
         self._lm_nccl = lm_comm       # RCCL communicator of the LM block when its xGMI probe failed
         self.native = native
         native.load(required=True)
@@ -656,7 +685,7 @@ class HipBackend:
                 raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets up to 174 parameters)")
             P, R, nblk, two = shp
             t = self.tcfg
-            nw = lm_pass_wgs(self.n_local, bool(two))
+            nw, leaf = lm_pass_schedule(self.n_local, int(t.lm_leaf_paths))
             W = max(self.world, 1)
             # the global Gram subsample (every rank: gw = ns / 64 Gram workgroups,
             # past the path grid where it is larger)
@@ -694,6 +723,7 @@ class HipBackend:
             lm.out_gram = 1 if lm.out_n > 0 else 0
             lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
             lm.gram_skip = int(os.environ.get("RPH_LM_GRAM_SKIP", t.lm_gram_skip))  # (env: tuning sweeps)
+            lm.leaf_blocks = leaf
             bufs["desc"] = lm
             return bufs
         return self._cache.get(("lm",) if not pin else ("lm", L.LOSS_PINBALL), make)
@@ -793,7 +823,14 @@ class HipBackend:
         if int(fcfg.lm_starts) >= 1 and int(fcfg.lm_explore_passes) > 0:
             self._lm_explore(d, fcfg)
             lm.lam_carry = 1.0  # the polish starts at the chosen exploration's damping
-        if self.world <= 1 and not self.tcfg.lm_split:
+        # data parallel on the shared Gram subsample with the xGMI mailbox: the
+        # gradient region is summed inside k_lm_reduce (no extra launch per pass)
+        fused = (self.world > 1 and self.lm_mailbox is not None and self._lm_same_gram and not pin
+                 and not self.tcfg.lm_split)
+        lm.dp_fused = 1 if fused else 0
+        if fused:
+            lm.dp = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
+        if (self.world <= 1 or fused) and not self.tcfg.lm_split:
             n.lm_fit(d, lm, b["red"], self.stream)
             return
         for k in range(lm.passes + 1):
@@ -832,7 +869,7 @@ class HipBackend:
         def make():
             _, R, nblk, two = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             t, dev = self.tcfg, self.device
-            nw = lm_pass_wgs(nsub, bool(two))
+            nw, leaf = lm_pass_schedule(nsub, 0 if int(t.lm_leaf_paths) >= 0 else -1)
             gw = int(max(1, min(max(L.LM_TILE, min(int(t.lm_gram_paths), nsub)) // L.LM_TILE, nw)))
             w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
             rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)[:K, :P]
@@ -846,9 +883,9 @@ class HipBackend:
             lm.state, lm.slab_b, lm.slab_g = (bufs[k].data_ptr() for k in ("state", "slab_b", "slab_g"))
             lm.w0 = bufs["w0"].data_ptr()
             lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
-            lm.out_n, lm.out_gram, lm.gram_side = 0, 0, 0  # (the prefix's own Gram subsample)
+            lm.out_n, lm.out_gram, lm.gram_side, lm.dp_fused = 0, 0, 0, 0  # (the prefix's own Gram subsample)
             bufs["w0_rows"] = np.ascontiguousarray(rows).tobytes()
-            lm.num_wgs, lm.gram_wgs = nw, gw
+            lm.num_wgs, lm.gram_wgs, lm.leaf_blocks = nw, gw, leaf
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
             lm.inv_ns, lm.inv_n = 1.0 / float(gw * L.LM_TILE), 1.0 / float(nsub)
             bufs["desc"] = lm
@@ -947,7 +984,7 @@ class HipBackend:
             src = b["desc"]
             lm = type(src).from_buffer_copy(src)
             lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol, lm.out_n, lm.out_gram = 0, 1, 1, 0.0, 0, 0
-            lm.renorm, lm.lam_carry, lm.gram_side = 0, 0.0, 0  # (not inherited from the main fit's desc)
+            lm.renorm, lm.lam_carry, lm.gram_side, lm.dp_fused = 0, 0.0, 0, 0  # (not inherited from the main fit's desc)
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
             return lm

@@ -79,6 +79,8 @@ LMS_FAILTOT = LMS_BEST + 5          # Cholesky failures of every fit on this sta
 LM_SEL_W = LM_NPMAX + 2             # multi-start selection block: [loss, damping, weights] per candidate
 LM_SEL_MAX = 64
 LM_DP_WGS = 16
+LM_DP_FLAGS = 128                   # fused exchange: per-workgroup flags after the LM_RED data entries
+LM_DP_PITCH = LM_RED + LM_DP_FLAGS  # LM mailbox row pitch
 LM_SPEC = 4
 LMS_SPEC_LAM = LMS_FAIL + 8
 LMS_SPEC_PRED = LMS_SPEC_LAM + LM_SPEC

@@ -81,6 +81,13 @@ class PnlDesc(C.Structure):
     ]
 
 
+class LmDpDesc(C.Structure):
+    _fields_ = [
+        ("mbox", VP * 8), ("counter", VP), ("error", VP),
+        ("world", C.c_int), ("rank", C.c_int), ("pitch", C.c_int), ("pad0", C.c_int),
+    ]
+
+
 class LmDesc(C.Structure):
     _fields_ = [
         ("state", VP), ("slab_b", VP), ("slab_g", VP),
@@ -94,18 +101,12 @@ class LmDesc(C.Structure):
         ("out_n", C.c_int), ("out_mu", C.c_float), ("out_gram", C.c_int), ("pad3", C.c_int),
         ("slab_o", VP),
         ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("q_delta", C.c_float), ("q_kappa", C.c_float),
+        ("dp", LmDpDesc), ("dp_fused", C.c_int), ("pad4", C.c_int),
     ]
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
         self.inst = 1  # one fit per launch unless a multi-start exploration sets more
-
-
-class LmDpDesc(C.Structure):
-    _fields_ = [
-        ("mbox", VP * 8), ("counter", VP), ("error", VP),
-        ("world", C.c_int), ("rank", C.c_int), ("pitch", C.c_int), ("pad0", C.c_int),
-    ]
 
 
 class SimDesc(C.Structure):
@@ -150,7 +151,8 @@ def _expected_layout() -> list[int]:
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
         LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, LmDesc.renorm.offset,
         LmDesc.ren_isd.offset, LmDesc.out_n.offset, LmDesc.gfeat.offset, LmDesc.gprice.offset,
-        LmDesc.gram_side.offset, C.sizeof(LmDesc), L.LMS_LFIN, L.LM_SEL_W,
+        LmDesc.gram_side.offset, LmDesc.q_delta.offset, LmDesc.dp.offset, LmDesc.dp_fused.offset, C.sizeof(LmDesc),
+        L.LMS_LFIN, L.LMS_FAILTOT, L.LM_SEL_W, L.LM_DP_PITCH,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
         L.LM_SPEC, L.LMS_SPEC_W, L.LMS_SLOTS, L.LM_SLOT, L.LSS_LBEST, L.LSS_STOP,
@@ -529,8 +531,9 @@ class IpcMailbox:
         d.dp_error = self.error.data_ptr()
 
     def lm_desc(self) -> "LmDpDesc":
-        """Descriptor of this mailbox for the LM block exchange (k_lm_dp_exchange;
-        allocated with R >= LM_RED + LM_DP_WGS entries per row)."""
+        """Descriptor of this mailbox for the LM block exchange (k_lm_dp_exchange,
+        and the exchange fused into k_lm_reduce; allocated with R >= LM_DP_PITCH
+        entries per row)."""
         x = LmDpDesc()
         for q in range(self.world):
             x.mbox[q] = self.ptrs[q]

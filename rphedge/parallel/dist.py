@@ -224,7 +224,7 @@ def select_transport(info: DistInfo) -> str:
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
     mb = try_mailbox(spec.red_width, "rph_probe")
-    lmb = try_mailbox(L.LM_RED + L.LM_DP_WGS, "rph_probe_lm")
+    lmb = try_mailbox(L.LM_DP_PITCH, "rph_probe_lm")
     probe = {}
     for name, lm in (("packet", False), ("lm", True)):
         ok_l, wv = _probe_xgmi_local(info, mb, lmb, lm)

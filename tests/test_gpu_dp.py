@@ -143,7 +143,8 @@ def _ms_starts(spec, k):
     return np.stack([init_weights(spec, [0.5, 0.0], seed=1234 + 1000 * c) for c in range(k)])
 
 
-def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0, n_total=None, side=False):
+def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0, n_total=None, side=False,
+            leaf=0, out_fix=False):
     from rphedge.engine import DateData, FitConfig, HipBackend, TrainConfig, current_weights, gram_subsample
     from rphedge.models.hedge_mlp import NetSpec, init_weights
     from rphedge.ops.paths import path_indices
@@ -152,8 +153,8 @@ def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0
     per = n // world
     f, p1, y = _data(n if n_total is None else n_total, dev, rank * per, per)
     y = y + 0.02 * torch.sin(9 * f)
-    be = HipBackend(spec, per, TrainConfig(batch_size=per, lm_gram_paths=2048), device=dev, world=world,
-                    rank=rank, mailbox=mailbox, lm_mailbox=lm_mailbox)
+    be = HipBackend(spec, per, TrainConfig(batch_size=per, lm_gram_paths=2048, lm_leaf_paths=leaf, lm_out_fix=out_fix),
+                    device=dev, world=world, rank=rank, mailbox=mailbox, lm_mailbox=lm_mailbox)
     gk = {}
     if side:  # the global Gram subsample, identical on every rank (engine.gram_subsample)
         ns, blk, stride = gram_subsample(n, 2048)
@@ -180,7 +181,7 @@ def _lm_fit(rank, world, n, passes, dev, mailbox=None, lm_mailbox=None, starts=0
     return current_weights(spec, w), be.lm_state()
 
 
-def _worker_lm(rank, world, port, n, passes, out, side=False):
+def _worker_lm(rank, world, port, n, passes, out, side=False, leaf=0, out_fix=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     from torch.distributed import distributed_c10d as c10d
@@ -192,10 +193,10 @@ def _worker_lm(rank, world, port, n, passes, out, side=False):
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     store = c10d._get_default_store()
-    mb = IpcMailbox(rank, world, 128, store, dev, tag="t_lm_a")
-    lmb = IpcMailbox(rank, world, L.LM_RED + L.LM_DP_WGS, store, dev, tag="t_lm_b")
+    mb = IpcMailbox(rank, world, 128, store, dev, tag=f"t_lm_a{world}")
+    lmb = IpcMailbox(rank, world, L.LM_DP_PITCH, store, dev, tag=f"t_lm_b{world}")
     dist.barrier()
-    w, st = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb, side=side)
+    w, st = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb, side=side, leaf=leaf, out_fix=out_fix)
     lmb.check()
     np.save(out + f".{rank}.npy", w)
     with open(out + f".{rank}.txt", "w") as fh:
@@ -232,7 +233,42 @@ def test_lm_mailbox_exchange_two_ranks_one_gpu(side):
     assert np.array_equal(w0, w1) and s0 == s1
     ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0), side=side)
     assert s0 == f"{st['accepted']} {st['chol_failures']}"
-    np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
+    if side:
+        # the shared Gram, the gradient region summed in k_lm_reduce (fused
+        # exchange) and W-invariant leaves / reduction trees: the one-rank fit
+        # bit for bit (2^15 paths: the auto leaf is one 128-path block at both
+        # world sizes)
+        assert np.array_equal(w0, ref), np.abs(w0 - ref).max()
+    else:
+        np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_lm_strong_scaling_rehearsal_is_bitwise(world):
+    """The same 2^18 global paths fitted by 1, 2 or 4 ranks on one GPU (shared
+    Gram subsample, gradient region summed inside k_lm_reduce over the IPC
+    mailboxes, output-layer Newton step): with the same contiguous 256-path
+    leaves at every world size (TrainConfig.lm_leaf_paths) and the
+    contiguous-halves reduction trees, every rank's weights are bit for bit
+    those of the one-rank fit."""
+    n, passes, leaf = 1 << 18, 10, 256
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "w")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_lm, args=(r, world, port, n, passes, out, True, leaf, True))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        ws = [np.load(out + f".{r}.npy") for r in range(world)]
+        ss = [open(out + f".{r}.txt").read() for r in range(world)]
+    ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0), side=True, leaf=leaf, out_fix=True)
+    for r in range(world):
+        assert np.array_equal(ws[r], ref), (r, np.abs(ws[r] - ref).max())
+        assert ss[r] == f"{st['accepted']} {st['chol_failures']}"
 
 
 def test_lm_gram_side_one_rank_is_bitwise_the_shard_gram():
@@ -258,7 +294,7 @@ def _worker_ms(rank, world, port, n, passes, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     store = c10d._get_default_store()
     mb = IpcMailbox(rank, world, 128, store, dev, tag="t_ms_a")
-    lmb = IpcMailbox(rank, world, L.LM_RED + L.LM_DP_WGS, store, dev, tag="t_ms_b")
+    lmb = IpcMailbox(rank, world, L.LM_DP_PITCH, store, dev, tag="t_ms_b")
     dist.barrier()
     w, losses = _lm_fit(rank, world, n, passes, dev, mailbox=mb, lm_mailbox=lmb, starts=3)
     lmb.check()

@@ -156,7 +156,7 @@ def _inject_worker(rank, world, port, inject, n, out):
 
     # the mailboxes api.HedgeRun.build would create for these transports
     mb = D.make_mailbox(info, spec.red_width, tag="t_inj_pk", mode=info.dp_mode)
-    lmb = D.make_mailbox(info, L.LM_RED + L.LM_DP_WGS, tag="t_inj_lm", mode=info.lm_dp_mode)
+    lmb = D.make_mailbox(info, L.LM_DP_PITCH, tag="t_inj_lm", mode=info.lm_dp_mode)
     be = HipBackend(spec, per, TrainConfig(batch_size=n, lm_gram_paths=2048), device=dev, world=world, rank=rank,
                     comm=info.comm, mailbox=mb, lm_mailbox=lmb, lm_comm=info.lm_comm)
     w, hist = _lm_fit(be, spec, f, p1, y, 8)
