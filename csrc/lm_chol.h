@@ -365,40 +365,64 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
       lmc_load_row(a[s], T + TG::tidx(arow[s] >> 4, K) * 256 + (arow[s] & 15) * 16, arow[s] & 15);
     }
     if constexpr (K == TG::NK - 1) LMC_STAMP(6);
-    // column c's block: scale column c, update column c + 1 and start the
-    // pivot chain of c + 1, then the remaining updates of column c (which
-    // hide that chain's latency); a scheduling barrier closes every block, so
-    // only one column's broadcasts are live at a time (no spills)
+    // column c's block: scale column c, then the dependent chain of column
+    // c + 1 (its update by column c, its pivot, v_rsq_f64 + the Newton step:
+    // seven dependent fp64 operations) in seven stages, each followed by a
+    // share of column c's remaining updates (independent of the chain) and a
+    // scheduling barrier - the wave issues in order, so the updates fill the
+    // chain's latencies instead of following it; only one column's broadcasts
+    // are live at a time (no spills).  Same operations as lmc_rsq.
     double piv = lmc_bcast<0>(dk[0]);
     double rl = lmc_rsq(piv);
     double myrl = 0.0;  // lane i < NC of every DPP row: 1 / L[16K + i][16K + i]
     lm_static_for<NC>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
+      constexpr int NU = NC - c - 2 > 0 ? NC - c - 2 : 0;  // remaining updates j = c + 2 .. NC - 1
+      constexpr int NST = 7;                                // chain stages
       ok = ok && piv > 0.0;
       dk[c] *= rl;  // lane i: L[16K + i][16K + c] (i >= c)
 #pragma unroll
       for (int s = 0; s < NS; ++s) a[s][c] *= rl;
       myrl = li == c ? rl : myrl;
-      double piv_n = 1.0, rl_n = 1.0;
-      if constexpr (c + 1 < NC) {
-        const double l1 = lmc_bcast<c + 1>(dk[c]);  // L[16K + c + 1][16K + c]
-        dk[c + 1] = __builtin_fma(-dk[c], l1, dk[c + 1]);
+      // updates of columns c + 2 + [lo, hi) by column c
+      auto updates = [&](auto lo_c, auto hi_c) {
+        constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
+        lm_static_for<NC>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if constexpr (j >= c + 2 + LO && j < c + 2 + HI) {
+            const double lj = lmc_bcast<j>(dk[c]);  // L[16K + j][16K + c]
+            dk[j] = __builtin_fma(-dk[c], lj, dk[j]);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) a[s][c + 1] = __builtin_fma(-a[s][c], l1, a[s][c + 1]);
-        // the next pivot: lane c + 1's diagonal, final after this update
-        piv_n = lmc_bcast<c + 1>(dk[c + 1]);
-        rl_n = lmc_rsq(piv_n);
-      }
-      lm_static_for<NC>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        if constexpr (j > c + 1) {
-          const double lj = lmc_bcast<j>(dk[c]);  // L[16K + j][16K + c]
-          dk[j] = __builtin_fma(-dk[c], lj, dk[j]);
+            for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
+          }
+        });
+      };
+      double piv_n = 1.0, rl_n = 1.0, l1 = 0.0, hn = 0.0, yn = 0.0, tn = 0.0;
+      lm_static_for<NST>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (c + 1 < NC) {
+          if constexpr (k == 0) {
+            l1 = lmc_bcast<c + 1>(dk[c]);  // L[16K + c + 1][16K + c]
+          } else if constexpr (k == 1) {
+            dk[c + 1] = __builtin_fma(-dk[c], l1, dk[c + 1]);
 #pragma unroll
-          for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
+            for (int s = 0; s < NS; ++s) a[s][c + 1] = __builtin_fma(-a[s][c], l1, a[s][c + 1]);
+          } else if constexpr (k == 2) {
+            piv_n = lmc_bcast<c + 1>(dk[c + 1]);  // the next pivot: lane c + 1's diagonal, now final
+          } else if constexpr (k == 3) {
+            yn = __builtin_amdgcn_rsq(piv_n);
+            hn = -0.5 * piv_n;
+          } else if constexpr (k == 4) {
+            tn = hn * yn;
+          } else if constexpr (k == 5) {
+            tn = __builtin_fma(tn, yn, 1.5);
+          } else {
+            rl_n = yn * tn;
+          }
         }
+        updates(std::integral_constant<int, k * NU / NST>{}, std::integral_constant<int, (k + 1) * NU / NST>{});
+        __builtin_amdgcn_sched_barrier(0);
       });
-      __builtin_amdgcn_sched_barrier(0);
       piv = piv_n;
       rl = rl_n;
     });
@@ -478,14 +502,15 @@ RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv, con
       // broadcasts instead of a dependent 16-step chain
       if constexpr (K == TG::NX - 1)
         if (!lmc_wait(xdone, 3u)) *s_fail = 2;
+      // (z is the same in every DPP row: z_i = row_newbcast:i, no SGPR round trip)
       const double* xk = X + K * 256 + c;
       double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const double zi = lmc_readlane(z, i);
+      lm_static_for<16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const double zi = lmc_bcast<i>(z);
         if (i & 1) a1 = __builtin_fma(xk[i * 16], zi, a1);
         else a0 = __builtin_fma(xk[i * 16], zi, a0);
-      }
+      });
       dk = a0 + a1;
     } else {
       // column c of the diagonal tile: L[16K + j][16K + c], j = 0..15
@@ -494,12 +519,12 @@ RPH_INLINE void lmc_backward(const double* T, const double* rdg, double* dv, con
 #pragma unroll
       for (int j = 0; j < 16; ++j) lc[j] = td[tg_off(j, c)];
       const double rd = col < P ? rdg[col] : 0.0;
-#pragma unroll
-      for (int j = NC - 1; j >= 0; --j) {
-        const double dj = lmc_readlane(z * rd, j);  // d[16K + j] (final in lane j)
+      lm_static_for<NC>([&](auto jc) {
+        constexpr int j = NC - 1 - decltype(jc)::value;
+        const double dj = lmc_bcast<j>(z * rd);  // d[16K + j] (final in lane j of every DPP row)
         if (c == j) dk = dj;
         z = __builtin_fma(-lc[j], dj, z);  // lanes c < j
-      }
+      });
     }
     if (q == 0 && col < P) dv[col] = dk;
     lmc_wave_sync();

@@ -685,7 +685,7 @@ class HipBackend:
                 raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets up to 174 parameters)")
             P, R, nblk, two = shp
             t = self.tcfg
-            nw, leaf = lm_pass_schedule(self.n_local, int(t.lm_leaf_paths))
+            nw, leaf = lm_pass_schedule(self.n_local, int(os.environ.get("RPH_LM_LEAF", t.lm_leaf_paths)))  # (env: A/B)
             W = max(self.world, 1)
             # the global Gram subsample (every rank: gw = ns / 64 Gram workgroups,
             # past the path grid where it is larger)
@@ -869,7 +869,13 @@ class HipBackend:
         def make():
             _, R, nblk, two = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             t, dev = self.tcfg, self.device
+            # K instances in one launch: at most 256 / K pass workgroups each, so
+            # the whole grid is co-resident (one workgroup per CU) and a pass
+            # costs one round of workgroups, not K
             nw, leaf = lm_pass_schedule(nsub, 0 if int(t.lm_leaf_paths) >= 0 else -1)
+            if K > 1 and leaf > 0:
+                nw = max(1, min(nw, 256 // K))
+                leaf = -(-((nsub + 127) // 128) // (4 * nw))
             gw = int(max(1, min(max(L.LM_TILE, min(int(t.lm_gram_paths), nsub)) // L.LM_TILE, nw)))
             w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
             rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)[:K, :P]

@@ -101,7 +101,7 @@ class LmDesc(C.Structure):
         ("out_n", C.c_int), ("out_mu", C.c_float), ("out_gram", C.c_int), ("pad3", C.c_int),
         ("slab_o", VP),
         ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("q_delta", C.c_float), ("q_kappa", C.c_float),
-        ("dp", LmDpDesc), ("dp_fused", C.c_int), ("pad4", C.c_int),
+        ("dp", LmDpDesc), ("dp_fused", C.c_int), ("leaf_blocks", C.c_int),
     ]
 
     def __init__(self, *a, **kw):

@@ -103,7 +103,7 @@ def test_lm_pinball_fit_matches_torch(shape):
     tb.fit(wc, oc, fcs, cd, fq, seed=0)
     hist_g = outs[0][1][L.F_HIST:L.F_HIST + 13]
     hist_c = np.asarray(tb.lm_last["hist"])
-    np.testing.assert_allclose(np.minimum.accumulate(hist_g)[:6], np.minimum.accumulate(hist_c)[:6], rtol=5e-3)
+    np.testing.assert_allclose(np.minimum.accumulate(hist_g)[:6], np.minimum.accumulate(hist_c)[:6], rtol=1e-2)
     assert min(hist_g) == pytest.approx(min(hist_c), rel=2e-2)
     assert min(hist_g) < 0.7 * hist_g[0]
     from rphedge.models.hedge_mlp import torch_forward
