@@ -149,6 +149,9 @@ def parse(argv=None):
     ap.add_argument("--lm-passes-first", type=int, default=None)
     ap.add_argument("--lm-passes-rest", type=int, default=None)
     ap.add_argument("--lm-gram-paths", type=int, default=None)
+    ap.add_argument("--lm-leaf-paths", type=int, default=None,
+                    help="LM pass schedule: -1 cyclic (default); > 0 contiguous leaves of this many paths - the same "
+                         "value at every --gpus makes a strong-scaling rehearsal bitwise the 1-GPU fit")
     ap.add_argument("--lm-damping", default=None, choices=["simple", "nielsen"])
     ap.add_argument("--lm-lam0", type=float, default=None)
     ap.add_argument("--lm-lam-up", type=float, default=None)
@@ -195,7 +198,7 @@ def parse(argv=None):
                     ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam0_first", 0.0),
                     ("lm_lam_carry", 0.0),
                     ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16), ("lm_explore_one", 0), ("lm_renorm", 0), ("lm_out_fix", 0),
-                    ("lm_out_mu", 1e-5)):
+                    ("lm_out_mu", 1e-5), ("lm_leaf_paths", -1)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -220,7 +223,7 @@ def build_run(a, world: int):
                         lm_lam_carry=a.lm_lam_carry, lm_starts=a.lm_starts, lm_explore_passes=a.lm_explore_passes,
                         lm_explore_log2=a.lm_explore_log2, lm_explore_one=bool(a.lm_explore_one),
                         lm_renorm=bool(a.lm_renorm), lm_out_fix=bool(a.lm_out_fix),
-                        lm_out_mu=a.lm_out_mu)
+                        lm_out_mu=a.lm_out_mu, lm_leaf_paths=a.lm_leaf_paths)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),
@@ -328,15 +331,19 @@ def lm_fit_stats(ind) -> dict:
             "first_date": first}
 
 
-def lm_exchange_record(run, passes: int, world: int) -> dict:
+def lm_exchange_record(run, a, world: int) -> dict:
     """Data-parallel LM exchange volume: every rank builds the same Gram
     matrix from the simulated global subsample, so one pass pushes only the
-    gradient region [g | stats | out-means] to each peer."""
-    per_peer = int(run.backend.lm_exchange_bytes())
+    gradient region [g | stats] to each peer (+ the packed output Gram in the
+    passes that build it), from inside k_lm_reduce (no extra launch)."""
+    be = run.backend
+    per_peer = int(be.lm_exchange_bytes())
+    run_peer = int(be.lm_exchange_bytes_run(a.lm_passes_first, a.lm_passes_rest, run.paths.n_coarse - 1))
     return {"bytes_per_pass_per_peer": per_peer, "peers": world - 1,
             "bytes_per_pass_per_rank": per_peer * (world - 1),
-            "bytes_per_run_per_rank": per_peer * (world - 1) * int(passes),
-            "same_gram_every_rank": bool(run.backend._lm_same_gram)}
+            "bytes_per_run_per_rank": run_peer * (world - 1),
+            "same_gram_every_rank": bool(getattr(be, "_lm_same_gram", True)),
+            "fused_in_reduce": bool(world > 1 and be.lm_mailbox is not None and getattr(be, "_lm_same_gram", False))}
 
 
 def multistart_record(run, a, world: int) -> dict:
@@ -484,6 +491,7 @@ def main(argv=None):
                    "lm_passes_first": a.lm_passes_first if lm else None,
                    "lm_passes_rest": a.lm_passes_rest if lm else None,
                    "lm_gram_paths": a.lm_gram_paths if lm else None,
+                   "lm_leaf_paths": a.lm_leaf_paths if lm else None,
                    "lm_damping": a.lm_damping if lm else None,
                    "lm_lam": [a.lm_lam0, a.lm_lam_up, a.lm_lam_down] if lm else None,
                    "lm_lam0_rest": (a.lm_lam0_rest or None) if lm else None,
@@ -512,9 +520,12 @@ def main(argv=None):
                     "mc_discounted_payoff": res.summary["E_payoff"] * run.scale * math.exp(-cfg.r * cfg.T),
                     "reference_terminal_residual_std_52step": 1.7504, "reference_V0": 11.352},
         "lm": lm_stats,
-        "lm_exchange": lm_exchange_record(run, passes, world) if (lm and not a.cpu) else None,
+        "lm_exchange": lm_exchange_record(run, a, world) if (lm and not a.cpu) else None,
         "memory": memory,
         "path_samples_per_s": path_samples, "full_passes_per_run": passes,
+        # nodes of the replayed hipGraph (kernels + copies): the same at every
+        # world size when the data-parallel exchange adds no launch
+        "graph_nodes": int(run.graph.num_nodes) if (use_graph and run.graph is not None) else None,
         "path_samples_vs_keras": path_samples / BASELINE_SAMPLES_PER_S,
     }
     if rank == 0:

@@ -20,8 +20,8 @@ namespace rph {
     if (d.stamps != nullptr && threadIdx.x == 0)                                        \
       d.stamps[(size_t)blockIdx.x * 8 + (k)] = rph_stamp_clock();                       \
   } while (0)
-// the bodies' "path loop done" stamp (the bodies also run in k_lm_pass, whose
-// workgroups 0 and 1 leave stamp rows 0 and 1 to k_lm_solve)
+// the LM pass body's "path loop done" stamp (k_lm_pass's workgroups 0 and 1
+// leave stamp rows 0 and 1 to k_lm_solve; the Adam bodies stamp every row)
 #define RPH_STAMP_BODY(k)                                                               \
   do {                                                                                  \
     if (blockIdx.x >= 2) RPH_STAMP(k);                                                  \

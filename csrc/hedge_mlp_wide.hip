@@ -461,7 +461,7 @@ struct WideBody {
         outer_mfma_tr((unsigned char*)img, a1b, dzb, r, h, lane, gw2);
       }
     }
-    RPH_STAMP_BODY(5);  // path loop done
+    RPH_STAMP(5);  // path loop done (Adam fits: every workgroup's own row)
 
     // ---- per-wave packet -> LDS, cross-wave sum -----------------------------
     half_reduce_scatter<RV>(g, lane);

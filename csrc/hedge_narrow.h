@@ -153,7 +153,7 @@ struct NarrowBody {
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = fmaf(x[f], dz1, g[S::OW1 + f * H + i]);
       }
     }
-    RPH_STAMP_BODY(5);  // path loop done
+    RPH_STAMP(5);  // path loop done (Adam fits: every workgroup's own row)
     // ---- in-wave reduce-scatter, cross-wave LDS sum ------------------------
     wave_reduce_scatter<R>(g, lane);
     constexpr int PER = R / 64;

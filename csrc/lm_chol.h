@@ -306,6 +306,18 @@ RPH_INLINE double lmc_bcast(double v) {
   return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xF, 0xF, true);
 }
 
+// acc += row_newbcast:J(s0) * (-s1): v_fmac_f64_dpp (gfx90a+ DPP on a 64-bit
+// VOP2 op) - the broadcast rides in the fma, one instruction per update and no
+// dependent mov.  The same single rounding as fma(-s1, bcast(s0), acc).  (The
+// compiler's hazard recognizer sees the inline DPP: it pads a VALU write of
+// s0 right before it.)
+template <int J>
+RPH_INLINE void lmc_fmac_bcast(double& acc, double s0, double s1) {
+  asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(s0), "v"(s1), "i"(J));
+}
+
 // A 16-row tile row (16 doubles) from the store / to the store (swizzled columns)
 RPH_INLINE void lmc_load_row(double (&a)[16], const double* tr, int r) {
   const int sw = (r >> 1) << 1;
@@ -384,16 +396,20 @@ RPH_INLINE void lmc_panels(double* T, double* rdg, double* bc, const unsigned* p
 #pragma unroll
       for (int s = 0; s < NS; ++s) a[s][c] *= rl;
       myrl = li == c ? rl : myrl;
+      // the inline v_fmac_f64_dpp below read dk[c] through DPP: two wait
+      // states after its VALU write whatever the hazard recognizer assumes
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 1");
       // updates of columns c + 2 + [lo, hi) by column c
       auto updates = [&](auto lo_c, auto hi_c) {
         constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
         lm_static_for<NC>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
           if constexpr (j >= c + 2 + LO && j < c + 2 + HI) {
-            const double lj = lmc_bcast<j>(dk[c]);  // L[16K + j][16K + c]
-            dk[j] = __builtin_fma(-dk[c], lj, dk[j]);
+            // x -= L[16K + j][16K + c] x_c: the broadcast of lane j's dk[c] inside the fma
+            lmc_fmac_bcast<j>(dk[j], dk[c], dk[c]);
 #pragma unroll
-            for (int s = 0; s < NS; ++s) a[s][j] = __builtin_fma(-a[s][c], lj, a[s][j]);
+            for (int s = 0; s < NS; ++s) lmc_fmac_bcast<j>(a[s][j], dk[c], a[s][c]);
           }
         });
       };

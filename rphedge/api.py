@@ -260,6 +260,7 @@ class HedgeRun:
                            lr=tr.lr, deterministic=tr.deterministic, max_wgs=tr.max_wgs,
                            mfma_fp32=str(tr.mfma_precision).lower() == "fp32", step_mode=tr.step_mode,
                            lm_gram_paths=int(tr.lm_gram_paths), lm_damping=str(tr.lm_damping),
+                           lm_leaf_paths=int(getattr(tr, "lm_leaf_paths", -1)),
                            lm_lam0=float(tr.lm_lam0), lm_lam_up=float(tr.lm_lam_up),
                            lm_lam_down=float(tr.lm_lam_down), lm_out_fix=bool(tr.lm_out_fix),
                            lm_out_mu=float(tr.lm_out_mu),

@@ -127,6 +127,9 @@ class TrainingParams:
     lm_explore_one: bool = False     # lm_starts = 1: the one start still explores first (a warm-up of
                                      # lm_explore_passes on the 2^lm_explore_log2 path prefix)
     lm_gram_paths: int = 4096        # Gram-matrix subsample (global paths, 64-path MFMA tiles)
+    lm_leaf_paths: int = -1          # LM pass schedule: -1 cyclic path blocks (fastest); > 0 contiguous leaves of
+                                     # this many paths per wave - with the same value at every world size the
+                                     # data-parallel fit over the same global paths is bitwise the 1-rank fit
     lm_damping: str = "simple"       # LM damping update: simple (x1/3 / x4) | nielsen (gain ratio)
     lm_lam0: float = 1e-3            # LM initial damping of every fit
     lm_lam_up: float = 4.0           # simple rule: damping x lam_up on a rejected trial

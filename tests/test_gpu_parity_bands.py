@@ -67,7 +67,14 @@ def test_mts_notebook_headline_seed_band():
     assert abs(np.mean(v0) / PUB["V0"] - 1) < 0.015, np.mean(v0)
     _band(v0, PUB["V0"], max_rel_scatter=0.035)
     _band(phi, PUB["phi0"], max_rel_scatter=0.06)
-    _band(psi, PUB["psi0"], max_rel_scatter=0.125)
+    _band(psi, PUB["psi0"], max_rel_scatter=0.095)
+    # the published (phi0, psi0) pair as one draw of the seed distribution:
+    # squared Mahalanobis distance under the 8-seed covariance within the 99 %
+    # chi-square(2) quantile (the CPU oracle's 13-variant sweep puts the
+    # reference semantics at 1.7, profiles/r5/mts_variants_cpu_8seeds.jsonl)
+    d = np.array([PUB["phi0"] - np.mean(phi), PUB["psi0"] - np.mean(psi)])
+    md2 = float(d @ np.linalg.solve(np.cov(np.vstack([phi, psi])), d))
+    assert md2 <= 9.21, md2
     # the total t = 0 hedge value phi0 + psi0 is far tighter than its split
     # (8 seeds: 7 within 3 % of each other, seed 1235 +6.7 %: robust band)
     _robust_band(np.add(phi, psi), PUB["phi0"] + PUB["psi0"], max_rel_scatter=0.02)
