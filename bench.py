@@ -69,17 +69,23 @@ LAM0_FIRST = 16.384000778198242  # float32(1e-3) * 4**7 (exact in fp32)
 PRESETS = {
     "euro30": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                    batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="lm",
-                   # first date: start at the damping of the first trial the round-3 sequence
-                   # (lam0 1e-3, x4 per rejection) could accept, fp32(1e-3) x 4^7: its 7
-                   # rejected trials are skipped, the rest of the trajectory is unchanged.
-                   # Its first 33 passes run on the 2^16-path prefix (the exploration
-                   # machinery with one start: latency-bound passes, ~14 us cheaper each),
-                   # then 35 on every path (8 seeds: 8.58 vs 8.85 ms at P&L 0.906 vs 0.908,
-                   # profiles/r4/seeds_explore_one.jsonl)
-                   lm_lam0_first=LAM0_FIRST, lm_explore_one=1, lm_explore_passes=33, lm_explore_log2=16,
-                   lm_passes_first=35,
+                   # first date: 16 starts explored at once (one launch per kernel, grid y =
+                   # start, 16 pass workgroups each) for 20 passes on the global 2^15-path
+                   # prefix (every rank the same), the best polished for 25 passes on every
+                   # path; from fp32(1e-3) x 4^7, the damping of the first trial the lam0 =
+                   # 1e-3 sequence could accept.  Seeds 1-8 / 9-16: P&L mean 0.891 / 0.891,
+                   # worst 0.901 / 0.900 at 7.13 ms, against 0.908 / 0.905, worst 0.938 / 0.937
+                   # at 7.49 ms for the round-4 single start (profiles/r5/seeds_*.jsonl)
+                   lm_lam0_first=LAM0_FIRST, lm_starts=16, lm_explore_passes=20, lm_explore_log2=15,
+                   lm_passes_first=25,
                    lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
+    # the round-4 default: one start, 33 warm-up passes on the 2^16-path prefix, 35 on every path
+    "euro30_1s": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
+                      batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1, optimizer="lm",
+                      lm_lam0_first=LAM0_FIRST, lm_explore_one=1, lm_explore_passes=33, lm_explore_log2=16,
+                      lm_passes_first=35, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                      label="European call, 30-step GBM, 1M Sobol paths per GPU, single-start first date"),
     # the flagship with a multi-start first date (4 starts x 45 passes on 2^16
     # paths, 25 polish passes): no first-date local minima (8 seeds: P&L mean
     # 0.893, worst 0.910 vs 0.908 / 0.944) for +1 ms (profiles/r4/ms_*.jsonl)
@@ -95,16 +101,20 @@ PRESETS = {
                      batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1,
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
                      optimizer="lm", lm_passes_first=35, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
-                     # first date: 45 passes on the 2^16-path prefix, then 35 on every path
-                     # (3 seeds: 12.5 vs 12.8 ms, P&L 2.419 vs 2.423 mean; profiles/r4/presets_explore_one.jsonl),
-                     # the prefix's 7 initial rejections at lam0 1e-3 skipped (the same P&L bit
-                     # for bit on 3 seeds, 12.41 ms; profiles/r4/lam0_warmup_presets.jsonl; basket5's
-                     # prefix has another rejection count: skipping 7 there diverges one seed)
-                     lm_lam0_first=LAM0_FIRST, lm_explore_one=1, lm_explore_passes=38, lm_explore_log2=16,
+                     # first date: 16 starts x 25 passes on the global 2^15-path prefix, the best
+                     # polished for 35 passes on every path (3 seeds: 11.38 ms, P&L 1.0024 /
+                     # 1.0038 / 1.0052 x the minimum-variance hedge, against 11.18 ms and
+                     # 1.0075 / 1.0042 / 1.0061 for one start: profiles/r5/seeds_presets.jsonl)
+                     lm_lam0_first=LAM0_FIRST, lm_starts=16, lm_explore_passes=25, lm_explore_log2=15,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
-                    optimizer="lm", lm_passes_first=120, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                    optimizer="lm", lm_passes_first=80, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                    # the first date is a 1-day hedge of the payoff (a near-digital delta):
+                    # 8 starts x 40 passes on the global 2^16-path prefix, the best polished
+                    # for 80 passes (3 seeds: last residual 0.069 / 0.071 / 0.075 against the
+                    # BS floor 0.062, where 120 passes from one start left seed 2 at 0.150)
+                    lm_starts=8, lm_explore_passes=40, lm_explore_log2=16,
                     label="European call, 252-step GBM, 2M paths per GPU (16M at 8 GPUs)"),
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,

@@ -1,11 +1,18 @@
-"""Hedge quality of the GPU presets against analytic hedges on the SAME paths
-(bench.py's hedge_anchor): Black-Scholes delta (euro30, euro252), the Heston
-minimum-variance hedge (heston30; rphedge.analytic.heston_hedge_anchor) and
-the Levy moment-matched basket delta (basket5).  2^18 paths per run, seed
-1234; the bounds are the measured ratios (profiles/r4/quality_2p18_ratios.jsonl)
-with a small margin: euro30 1.009, heston30 1.006, euro252 1.065, basket5
-1.160 (the basket is the one preset above the 1.05 target at this path
-count: BENCHMARKS.md round 4)."""
+"""Hedge quality of the GPU presets at their BASELINE sizes against analytic
+hedges on the SAME paths (bench.py's hedge_anchor): Black-Scholes delta
+(euro30, euro252), the Heston minimum-variance hedge (heston30;
+rphedge.analytic.heston_hedge_anchor) and the Levy moment-matched basket delta
+(basket5).  Two weight-init seeds per preset (the spread between seeds is a
+first-date local-minimum / later-date effect; one seed cannot show it).  The
+bounds are the round-5 measurements (profiles/r5/seeds_*.jsonl, BENCHMARKS.md)
+with a small margin:
+
+  euro30   (2^20 paths)  16 seeds: P&L <= 1.030 x BS delta            -> 1.04
+  heston30 (2^20 paths)  seeds 1-3: <= 1.0052 x min-variance          -> 1.01
+  euro252  (2^21 paths)  seeds 1-3: 1.114 / 1.174 / 1.117 x BS delta  -> 1.20,
+                         last one-step residual 0.069-0.075 (floor 0.062) -> 0.08
+  basket5  (2^23 paths)  seeds 1-2: 1.082 / 1.076 x Levy delta        -> 1.10
+"""
 import math
 
 import pytest
@@ -15,16 +22,21 @@ from test_bench_analytic import _bench
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("preset,ratio,price_tol", [("euro30", 1.03, 0.01), ("heston30", 1.02, 0.02),
-                                                    ("euro252", 1.08, 0.01), ("basket5", 1.18, None)])
-def test_preset_pnl_within_anchor(preset, ratio, price_tol):
-    r = _bench(["--preset", preset, "--paths-log2", "18", "--steps", "1", "--warmup", "1"])
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("preset,ratio,price_tol,resid_max", [("euro30", 1.04, 0.01, None),
+                                                              ("heston30", 1.01, 0.02, None),
+                                                              ("euro252", 1.20, 0.01, 0.08),
+                                                              ("basket5", 1.10, None, None)])
+def test_preset_pnl_within_anchor(preset, ratio, price_tol, resid_max, seed):
+    r = _bench(["--preset", preset, "--steps", "1", "--warmup", "1", "--seed", str(seed)])
     q = r["quality"]
     a = q["hedge_anchor"]
     assert a and a.get("pnl_std"), q
     pnl = q["terminal_pnl_std"]
     assert math.isfinite(pnl) and pnl <= ratio * a["pnl_std"], (preset, pnl, a["pnl_std"])
     assert abs(q["terminal_pnl_mean"]) < 0.05 * a["pnl_std"] + 0.01, q["terminal_pnl_mean"]
+    if resid_max is not None:
+        assert q["terminal_residual_std"] <= resid_max, q["terminal_residual_std"]
     if price_tol is not None:
         assert abs(q["V0"] - q["anchor"]["price"]) < price_tol, (q["V0"], q["anchor"])
     else:
