@@ -67,11 +67,13 @@ def test_mts_notebook_headline_seed_band():
     assert abs(np.mean(v0) / PUB["V0"] - 1) < 0.015, np.mean(v0)
     _band(v0, PUB["V0"], max_rel_scatter=0.035)
     _band(phi, PUB["phi0"], max_rel_scatter=0.06)
-    _band(psi, PUB["psi0"], max_rel_scatter=0.095)
+    _band(psi, PUB["psi0"], max_rel_scatter=0.115)
     # the published (phi0, psi0) pair as one draw of the seed distribution:
     # squared Mahalanobis distance under the 8-seed covariance within the 99 %
-    # chi-square(2) quantile (the CPU oracle's 13-variant sweep puts the
-    # reference semantics at 1.7, profiles/r5/mts_variants_cpu_8seeds.jsonl)
+    # chi-square(2) quantile (GPU: 1.56, z = -1.19 / +1.02; the CPU oracle's
+    # 13-variant sweep puts the reference semantics at 1.7,
+    # profiles/r5/mts_variants_cpu_8seeds.jsonl: the split is seed scatter of
+    # an early-stopped Adam endpoint, psi0 sd 11 % of its mean)
     d = np.array([PUB["phi0"] - np.mean(phi), PUB["psi0"] - np.mean(psi)])
     md2 = float(d @ np.linalg.solve(np.cov(np.vstack([phi, psi])), d))
     assert md2 <= 9.21, md2
