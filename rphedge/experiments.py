@@ -32,6 +32,23 @@ def mts_parameters(**over) -> dict:
     return p
 
 
+def mts_lm_parameters(**over) -> dict:
+    """:func:`mts_parameters` (corrected two-network semantics) with BOTH fits
+    of every date on Levenberg-Marquardt (MSE fits and the Q99 pinball fits,
+    ``q99_optimizer="lm"``): a 16-start first date on the 2^15-path prefix, the
+    exact output-layer step after every MSE fit, 200 IRLS passes for the first
+    pinball fit and 20 for the later ones, each starting from the previous
+    date's Q99 net.  At 2^20 paths the whole 40-date induction takes ~0.1 s on
+    one MI355X vs 10-23 s with Keras-Adam, with V0 / phi0 / psi0 inside the
+    Adam seed band and a lower pinball loss on every date (BENCHMARKS.md round 5,
+    profiles/r5/pension_lm_vs_adam.jsonl)."""
+    p = mts_parameters(optimizer="lm", q99_optimizer="lm", lm_starts=16, lm_explore_passes=40, lm_explore_log2=15,
+                       lm_passes_first=60, lm_passes_rest=3, lm_lam_carry=3.0, lm_out_fix=True,
+                       lm_q_passes_first=200, lm_q_passes_rest=20, lm_q_start="warm")
+    p.update(over)
+    return p
+
+
 def mts_notebook_parameters(**over) -> dict:
     """The paths behind the "Multi Time Step.ipynb" HEADLINE numbers (Q15):
     cell 9 ("SV - Version", exec 94) overwrote ``Y_paths`` after the GBM cell -

@@ -115,20 +115,39 @@ def test_lm_pinball_fit_matches_torch(shape):
     assert above < 0.03, above  # (12 IRLS passes approach the quantile from above)
 
 
+def _q99_coverage(run):
+    """Per date: fraction of paths whose next value exceeds the Q99 net's
+    hedge (V_{t+1} - h_q(state_t) . prices_{t+1} > 0)."""
+    from rphedge.models.hedge_mlp import torch_forward
+
+    ind, spec, p = run.induction, run.spec, run.paths
+    out = []
+    with torch.no_grad():
+        for t in range(ind.n_dates):
+            X = torch.stack([f.float() for f in p.features(t)], 1)
+            mu, isd = ind.norms[t]
+            X = (X - torch.tensor(mu, dtype=torch.float32, device=X.device)) * \
+                torch.tensor(isd, dtype=torch.float32, device=X.device)
+            pr = torch.stack([q.float() for q in p.prices(t + 1)] + [torch.full_like(X[:, 0], float(p.bond[t + 1]))], 1)
+            r = ind.values[t + 1] - (torch_forward(spec, ind.snap[t, 1, :spec.nparams], X) * pr).sum(1)
+            out.append(float((r > 0).double().mean()))
+    return np.asarray(out)
+
+
 def test_pension_both_fits_on_lm():
     """Corrected-mode pension (two networks, RP-module parameters, 2^16 paths,
-    40 quarterly dates): MSE and Q99 fits both on LM.  Every pinball fit ends
-    with ~1 % of its targets above the fitted quantile (the Q99 sign condition
-    of "Single Time Step.ipynb":656-662 at the 99 % level), V0 sits between the
-    pure-MSE value and the Q99 one, and the run has no Cholesky failure."""
+    40 quarterly dates) on experiments.mts_lm_parameters: MSE and Q99 fits
+    both on LM.  Every date's pinball fit leaves ~1 % of its targets above the
+    fitted quantile (the Q99 sign condition of "Single Time Step.ipynb":656-662
+    at the 99 % level; 2^20-path runs: 1.01 % mean over 8 seeds vs 1.10 % with
+    Adam, profiles/r5/pension_lm_vs_adam.jsonl), V0 / phi0 / psi0 sit in the
+    Adam seed band, and the run has no Cholesky failure."""
     from rphedge import experiments
     from rphedge.api import HedgeRun
     from rphedge.config import parse_params
+    from rphedge.ops import layout as L
 
-    p = experiments.mts_parameters()
-    p.update(n_paths=16, optimizer="lm", q99_optimizer="lm", lm_passes_first=40, lm_passes_rest=3,
-             lm_q_passes_first=30, lm_q_passes_rest=4, lm_lam_carry=3.0, verbose=False, device="cuda:0")
-    cfg = parse_params(p)
+    cfg = parse_params(experiments.mts_lm_parameters(n_paths=16, verbose=False, device="cuda:0"))
     run = HedgeRun(cfg)
     res = run.run()
     torch.cuda.synchronize()
@@ -136,9 +155,13 @@ def test_pension_both_fits_on_lm():
     ind = res.induction
     for dres in ind.dates:
         assert dres.fit_q99 is not None and dres.fit_q99["best_loss"] == dres.fit_q99["best_loss"]
-    # the final date's Q99 hedge: fraction of paths whose next value exceeds it
-    st_q = run.backend._lm_buffers(1)["state"].cpu().numpy()
-    from rphedge.ops import layout as L
-
-    assert int(st_q[L.LMS_FAIL]) == 0
-    assert 0.5e6 < res.v0 < 1.5e6
+    bq = run.induction.backend_q or run.backend  # the pinball fits' backend (side stream when concurrent)
+    # a failed factorisation is handled as a rejected trial (damping x lam_up);
+    # allow a rare one among the ~1,900 trials of the run
+    fails = [int(be._lm_buffers(loss)["state"].cpu().numpy()[L.LMS_FAILTOT])
+             for be, loss in ((run.backend, L.LOSS_MSE), (bq, L.LOSS_PINBALL))]
+    assert sum(fails) <= 3, fails
+    cov = _q99_coverage(run)
+    assert 0.006 < cov.mean() < 0.014 and cov.max() < 0.03, cov
+    # Adam seed band at 2^20 paths (8 seeds): V0 972.6k-1043.9k, phi0 607k-671k, psi0 314k-428k
+    assert 940e3 < res.v0 < 1060e3 and 560e3 < res.phi < 720e3 and 250e3 < res.psi < 460e3, (res.v0, res.phi, res.psi)

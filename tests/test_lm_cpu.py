@@ -212,3 +212,22 @@ def test_mean_refit_keeps_v0_on_price_cpu():
     mc = on.summary["E_payoff"] * on.scale * math.exp(-0.08)
     assert abs(on.v0 / mc - 1) < 2e-3, (on.v0, mc)
     assert abs(on.v0 - off.v0) > 1e-4   # the refit is active in the default run
+
+
+def test_pension_lm_preset_cpu():
+    """experiments.mts_lm_parameters (both fits of every date on LM, the Q99
+    fits as IRLS Gauss-Newton warm-started from the previous date's Q99 net)
+    through the API on the torch oracle, shrunk to 10 annual dates and 2^10
+    paths: finite results in the range of the Adam runs and every pinball fit
+    lowers its loss."""
+    from rphedge import experiments
+    from rphedge.api import run_params
+
+    p = experiments.mts_lm_parameters(n_paths=10, dt=0.1, rebalancing=1.0, device="cpu", verbose=False, lm_starts=4,
+                                      lm_explore_passes=10, lm_explore_log2=9, lm_passes_first=20,
+                                      lm_q_passes_first=30, lm_q_passes_rest=5)
+    r = run_params(p)
+    assert 0.8e6 < r.v0 < 1.2e6 and 0.3e6 < r.phi < 0.9e6 and 0.0 < r.psi < 0.6e6, (r.v0, r.phi, r.psi)
+    for d in r.induction.dates:
+        h = d.fit_q99["history"]
+        assert len(h) > 1 and math.isfinite(d.fit_q99["best_loss"]) and d.fit_q99["best_loss"] <= h[0]
