@@ -1329,16 +1329,15 @@ extern "C" int rph_lm_dp_exchange(const LmDpDesc* x, double* red, int ng, int p,
 // (lm_chol.h); larger nets have no LM solver and fit with Adam
 // (HipBackend.lm_supported() is False)
 
-// Geometry of the LM kernels for a shape: returns 0 and fills (P, R, NBLK,
-// two workgroups per CU) or -1 for shapes without an LM solver.
-extern "C" int rph_lm_shape(int nin, int h, int nout, int head, int* p, int* r, int* nblk, int* two_per_cu) {
+// Geometry of the LM kernels for a shape: returns 0 and fills (P, R, NBLK)
+// or -1 for shapes without an LM solver.
+extern "C" int rph_lm_shape(int nin, int h, int nout, int head, int* p, int* r, int* nblk) {
 #define X(A, B, C, E)                                                    \
   if (shape_is(nin, h, nout, head, A, B, C, E)) {                        \
     using K = LmKernels<A, B, C, E>;                                     \
     *p = K::S::P;                                                        \
     *r = K::S::R;                                                        \
     *nblk = LmShape<K::S::P>::NBLK;                                      \
-    *two_per_cu = 0;                                                     \
     return 0;                                                            \
   }
   RPH_LM_SHAPES(X)

@@ -298,15 +298,11 @@ def gram_subsample(n_total: int, lm_gram_paths: int) -> tuple[int, int, int]:
     return ns, ns // nb, n_total // nb
 
 
-def lm_pass_wgs(n_local: int, two_per_cu: bool) -> int:
+def lm_pass_wgs(n_local: int) -> int:
     """Workgroups of the LM pass kernel (HipBackend._lm_buffers; the torch
-    oracle derives its Gram subsample from the same number): 512 where two
-    pass workgroups fit per CU (1-3 input nets), else 256, at most one per
-    256 local paths."""
-    return int(max(1, min(512 if two_per_cu else 256, n_local // 256)))
-
-
-LM_PAIR_WPS = 1  # csrc/hedge_lm.hip RPH_LM_PAIR_WPS default (one pass workgroup per CU)
+    oracle derives its Gram subsample from the same number): one per CU (256),
+    at most one per 256 local paths."""
+    return int(max(1, min(256, n_local // 256)))
 
 
 def lm_pass_schedule(n_local: int, leaf_paths: int = 0) -> tuple[int, int]:
@@ -315,7 +311,7 @@ def lm_pass_schedule(n_local: int, leaf_paths: int = 0) -> tuple[int, int]:
     split into 4 x that many contiguous leaves; > 0 = leaves of that many
     paths (the workgroups to cover them, at most 256); < 0 = the cyclic
     schedule (leaf 0)."""
-    nw = lm_pass_wgs(n_local, False)
+    nw = lm_pass_wgs(n_local)
     nblk = (int(n_local) + 127) // 128
     if leaf_paths < 0:
         return nw, 0
@@ -367,12 +363,6 @@ def lm_tpack_image(blocks, P: int, nblk: int):
     img = np.zeros(ln)
     img[off[ok]] = 2.0 * np.asarray(blocks, dtype=np.float64)[:nblk * 1024][ok]
     return img
-
-
-def lm_two_per_cu(spec) -> bool:
-    """csrc/hedge_lm.hip LmKernels::TWO for a net shape (no native library
-    needed; tests/test_lm_cpu.py checks it against native.lm_shape)."""
-    return LM_PAIR_WPS == 2 and spec.hidden == 8 and spec.nin <= 3 and spec.red_width <= 128
 
 
 def lm_gram_geometry(n_local: int, ns_local: int, world: int) -> tuple[int, int]:
@@ -686,7 +676,7 @@ class HipBackend:
             shp = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             if shp is None:
                 raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets up to 174 parameters)")
-            P, R, nblk, two = shp
+            P, R, nblk = shp
             t = self.tcfg
             nw, leaf = lm_pass_schedule(self.n_local, int(os.environ.get("RPH_LM_LEAF", t.lm_leaf_paths)))  # (env: A/B)
             W = max(self.world, 1)
@@ -761,7 +751,7 @@ class HipBackend:
         when the Gram is built redundantly, else the whole reduced block)."""
         if self.world <= 1:
             return 0
-        P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+        P, _, nblk = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
         return 8 * self._lm_greg(False) if self._lm_same_gram else 8 * (nblk * 1024 + lm_tpack_len(P, nblk) + L.LM_RED - L.LM_GBLK_MAX)
 
     def _lm_greg(self, og: bool) -> int:
@@ -870,7 +860,7 @@ class HipBackend:
         P = self.P
 
         def make():
-            _, R, nblk, two = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+            _, R, nblk = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             t, dev = self.tcfg, self.device
             # K instances in one launch: at most 256 / K pass workgroups each, so
             # the whole grid is co-resident (one workgroup per CU) and a pass
@@ -940,7 +930,7 @@ class HipBackend:
         (every rank built the same Gram matrix): only the gradient region
         travels, [g | stats] = 200 doubles (1.6 KB), + the packed output Gram
         in the passes that build it (``og``)."""
-        P, _, nblk, _ = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+        P, _, nblk = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
         if self.lm_mailbox is not None:
             x = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
             if gram:
@@ -1245,7 +1235,7 @@ class TorchBackend:
                     sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
                     Xg, pg, yg = Xn[sub], prn[sub], yn[sub]
             else:
-                nw = lm_pass_wgs(n_loc, lm_two_per_cu(spec))
+                nw = lm_pass_wgs(n_loc)
                 ns_local = max(L.LM_TILE, min(int(t.lm_gram_paths) // world, n_loc))
                 gw = max(1, min(ns_local // L.LM_TILE, nw))
                 ns = gw * L.LM_TILE

@@ -192,7 +192,7 @@ def _bind(lib):
         "rph_train_ticket_fit": (C.c_int, [C.POINTER(TrainDesc), C.c_int, VP]),
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_pnl": (C.c_int, [C.POINTER(PnlDesc), VP]),
-        "rph_lm_shape": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4),
+        "rph_lm_shape": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int)] * 3),
         "rph_lm_eval": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_solve": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_fit": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, VP]),
@@ -341,9 +341,9 @@ def eval_(desc: EvalDesc, stream=None):
 
 
 def lm_shape(nin: int, h: int, nout: int, head: int):
-    """(P, R, Gram blocks, two workgroups per CU) of the LM kernels, or None."""
+    """(P, R, Gram blocks) of the LM kernels, or None."""
     lib = load(required=True)
-    v = [C.c_int() for _ in range(4)]
+    v = [C.c_int() for _ in range(3)]
     if lib.rph_lm_shape(nin, h, nout, head, *[C.byref(x) for x in v]) != 0:
         return None
     return tuple(int(x.value) for x in v)

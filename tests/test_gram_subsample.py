@@ -100,18 +100,3 @@ def test_lm_oracle_same_gram_every_world_size():
         be.fit(w, o, f, data, FitConfig(epochs=8, optimizer="lm", early_stopping=False), seed=0)
         res.append((w.clone(), list(be.lm_last["hist"])))
     assert torch.equal(res[0][0], res[1][0]) and res[0][1] == res[1][1]
-
-
-def test_lm_pair_wps_mirrors_native():
-    """engine.lm_two_per_cu (the oracle's pass grid) follows the library's
-    LmKernels::TWO (RPH_LM_PAIR_WPS) for every LM shape."""
-    from rphedge.engine import lm_two_per_cu
-    from rphedge.models.hedge_mlp import NetSpec
-    from rphedge.ops import native
-
-    if not native.load(required=False):
-        pytest.skip("native library not built")
-    for shape in ((1, 8, 1, 1), (1, 8, 2, 0), (2, 8, 2, 0), (3, 8, 2, 0), (4, 8, 2, 0), (5, 8, 6, 0)):
-        spec = NetSpec(*shape)
-        _, _, _, two = native.lm_shape(*shape)
-        assert bool(two) == lm_two_per_cu(spec), shape
