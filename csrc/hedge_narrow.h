@@ -372,9 +372,25 @@ struct NarrowPairBody {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long long stride = sc.bstep * 128;
     const long long jend = sc.bend * 128 < d.batch ? sc.bend * 128 : d.batch;
+    // PKG (an even output count, so every parameter group has an even size
+    // and offset): the gradient sums as PAIRS of adjacent parameters, updated
+    // by packed fmas whose operands are the per-path values regrouped by
+    // parameter (one 2 x 2 transpose per pair of units) and the other
+    // factor's per-path value broadcast - instead of two scalar fmas per
+    // entry, which the compiler packed with a v_mov gather per operand.  Same
+    // operations per entry in the same order (bitwise the scalar form).
+    // With the backward's own weight reads (below) the path loop issues 555
+    // VALU instructions per iteration instead of 682 (171 -> 92 v_mov, no
+    // AGPR traffic); the pass takes 20.8 / 28.5 µs instead of 21.0 / 29.8
+    // (plain / output-Gram; profiles/r5/pkg_ab/) - the loop is latency-bound
+    // at one wave per SIMD, not issue-bound.
+    constexpr bool PKG = HEAD == HEAD_FREE && NO % 2 == 0 && P % 2 == 0;
     float g[R];
+    nb_f2 gv[PKG ? R / 2 : 1];
 #pragma unroll
     for (int i = 0; i < R; ++i) g[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < (PKG ? R / 2 : 1); ++i) gv[i] = nb_s(0.f);
     const float alpha = d.alpha;
     const float two_inv = 2.f * d.inv_batch;
     const bool pinball = d.loss == LOSS_PINBALL;
@@ -463,10 +479,17 @@ struct NarrowPairBody {
       const nb_f2 ae = nb_f2{fabsf(e.x), fabsf(e.y)} * m;
       const nb_f2 ape = ae * nb_f2{__builtin_amdgcn_rcpf(fmaxf(fabsf(y.x), 1e-7f)),
                                    __builtin_amdgcn_rcpf(fmaxf(fabsf(y.y), 1e-7f))};
-      g[P + 0] += le.x + le.y;
-      g[P + 1] += ae.x + ae.y;
-      g[P + 2] += ape.x + ape.y;
-      g[P + 3] += m.x + m.y;
+      if constexpr (PKG) {
+        gv[P / 2].x += le.x + le.y;
+        gv[P / 2].y += ae.x + ae.y;
+        gv[P / 2 + 1].x += ape.x + ape.y;
+        gv[P / 2 + 1].y += m.x + m.y;
+      } else {
+        g[P + 0] += le.x + le.y;
+        g[P + 1] += ae.x + ae.y;
+        g[P + 2] += ape.x + ape.y;
+        g[P + 3] += m.x + m.y;
+      }
       if constexpr (OGM) {
         if (og) og_accum(img, oacc, a2, pr, m, lane);
       }
@@ -478,6 +501,66 @@ struct NarrowPairBody {
       } else {
 #pragma unroll
         for (int k = 0; k < NO; ++k) dout[k] = dV * pr[k];
+      }
+      if constexpr (PKG) {
+        // the backward's weight reads from their own opaque base: not CSEd
+        // with the forward's, each broadcast has one use (an op_sel operand)
+        uint32_t zb = 0;
+        asm volatile("" : "+v"(zb));
+        const float* __restrict__ Wb = (const float*)__builtin_assume_aligned(W + (zb & ~3u), 16);
+        auto tx = [](nb_f2 a, nb_f2 b) { return nb_f2{a.x, b.x}; };
+        auto ty = [](nb_f2 a, nb_f2 b) { return nb_f2{a.y, b.y}; };
+        auto bx = [](nb_f2 a) { return nb_f2{a.x, a.x}; };
+        auto by = [](nb_f2 a) { return nb_f2{a.y, a.y}; };
+        // g += a.x b.x + a.y b.y per entry: fma(a.x, b.x, fma(a.y, b.y, g))
+        auto acc2 = [&](int e, nb_f2 a, nb_f2 bxp, nb_f2 byp) {
+          gv[e / 2] = nb_fma(bx(a), bxp, nb_fma(by(a), byp, gv[e / 2]));
+        };
+#pragma unroll
+        for (int k = 0; k < NO; k += 2) {
+          const nb_f2 dx = tx(dout[k], dout[k + 1]), dy = ty(dout[k], dout[k + 1]);
+          gv[(S::OB3 + k) / 2] += dx + dy;
+#pragma unroll
+          for (int j = 0; j < H; ++j) acc2(S::OW3 + j * NO + k, a2[j], dx, dy);
+        }
+        nb_f2 dz2[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          nb_f2 da = nb_s(0.f);
+#pragma unroll
+          for (int k = 0; k < NO; ++k) da = nb_fma(nb_s(Wb[S::OW3 + j * NO + k]), dout[k], da);
+          dz2[j] = nb_lrelu_bwd(a2[j], da, alpha);
+        }
+        // layer-2 backward: per unit i two chains (even / odd j), all 2 H
+        // chains interleaved (j outer) - the same sums as the serial form
+        nb_f2 da0[H], da1[H];
+#pragma unroll
+        for (int i = 0; i < H; ++i) da0[i] = da1[i] = nb_s(0.f);
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+#pragma unroll
+          for (int i = 0; i < H; ++i) {
+            if (j & 1) da1[i] = nb_fma(nb_s(Wb[S::OW2 + i * H + j]), dz2[j], da1[i]);
+            else da0[i] = nb_fma(nb_s(Wb[S::OW2 + i * H + j]), dz2[j], da0[i]);
+          }
+#pragma unroll
+        for (int j = 0; j < H; j += 2) {
+          const nb_f2 zx = tx(dz2[j], dz2[j + 1]), zy = ty(dz2[j], dz2[j + 1]);
+          gv[(S::OB2 + j) / 2] += zx + zy;
+#pragma unroll
+          for (int i = 0; i < H; ++i) acc2(S::OW2 + i * H + j, a1[i], zx, zy);
+        }
+        nb_f2 dz1[H];
+#pragma unroll
+        for (int i = 0; i < H; ++i) dz1[i] = nb_lrelu_bwd(a1[i], da0[i] + da1[i], alpha);
+#pragma unroll
+        for (int i = 0; i < H; i += 2) {
+          const nb_f2 zx = tx(dz1[i], dz1[i + 1]), zy = ty(dz1[i], dz1[i + 1]);
+          gv[(S::OB1 + i) / 2] += zx + zy;
+#pragma unroll
+          for (int f = 0; f < NIN; ++f) acc2(S::OW1 + f * H + i, x[f], zx, zy);
+        }
+        continue;
       }
 #pragma unroll
       for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k].x + dout[k].y;
@@ -506,6 +589,13 @@ struct NarrowPairBody {
         g[S::OB1 + i] += dz1.x + dz1.y;
 #pragma unroll
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = nb_acc(g[S::OW1 + f * H + i], x[f], dz1);
+      }
+    }
+    if constexpr (PKG) {
+#pragma unroll
+      for (int i = 0; i < R / 2; ++i) {
+        g[2 * i] = gv[i].x;
+        g[2 * i + 1] = gv[i].y;
       }
     }
     RPH_STAMP_BODY(5);  // path loop done
