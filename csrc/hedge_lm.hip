@@ -374,6 +374,18 @@ RPH_INLINE double lm_dp_sum_wave(const LmDpDesc& x, const unsigned seq, const in
 // workgroups of the output-Gram part of k_lm_reduce (64 packed entries each)
 constexpr int lm_og_wgs(int NU) { return NU <= LM_OG_MAX ? (NU * (NU + 1) / 2 + 63) / 64 : 0; }
 
+// Gram slabs up to this many (the multi-start exploration's 16-workgroup
+// instances): k_lm_reduce sums each Gram entry in ONE thread (1,024 entries
+// per workgroup) instead of 16 threads + an LDS combine - the same adds in
+// the same order, 16 x fewer workgroups (16 instances: 720 instead of 3,120)
+constexpr int LM_TPE_MAX = 16;
+__host__ __device__ constexpr int lm_gram_red_wgs(int ng, int gram_wgs) { return gram_wgs <= LM_TPE_MAX ? ng / 1024 : ng / 64; }
+// the gradient packet likewise, for <= 16 packet rows (no fused exchange):
+// one workgroup, thread = entry, the rows' contiguous-halves tree in registers
+__host__ __device__ constexpr int lm_pk_red_wgs(int R, int num_wgs, int dp_fused) {
+  return (num_wgs <= LM_TPE_MAX && !dp_fused) ? 1 : R / 4;
+}
+
 
 template <int P, int R, int NU>
 __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
@@ -388,11 +400,13 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
   const float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NG;
   const float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x >= NG / 64 + R / 4) {
+  const int NGW = lm_gram_red_wgs(NG, lm.gram_wgs);       // Gram workgroups
+  const int NPW = lm_pk_red_wgs(R, lm.num_wgs, lm.dp_fused);  // packet workgroups
+  if ((int)blockIdx.x >= NGW + NPW) {
     // full-batch output-layer Gram (packed upper triangle, mean over every
     // path); a pass that did not build it marks entry 0 with -1
     const bool og_pass = lm.out_gram && pass > lm.passes - LM_OUTG_TAIL;
-    const int ob = blockIdx.x - (NG / 64 + R / 4);
+    const int ob = blockIdx.x - (NGW + NPW);
     if (!og_pass) {
       if (ob == 0 && tid == 0) red[LM_RED_OUTG] = -1.0;
       return;
@@ -445,7 +459,37 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     }
     return;
   }
-  if ((int)blockIdx.x < NG / 64) {
+  // this entry's place in the solve's tile store (strictly lower only)
+  auto tpack = [&](const int e, const double v) {
+    if constexpr (LmTPack<P>::ON) {
+      using TG = TileGrid<P>;
+      const int b = e >> 10, f = e & 1023;
+      int mb = 0, rem = b;
+      while (rem >= TG::NBG - mb) rem -= TG::NBG - mb++;
+      const int q = f >> 6, h = (f >> 5) & 1;
+      const int lo = 32 * mb + (q & 3) + 4 * h + 8 * (q >> 2), hi = 32 * (mb + rem) + (f & 31);
+      if (lo < hi && hi < P) red[LmTPack<P>::OFF + TG::tidx(hi >> 4, lo >> 4) * 256 + tg_off(hi & 15, lo & 15)] = 2.0 * v;
+    }
+  };
+  if (NGW == NG / 1024 && (int)blockIdx.x < NGW) {
+    // <= 16 slabs: thread = entry, the 16 "group" partial sums (slab g or 0)
+    // combined in the LDS form's order: even groups, odd groups, their sum
+    const int e = blockIdx.x * 1024 + tid;
+    const float* col = slab_g + e;
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      const double p0 = q < lm.gram_wgs ? (0.0 + (double)col[(size_t)q * NG]) + 0.0 : 0.0 + 0.0;
+      const double p1 = q + 1 < lm.gram_wgs ? (0.0 + (double)col[(size_t)(q + 1) * NG]) + 0.0 : 0.0 + 0.0;
+      a += p0;
+      b += p1;
+    }
+    const double v = (a + b) * (double)lm.inv_ns;
+    red[e] = v;
+    tpack(e, v);
+    return;
+  }
+  if ((int)blockIdx.x < NGW) {
     // Gram: workgroup handles entries [64 b, 64 b + 64); thread (g, l) sums
     // the slabs g, g + 16, ... of entry 64 b + l (every load of a 64-slab
     // reduction in flight at once: 4 per thread), the 16 partial sums
@@ -471,17 +515,7 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       }
       const double v = (a + b) * (double)lm.inv_ns;
       red[e] = v;
-      if constexpr (LmTPack<P>::ON) {
-        // this entry's place in the solve's tile store (strictly lower only)
-        using TG = TileGrid<P>;
-        const int b = e >> 10, f = e & 1023;
-        int mb = 0, rem = b;
-        while (rem >= TG::NBG - mb) rem -= TG::NBG - mb++;
-        const int q = f >> 6, h = (f >> 5) & 1;
-        const int lo = 32 * mb + (q & 3) + 4 * h + 8 * (q >> 2), hi = 32 * (mb + rem) + (f & 31);
-        if (lo < hi && hi < P)
-          red[LmTPack<P>::OFF + TG::tidx(hi >> 4, lo >> 4) * 256 + tg_off(hi & 15, lo & 15)] = 2.0 * v;
-      }
+      tpack(e, v);
     }
     return;
   }
@@ -491,7 +525,29 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
   // first - a contiguous-halves tree over the rows, so a rank's rows (a
   // contiguous run of leaves, LmDesc.leaf_blocks) form a complete subtree and
   // the sum over the ranks (lm_dp_sum_wave) finishes the same tree
-  const int pw = blockIdx.x - NG / 64;
+  if (NPW == 1) {
+    // <= 16 rows: thread = entry; the LDS tree below puts row r at position
+    // bitrev8(r) = 16 bitrev4(r) and adds position p + st to p for st = 128 ..
+    // 1 - on these rows a pairwise tree over bitrev4 positions, then +0.0 for
+    // the all-zero rest (the same adds, so the same bits)
+    const int i = tid;
+    if (i < P + 4) {
+      double a[16];
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        const int r = (int)(__builtin_bitreverse32((unsigned)p) >> 28);
+        a[p] = r < lm.num_wgs ? (double)slab_b[(size_t)r * R + i] : 0.0;
+      }
+#pragma unroll
+      for (int st = 8; st >= 1; st >>= 1)
+#pragma unroll
+        for (int p = 0; p < st; ++p) a[p] += a[p + st];
+      const int e = i < P ? i : LM_NPMAX + i - P;
+      red[LM_GBLK_MAX + e] = a[0] + 0.0;
+    }
+    return;
+  }
+  const int pw = blockIdx.x - NGW;
   const int k = tid & 3, grp = tid >> 2;
   const int i = pw * 4 + k;
   const int row = (int)(__builtin_bitreverse32((unsigned)grp) >> 24);
@@ -1354,7 +1410,9 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK, K::Body::NU)) return rc; \
     if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R, K::Body::NU>), dim3(lm->red_wgs, lm->inst), dim3(1024), 0, s, \
+    const int rg = lm_gram_red_wgs(LmShape<K::S::P>::NBLK * 1024, lm->gram_wgs) +                   \
+                   lm_pk_red_wgs(K::S::R, lm->num_wgs, lm->dp_fused) + lm_og_wgs(K::Body::NU);             \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R, K::Body::NU>), dim3(rg, lm->inst), dim3(1024), 0, s, \
                        *lm, red_new, pass);                                                     \
     return (int)hipGetLastError();                                                              \
   }
