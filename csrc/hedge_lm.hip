@@ -874,12 +874,10 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
         if (i >= P - on) wd += lds[64 * 65 + i - (P - on)];
       } else if (i == lm.bias_index) {
         // exact Newton step on this bias alone (the loss is quadratic in it):
-        // d = -g_i / (2 G_ii), G_ii from the diagonal 32x32 Gram block
-        const int kb = i >> 5, ri = i & 31;
-        int b = 0;
-        for (int q = 0; q < kb; ++q) b += LS::NB - q;
-        const int q = (ri >> 3) * 4 + (ri & 3), hh = (ri >> 2) & 1;
-        const double gii = src[(size_t)b * 1024 + q * 64 + hh * 32 + ri];
+        // d = -g_i / (2 G_ii); the bias is the bond holding's, dV / db = B_{t+1}
+        // on every path, so G_ii = B^2 exactly (not the subsample Gram's
+        // rounded entry): d = -mean(e) / B
+        const double gii = (double)d.bond * (double)d.bond;
         if (gii > 0.0) wd -= g[i] / (2.0 * gii);
       }
       const float w = (float)wd;

@@ -196,6 +196,35 @@ typedef short nb_s16x4 __attribute__((ext_vector_type(4)));
 typedef short nb_s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) nb_s16x4 nb_lds_s16x4;
 
+// bf16 hi / lo image of a [row][unit] fp32 matrix in LDS for the matrix
+// cores (rows = paths): hi = bf16(u), lo = bf16(u - hi), 16 significant bits;
+// a row is [hi: NU units | lo: NU units] (+ padding in PITCH).  nb_img_put
+// writes units [c0, c0 + 4) of a row; nb_img_frag reads the MFMA fragment of
+// unit block ub (ub + NU / 32: its lo half), K-step s (16 rows): unit
+// 32 ub + lane % 32 of the 8 rows 16 s + 8 (lane / 32) .. + 7, by two
+// transposing reads (ds_read_b64_tr_b16).  G = sum_rows u u^T is then
+// hi hi^T + hi lo^T + lo hi^T on v_mfma_f32_32x32x16_bf16.
+template <int PITCH, int NU>
+RPH_INLINE void nb_img_put(unsigned char* img, int row, int c0, float u0, float u1, float u2, float u3) {
+  const __bf16 h0 = (__bf16)u0, h1 = (__bf16)u1, h2 = (__bf16)u2, h3 = (__bf16)u3;
+  const nb_bf16x4 h = {h0, h1, h2, h3};
+  const nb_bf16x4 l = {(__bf16)(u0 - (float)h0), (__bf16)(u1 - (float)h1), (__bf16)(u2 - (float)h2),
+                       (__bf16)(u3 - (float)h3)};
+  *(nb_bf16x4*)(img + row * PITCH + 2 * c0) = h;
+  *(nb_bf16x4*)(img + row * PITCH + 2 * (NU + c0)) = l;
+}
+template <int PITCH>
+RPH_INLINE nb_bf16x8 nb_img_frag(const unsigned char* img, int s, int ub, int lane) {
+  const int grp = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c0 = 32 * ub + 16 * (grp & 1), hh = grp >> 1;
+  const int off = (16 * s + 8 * hh + q) * PITCH + (c0 + 4 * p) * 2;
+  const nb_s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off));
+  const nb_s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off + 4 * PITCH));
+  // whole-vector bit cast: inserting the elements one by one as
+  // bit_cast<__bf16>(r[e]) was miscompiled into splats of r[0]
+  return __builtin_bit_cast(nb_bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 template <int NIN, int H, int NO, int HEAD, bool OG = false>
 struct NarrowPairBody {
   static constexpr int WAVES_PER_SIMD = 1;  // one pass workgroup per CU (256 VGPRs + AGPRs per lane)
@@ -282,28 +311,12 @@ struct NarrowPairBody {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // this lane's unit slice [c0, c0 + 4) of row `row` of the image: hi at
-  // units c0.., lo at NUP + c0..
+  // this lane's unit slice [c0, c0 + 4) of row `row` of the image (nb_img_put)
   RPH_INLINE static void og_put(unsigned char* img, int row, int c0, float u0, float u1, float u2, float u3) {
-    const __bf16 h0 = (__bf16)u0, h1 = (__bf16)u1, h2 = (__bf16)u2, h3 = (__bf16)u3;
-    const nb_bf16x4 h = {h0, h1, h2, h3};
-    const nb_bf16x4 l = {(__bf16)(u0 - (float)h0), (__bf16)(u1 - (float)h1), (__bf16)(u2 - (float)h2),
-                         (__bf16)(u3 - (float)h3)};
-    *(nb_bf16x4*)(img + row * OG_PITCH + 2 * c0) = h;
-    *(nb_bf16x4*)(img + row * OG_PITCH + 2 * (NUP + c0)) = l;
+    nb_img_put<OG_PITCH, NUP>(img, row, c0, u0, u1, u2, u3);
   }
-  // MFMA fragment of unit block ub (ub + NUP / 32: its lo half), K-step s (16
-  // paths): unit 32 ub + lane % 32 of the 8 paths 16 s + 8 (lane / 32) .. + 7
-  // (two transposing reads)
   RPH_INLINE static nb_bf16x8 og_frag(const unsigned char* img, int s, int ub, int lane) {
-    const int grp = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const int c0 = 32 * ub + 16 * (grp & 1), hh = grp >> 1;
-    const int off = (16 * s + 8 * hh + q) * OG_PITCH + (c0 + 4 * p) * 2;
-    const nb_s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off));
-    const nb_s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((nb_lds_s16x4*)(img + off + 4 * OG_PITCH));
-    // whole-vector bit cast: inserting the elements one by one as
-    // bit_cast<__bf16>(r[e]) was miscompiled into splats of r[0]
-    return __builtin_bit_cast(nb_bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+    return nb_img_frag<OG_PITCH>(img, s, ub, lane);
   }
 
   // one 128-path iteration of the output-layer Gram: u of both paths

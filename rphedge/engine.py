@@ -1438,9 +1438,12 @@ class TorchBackend:
                     w_best = lw.clone()
                     w_best[P - n_out:] += r[0]
                     Lb, self.lm_out_dl, out_ok = lL, r[1], True
-        if not out_ok and bi >= 0 and float(G[bi, bi]) > 0.0:
+        # (the bond holding's bias: dV/db = B on every path, so G_bb = B^2
+        # exactly - as k_lm_solve, independent of the subsample Gram's rounding)
+        gbb = float(np.float32(data.bond_next)) ** 2
+        if not out_ok and bi >= 0 and gbb > 0.0:
             w_best = w_best.clone()
-            w_best[bi] -= g[bi] / (2.0 * G[bi, bi])
+            w_best[bi] -= g[bi] / (2.0 * gbb)
         w32 = w_best.to(torch.float32)
         wts[:P] = w32
         wts[L.PMAX:L.PMAX + P] = w32
