@@ -573,8 +573,7 @@ struct NarrowPairBody {
 #pragma unroll
           for (int f = 0; f < NIN; ++f) acc2(S::OW1 + f * H + i, x[f], zx, zy);
         }
-        continue;
-      }
+      } else {
 #pragma unroll
       for (int k = 0; k < NO; ++k) g[S::OB3 + k] += dout[k].x + dout[k].y;
       nb_f2 dz2[H];
@@ -603,6 +602,7 @@ struct NarrowPairBody {
 #pragma unroll
         for (int f = 0; f < NIN; ++f) g[S::OW1 + f * H + i] = nb_acc(g[S::OW1 + f * H + i], x[f], dz1);
       }
+      }  // (PKG)
     }
     if constexpr (PKG) {
 #pragma unroll
