@@ -118,6 +118,7 @@ class TrainingParams:
                                      # in the value) instead of the bond bias alone
     lm_out_mu: float = 1e-5          # ... its relative Marquardt damping: directions of the output Gram below
                                      # ~1e-5 of its scale are rounding noise of the fp32-accumulated matrix
+    lm_ridge: float = 1e-10          # LM systems (the fit's and the output step's): + this x the mean diagonal
     lm_renorm: bool = False          # later dates: the warm start's first layer re-expressed for the date's input
                                      # standardisation (the previous hedge as a function of the raw state)
     lm_starts: int = 1               # first date: multi-start LM exploration, starts per rank (1: off)
