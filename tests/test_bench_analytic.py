@@ -181,3 +181,19 @@ def test_levy_basket_anchor():
     pay = ((torch.tensor(w, dtype=torch.float64)[:, None] * p.S[-1].double()).sum(0) - 1.0).clamp_min(0)
     assert a["levy_delta"]["pnl_std"] < 0.1 * float(pay.std())
     assert a["price"] == pytest.approx(float(pay.mean()) * math.exp(-0.05), rel=0.03)
+
+
+def test_bench_lm_knobs_reach_the_backend():
+    """--lm-ridge / --lm-out-mu travel bench -> TrainingParams -> the backend's
+    TrainConfig (the defaults are the engine's: 1e-10 / 1e-5)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from rphedge.api import HedgeRun
+
+    a = bench.parse(["--preset", "euro1_cpu"])
+    assert a.lm_ridge == 1e-10 and a.lm_out_mu == 1e-5
+    a = bench.parse(["--preset", "euro1_cpu", "--optimizer", "lm", "--lm-ridge", "1e-6", "--lm-out-mu", "1e-3"])
+    cfg = bench.build_run(a, 1)
+    assert cfg.train.lm_ridge == 1e-6 and cfg.train.lm_out_mu == 1e-3
+    run = HedgeRun(cfg).build()
+    assert run.backend.tcfg.lm_ridge == 1e-6 and run.backend.tcfg.lm_out_mu == 1e-3
