@@ -117,7 +117,9 @@ class TrainingParams:
     lm_out_fix: bool = False         # LM fits end with the exact Newton step on the whole output layer (linear
                                      # in the value) instead of the bond bias alone
     lm_out_mu: float = 1e-5          # ... its relative Marquardt damping: directions of the output Gram below
-                                     # ~1e-5 of its scale are rounding noise of the fp32-accumulated matrix
+                                     # ~1e-5 of its scale are rounding noise of the bf16 hi/lo products - and
+                                     # the net's own collinear directions (an exact fp32 Gram at 1e-7 blew up
+                                     # basket5 seeds: BENCHMARKS.md round 5)
     lm_ridge: float = 1e-10          # LM systems (the fit's and the output step's): + this x the mean diagonal
     lm_renorm: bool = False          # later dates: the warm start's first layer re-expressed for the date's input
                                      # standardisation (the previous hedge as a function of the raw state)
