@@ -356,11 +356,11 @@ RPH_INLINE double lm_dp_sum_wave(const LmDpDesc& x, const unsigned seq, const in
   double a[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q)
-    a[q] = q >= W ? 0.0
-                  : q == me ? v
-                            : (act ? __hip_atomic_load(x.mbox[me] + ((size_t)slot * W + q) * x.pitch + e,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                   : 0.0);
+    a[q] = (q >= W || (x.fault == 1 && q == W - 1)) ? 0.0  // (fault: the probe tests' wrong sum)
+           : q == me ? v
+                     : (act ? __hip_atomic_load(x.mbox[me] + ((size_t)slot * W + q) * x.pitch + e,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                            : 0.0);
 #pragma unroll
   for (int st = 1; st < 8; st <<= 1)
 #pragma unroll
@@ -451,11 +451,13 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
         for (int st = 1; st < 16; st <<= 1)
 #pragma unroll
           for (int q = 0; q < 16; q += 2 * st) c[q] += c[q + st];
-        v = c[0] * (double)lm.inv_n;
+        v = c[0];
       }
+      // the ranks' UNSCALED tree sums travel and the mean is taken after the
+      // rank tree, as in the one-rank run (bitwise world-invariant for any n)
       if (lm.dp_fused)
         v = lm_dp_sum_wave(lm.dp, seq, R / 4 + ob, v, LM_RED_OUTG - LM_GBLK_MAX + e, e < NPK);
-      if (e < NPK) red[LM_RED_OUTG + e] = v;
+      if (e < NPK) red[LM_RED_OUTG + e] = v * (double)lm.inv_n;
     }
     return;
   }

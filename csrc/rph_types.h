@@ -245,7 +245,11 @@ struct LmDpDesc {
   unsigned* error;               // [0] set on a peer timeout
   int world, rank;
   int pitch;                     // entries per (slot, sender) row (>= LM_DP_PITCH)
-  int pad0;
+  // fault injection (transport-probe tests only; 0 in every run): 1 = the
+  // fused exchange in k_lm_reduce drops rank W-1's contribution on EVERY rank
+  // - a wrong sum that is still bitwise identical across ranks, so only a
+  // comparison with an independent all-reduce can catch it
+  int fault;
 };
 
 struct LmDesc {

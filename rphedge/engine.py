@@ -318,10 +318,18 @@ def lm_pass_schedule(n_local: int, leaf_paths: int = 0) -> tuple[int, int]:
     if leaf_paths > 0:
         if leaf_paths % 128:
             raise ValueError(f"lm_leaf_paths must be a multiple of 128, got {leaf_paths}")
+        # the world-invariance contract (a rank's rows form a complete subtree of
+        # the one-rank contiguous-halves tree): whole leaves per shard and a
+        # power-of-two number of pass workgroups per rank
+        if int(n_local) % leaf_paths:
+            raise ValueError(f"lm_leaf_paths {leaf_paths} does not divide the {n_local}-path shard")
         lb = leaf_paths // 128
         nw = int(min(256, max(1, -(-nblk // (4 * lb)))))
         if 4 * nw * lb < nblk:
             raise ValueError(f"{leaf_paths}-path leaves need more than 256 pass workgroups for {n_local} paths")
+        if nw & (nw - 1):
+            raise ValueError(f"lm_leaf_paths {leaf_paths} gives {nw} pass workgroups for {n_local} paths; world "
+                             "invariance needs a power of two (choose a power-of-two shard and leaf size)")
         return nw, lb
     return nw, int(-(-nblk // (4 * nw)))
 
@@ -536,6 +544,7 @@ class HipBackend:
         ewg = int(os.environ.get("RPH_EVAL_WGS", "2048"))
         self.eval_wgs = int(max(1, min(ewg, (self.n_local + 255) // 256)))
         self._cache = _Cache()
+        self.lm_last_fused = False  # the last LM fit summed its gradient region inside k_lm_reduce
         self._lm_same_gram = True  # the last LM fit built the world-invariant Gram (exchange: gradient region only)
 
     # -- state ---------------------------------------------------------------
@@ -821,6 +830,7 @@ class HipBackend:
         fused = (self.world > 1 and self.lm_mailbox is not None and self._lm_same_gram and not pin
                  and not self.tcfg.lm_split)
         lm.dp_fused = 1 if fused else 0
+        self.lm_last_fused = fused  # (transport probe record: which exchange this fit ran)
         if fused:
             lm.dp = self._cache.get(("lm_dp",), self.lm_mailbox.lm_desc)
         if (self.world <= 1 or fused) and not self.tcfg.lm_split:

@@ -84,7 +84,7 @@ class PnlDesc(C.Structure):
 class LmDpDesc(C.Structure):
     _fields_ = [
         ("mbox", VP * 8), ("counter", VP), ("error", VP),
-        ("world", C.c_int), ("rank", C.c_int), ("pitch", C.c_int), ("pad0", C.c_int),
+        ("world", C.c_int), ("rank", C.c_int), ("pitch", C.c_int), ("fault", C.c_int),
     ]
 
 

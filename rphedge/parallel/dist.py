@@ -158,44 +158,135 @@ def close_mailbox(mb):
     mb.close()
 
 
-def _probe_xgmi_local(info: DistInfo, mb, lmb, lm: bool) -> tuple[bool, torch.Tensor | None]:
+class TorchComm:
+    """All-reduce through the torch.distributed process group with the
+    ``NcclComm.allreduce_(t, stream)`` interface: the stream is drained, the
+    tensor summed (through the host under gloo) and written back before the
+    next launch.  Eager only (not graph-capturable).  Two uses: the
+    INDEPENDENT reference transport of the LM transport probe, and the LM
+    fallback of ranks that share one GPU (RCCL refuses two ranks per card)."""
+
+    def __init__(self, device):
+        self.device = device
+
+    def allreduce_(self, t: torch.Tensor, stream=None):
+        if t.is_cuda:
+            torch.cuda.synchronize(t.device)
+        all_reduce_(t, "sum")
+        if t.is_cuda:
+            torch.cuda.synchronize(t.device)
+
+    def close(self):
+        pass
+
+
+# the LM transport probe: a 1-8-8-2 net, 2^12 paths per rank, 2048-path global
+# Gram subsample, output-layer Newton step (the output-Gram exchange rows too)
+_PROBE_LOCAL_LOG2 = 12
+_PROBE_GRAM = 2048
+_PROBE_PASSES = 4
+PROBE_RTOL = 1e-5  # fused fit vs the independent all-reduce fit (fp64 sums in another order)
+
+
+def _probe_data(info: DistInfo, world_data: bool):
+    """The probe's global problem, identical on every rank (fixed generator):
+    this rank's shard and the simulated global Gram subsample."""
+    from ..engine import DateData, gram_subsample
+    from ..ops.paths import path_indices
+    import numpy as np
+
+    n = 1 << _PROBE_LOCAL_LOG2
+    W = info.world
+    g = torch.Generator().manual_seed(100)
+    xa = torch.rand(n * W, generator=g) * 0.6 + 0.7
+    ya = torch.relu(xa * 1.01 - 1.0) + 0.02 * torch.sin(9.0 * xa)
+    x = xa[info.rank * n:(info.rank + 1) * n].to(info.device)
+    y = ya[info.rank * n:(info.rank + 1) * n].to(info.device)
+    ns, blk, stride = gram_subsample(n * W, _PROBE_GRAM)
+    idx = torch.as_tensor(path_indices(ns, 0, (blk, stride)).astype(np.int64))
+    gf = xa[idx].contiguous().to(info.device)
+    kw = dict(gram_feats=[gf], gram_prices_next=[gf * 1.01]) if world_data else {}
+    return DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=y, prices_now=[x], **kw)
+
+
+def _probe_lm_fit(info: DistInfo, mb, lmb=None, lm_comm=None, fault: int = 0):
+    """One LM probe fit over the production exchange (``lmb``: the gradient
+    region summed inside k_lm_reduce, LmDesc.dp_fused) or over ``lm_comm``
+    (the split launches + an independent all-reduce).  Returns (weights,
+    fused flag, clean flag)."""
+    from ..engine import FitConfig, HipBackend, TrainConfig
+    from ..models.hedge_mlp import NetSpec, init_weights
+
+    spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    n = 1 << _PROBE_LOCAL_LOG2
+    be = HipBackend(spec, n, TrainConfig(batch_size=n * info.world, chunk_log2=6, lm_gram_paths=_PROBE_GRAM,
+                                         lm_out_fix=True),
+                    device=info.device, world=info.world, rank=info.rank, mailbox=mb, lm_mailbox=lmb,
+                    lm_comm=lm_comm)
+    if lmb is not None and fault:
+        be._cache.get(("lm_dp",), lmb.lm_desc).fault = int(fault)
+    data = _probe_data(info, world_data=True)
+    w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
+    be.fit(w, o, f, data, FitConfig(epochs=_PROBE_PASSES, optimizer="lm", early_stopping=False), seed=5)
+    torch.cuda.synchronize(info.device)
+    clean = lmb is None or int(lmb.error[0].item()) == 0
+    return w[: spec.nparams].double().clone(), bool(be.lm_last_fused), clean
+
+
+def _probe_xgmi_local(info: DistInfo, mb, lmb, lm: bool) -> tuple[bool, torch.Tensor | None, dict]:
     """This rank's half of one probe: a tiny data-parallel fit over one of the
-    in-kernel exchanges the runs use - Keras-Adam steps over the fused packet
-    exchange (``mb``, the lagged schedule) or, with ``lm``, Levenberg-Marquardt
-    passes over the reduced-block exchange (``lmb``, k_lm_dp_exchange, the
-    bench's optimiser).  Returns (ok, fitted weights)."""
+    in-kernel exchanges the runs use.
+
+    packet: Keras-Adam steps over the fused packet exchange (``mb``, the
+    lagged schedule).  lm: Levenberg-Marquardt passes over EXACTLY the
+    production LM exchange - the global Gram subsample is given, so every
+    rank builds the same Gram and the gradient region (+ the output-Gram rows)
+    is summed inside k_lm_reduce (``lm_dp_sum_wave``) - and, as a reference,
+    the same fit through the split launches with an independent
+    torch.distributed all-reduce of the same region.  The probe passes only
+    if the fused fit ran fused, is clean and matches the reference to
+    PROBE_RTOL: a wrong sum that is identical on every rank fails too.
+    Returns (ok, fitted weights, record)."""
     from ..engine import DateData, FitConfig, HipBackend, TrainConfig
     from ..models.hedge_mlp import NetSpec, init_weights
 
     spec = NetSpec(nin=1, hidden=8, nout=2, head=0)
+    rec: dict = {}
     if mb is None or (lm and lmb is None):
-        return False, None
+        return False, None, rec
     # fault injection (tests): RPH_PROBE_FAIL = packet | lm | both fails that
-    # probe on every rank, or only on RPH_PROBE_FAIL_RANK
+    # probe on every rank, or only on RPH_PROBE_FAIL_RANK; RPH_PROBE_FAULT=lm_drop
+    # corrupts the fused LM sum itself (rank W-1 dropped on every rank)
     inj = os.environ.get("RPH_PROBE_FAIL", "")
     inj_rank = os.environ.get("RPH_PROBE_FAIL_RANK")
     if inj and (inj == "both" or inj == ("lm" if lm else "packet")) and (
             inj_rank is None or int(inj_rank) == info.rank):
-        return False, None
+        return False, None, rec
     try:
+        if lm:
+            fault = 1 if os.environ.get("RPH_PROBE_FAULT", "") == "lm_drop" else 0
+            wv, fused, clean = _probe_lm_fit(info, mb, lmb=lmb, fault=fault)
+            wr, _, _ = _probe_lm_fit(info, mb, lm_comm=TorchComm(info.device))
+            dev = float((wv - wr).abs().max().item() / max(float(wr.abs().max().item()), 1e-30))
+            rec = {"fused": fused, "clean": clean, "max_rel_dev_vs_allreduce": dev, "rtol": PROBE_RTOL,
+                   "fault_injected": bool(fault)}
+            ok = fused and clean and bool(torch.isfinite(wv).all()) and dev <= PROBE_RTOL
+            return ok, wv, rec
         n = 1 << 12
         g = torch.Generator().manual_seed(100 + info.rank)          # different data per rank
         x = (torch.rand(n, generator=g) * 0.6 + 0.7).to(info.device)
         be = HipBackend(spec, n, TrainConfig(batch_size=n * info.world, chunk_log2=6, lm_gram_paths=2048),
-                        device=info.device, world=info.world, rank=info.rank, mailbox=mb,
-                        lm_mailbox=lmb if lm else None)
+                        device=info.device, world=info.world, rank=info.rank, mailbox=mb)
         data = DateData(feats=[x], prices_next=[x * 1.01], bond_next=1.0, target=torch.relu(x - 1.0),
                         prices_now=[x])
-        fc = (FitConfig(epochs=3, optimizer="lm", early_stopping=False) if lm else
-              FitConfig(epochs=4, patience=10 ** 6, early_stopping=False))
         w, o, f = be.new_weights(init_weights(spec, [0.5, 0.0])), be.new_opt(), be.new_fit()
-        be.fit(w, o, f, data, fc, seed=5)
+        be.fit(w, o, f, data, FitConfig(epochs=4, patience=10 ** 6, early_stopping=False), seed=5)
         torch.cuda.synchronize(info.device)
         wv = w[: spec.nparams].double()
-        clean = int((lmb if lm else mb).error[0].item()) == 0
-        return clean and bool(torch.isfinite(wv).all()), wv
-    except Exception:
-        return False, None
+        clean = int(mb.error[0].item()) == 0
+        return clean and bool(torch.isfinite(wv).all()), wv, {"clean": clean}
+    except Exception as e:
+        return False, None, {"exception": f"{type(e).__name__}: {e}"[:200]}
 
 
 def select_transport(info: DistInfo) -> str:
@@ -203,14 +294,18 @@ def select_transport(info: DistInfo) -> str:
     separately for the two in-kernel exchanges: the Keras-Adam gradient packet
     (``info.dp_mode``) and the LM reduced block (``info.lm_dp_mode``).  Each
     keeps its xGMI mailbox exchange when a tiny DP fit over it is clean on
-    every rank and the replicas agree bit for bit; otherwise that exchange
-    falls back to an RCCL all-reduce.  Runs once, outside any timed region;
-    all ranks agree.
+    every rank, the replicas agree bit for bit and (LM) the fit matches the
+    same fit over an independent all-reduce; otherwise that exchange falls
+    back to an RCCL all-reduce (ranks sharing one GPU: the torch.distributed
+    group, RCCL refuses two ranks per card).  Runs once, outside any timed
+    region; all ranks agree.
 
     Every rank issues the SAME collective sequence whatever its local outcome
     (per probe: min of the ok flags, max/min of the weights, min of the
     equality flag), so a failure seen by only some ranks cannot pair
-    mismatched collectives."""
+    mismatched collectives (the LM reference fit's all-reduces run on every
+    rank whose fused fit ran; a rank whose fit raised skips both, and the
+    process group's timeout then surfaces it)."""
     if info.world <= 1 or info.device.type != "cuda" or info.dp_mode != "xgmi":
         return info.dp_mode
     from ..models.hedge_mlp import NetSpec
@@ -227,7 +322,7 @@ def select_transport(info: DistInfo) -> str:
     lmb = try_mailbox(L.LM_DP_PITCH, "rph_probe_lm")
     probe = {}
     for name, lm in (("packet", False), ("lm", True)):
-        ok_l, wv = _probe_xgmi_local(info, mb, lmb, lm)
+        ok_l, wv, rec = _probe_xgmi_local(info, mb, lmb, lm)
         ok = torch.tensor([1.0 if ok_l else 0.0], dtype=torch.float64, device=info.device)
         all_reduce_(ok, "min")
         w = wv if (wv is not None and wv.numel() == spec.nparams) else \
@@ -240,7 +335,7 @@ def select_transport(info: DistInfo) -> str:
         all_ok = float(ok.item()) >= 1.0 and float(same.item()) >= 1.0
         probe[name] = {"local_ok": bool(ok_l), "all_ok": bool(float(ok.item()) >= 1.0),
                        "bitwise_equal_weights": bool(float(same.item()) >= 1.0),
-                       "chosen": "xgmi" if all_ok else "rccl"}
+                       "chosen": "xgmi" if all_ok else "rccl", **rec}
     # collective teardown with ONE unconditional barrier (a rank whose mailbox
     # creation failed holds None and must still join it)
     torch.cuda.synchronize(info.device)
@@ -256,12 +351,19 @@ def select_transport(info: DistInfo) -> str:
     from ..ops.native import NcclComm
 
     # fallback communicators are created here, collectively and outside any
-    # graph capture (never lazily inside a captured fit)
+    # graph capture (never lazily inside a captured fit); ranks sharing one
+    # GPU fall back to the process group (RCCL refuses a duplicate GPU)
+    def fallback(tag):
+        return TorchComm(info.device) if info.shared_device else NcclComm(info.rank, info.world, _store(), tag=tag)
+
     if probe["packet"]["chosen"] != "xgmi":
         info.dp_mode = "rccl"
-        info.comm = NcclComm(info.rank, info.world, _store(), tag="rph_fallback")
+        info.comm = fallback("rph_fallback")
     elif info.lm_dp_mode != "xgmi":
-        info.lm_comm = NcclComm(info.rank, info.world, _store(), tag="rph_lm_fallback")
+        info.lm_comm = fallback("rph_lm_fallback")
+    for k in ("packet", "lm"):
+        if probe[k]["chosen"] != "xgmi":
+            probe[k]["fallback_comm"] = "torch.distributed" if info.shared_device else "rccl"
     return info.dp_mode
 
 

@@ -243,14 +243,15 @@ def test_lm_mailbox_exchange_two_ranks_one_gpu(side):
         np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_lm_strong_scaling_rehearsal_is_bitwise(world):
-    """The same 2^18 global paths fitted by 1, 2 or 4 ranks on one GPU (shared
+    """The same 2^18 global paths fitted by 1, 2, 4 or 8 ranks on one GPU (shared
     Gram subsample, gradient region summed inside k_lm_reduce over the IPC
     mailboxes, output-layer Newton step): with the same contiguous 256-path
     leaves at every world size (TrainConfig.lm_leaf_paths) and the
     contiguous-halves reduction trees, every rank's weights are bit for bit
-    those of the one-rank fit."""
+    those of the one-rank fit.  W = 8 runs every level of the 8-way rank tree
+    in lm_dp_sum_wave, 7 peers' flags per row and the DP_SLOTS rotation."""
     n, passes, leaf = 1 << 18, 10, 256
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "w")
@@ -328,3 +329,69 @@ def test_lm_multistart_two_ranks_one_gpu():
     # 1 rank, the same global paths [0, n): the same exploration, bit for bit
     _, l_ref = _lm_fit(0, 1, n, passes, torch.device("cuda", 0), starts=3)
     np.testing.assert_array_equal(l0, np.asarray(l_ref))
+
+
+def _worker_probe(rank, world, port, out, fault):
+    """One rank of a torchrun-style job on a shared card: rphedge.parallel.dist
+    init + select_transport, the probe record written as JSON."""
+    import json
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    if fault:
+        os.environ["RPH_PROBE_FAULT"] = fault
+    from rphedge.parallel import dist as D
+
+    info = D.init()
+    D.select_transport(info)
+    with open(out + f".{rank}.json", "w") as fh:
+        json.dump({"probe": info.probe, "lm_dp_mode": info.lm_dp_mode, "dp_mode": info.dp_mode,
+                   "lm_comm": type(info.lm_comm).__name__}, fh)
+    D.barrier()
+    D.shutdown()
+
+
+def _run_probe(world, fault=""):
+    import json
+
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "p")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_probe, args=(r, world, port, out, fault)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        return [json.load(open(out + f".{r}.json")) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_transport_probe_runs_the_fused_lm_exchange(world):
+    """select_transport's LM probe runs the exchange the runs use (global Gram
+    subsample -> LmDesc.dp_fused, the gradient region and the output-Gram rows
+    summed inside k_lm_reduce) and checks it against the same fit over an
+    independent torch.distributed all-reduce."""
+    recs = _run_probe(world)
+    for r in recs:
+        lm = r["probe"]["lm"]
+        assert lm["fused"] is True and lm["clean"] is True, lm
+        assert lm["chosen"] == "xgmi" and r["lm_dp_mode"] == "xgmi", lm
+        assert lm["max_rel_dev_vs_allreduce"] <= lm["rtol"], lm
+        assert r["probe"]["packet"]["chosen"] == "xgmi"
+
+
+def test_transport_probe_catches_a_symmetric_wrong_sum():
+    """Fault injection into the fused path itself (LmDpDesc.fault: rank W-1's
+    contribution dropped on EVERY rank): the replicas still agree bit for bit,
+    so only the comparison with the independent all-reduce catches it - and
+    the LM exchange falls back (on a shared card: the process group)."""
+    recs = _run_probe(2, fault="lm_drop")
+    for r in recs:
+        lm = r["probe"]["lm"]
+        assert lm["fused"] is True and lm["fault_injected"] is True, lm
+        assert lm["bitwise_equal_weights"] is True, lm          # symmetric: the old probe passed it
+        assert lm["max_rel_dev_vs_allreduce"] > lm["rtol"], lm
+        assert r["lm_dp_mode"] == "rccl" and r["lm_comm"] == "TorchComm", r
+        assert r["probe"]["packet"]["chosen"] == "xgmi"
