@@ -79,6 +79,11 @@ PRESETS = {
                    lm_lam0_first=LAM0_FIRST, lm_starts=16, lm_explore_passes=20, lm_explore_log2=15,
                    lm_passes_first=25,
                    lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                   # round 6: inputs centred at the strike and scaled by the remaining-horizon
+                   # spread (feature_norm "horizon", floor 0.1 x the date spread), first-layer
+                   # breakpoints spread over [-1.5, 1.5] (init "spread"): seeds 1-16 P&L mean
+                   # 0.881 / worst 0.898 vs 0.891 / 0.901 (profiles/r6/norm/)
+                   feature_norm="horizon", feature_norm_floor=0.1, init="spread",
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
     # the round-4 default: one start, 33 warm-up passes on the 2^16-path prefix, 35 on every path
     "euro30_1s": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
@@ -106,6 +111,9 @@ PRESETS = {
                      # 1.0038 / 1.0052 x the minimum-variance hedge, against 11.18 ms and
                      # 1.0075 / 1.0042 / 1.0061 for one start: profiles/r5/seeds_presets.jsonl)
                      lm_lam0_first=LAM0_FIRST, lm_starts=16, lm_explore_passes=25, lm_explore_log2=15,
+                     # round 6: the price input on the remaining-horizon scale (seeds 1-8: 1.0045 x
+                     # the minimum-variance hedge, worst 1.0076; the variance input keeps the date scale)
+                     feature_norm="horizon", feature_norm_floor=0.1,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
                     batch_log2=18, lr=2e-2, lr_rest=4e-3, lr_decay=0.03,
@@ -115,6 +123,10 @@ PRESETS = {
                     # for 80 passes (3 seeds: last residual 0.069 / 0.071 / 0.075 against the
                     # BS floor 0.062, where 120 passes from one start left seed 2 at 0.150)
                     lm_starts=8, lm_explore_passes=40, lm_explore_log2=16,
+                    # round 6: horizon-scaled inputs (floor 0.1) + spread breakpoints: seeds 1-16
+                    # P&L 1.040 x the BS delta hedge, worst 1.107 x, last residual <= 0.076
+                    # (date scaling: 1.114 x, worst 1.232 x, residual 0.118; profiles/r6/norm/)
+                    feature_norm="horizon", feature_norm_floor=0.1, init="spread",
                     label="European call, 252-step GBM, 2M paths per GPU (16M at 8 GPUs)"),
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
@@ -123,6 +135,9 @@ PRESETS = {
                     # first date: 40 passes on the 2^16-path prefix, then 40 on every path
                     # (2 seeds: 333 vs 340 ms, P&L 0.359 vs 0.374 mean; profiles/r4/presets_explore_one.jsonl)
                     lm_explore_one=1, lm_explore_passes=40, lm_explore_log2=16,
+                    # (round 6: neither spread breakpoints - 16 seeds 1.165 x Levy, worst 1.358 x,
+                    # vs 1.141 / 1.321 x - nor horizon-scaled inputs - 1.21-1.28 x on seeds 1-8 -
+                    # help the basket: profiles/r6/norm/)
                     label="Basket-of-5 European call, 252 steps, 8M paths per GPU (64M at 8 GPUs)"),
     "euro30_mfma": dict(model="gbm_log", dates=30, substeps=1, paths_log2=20, epochs_first=512, epochs_rest=12,
                         batch_log2=18, lr=5e-3, lr_rest=1e-3, lr_decay=0.1, hidden=32,
@@ -152,8 +167,10 @@ def parse(argv=None):
     ap.add_argument("--mfma-precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--variant", type=int, default=-1, help="narrow lag-kernel variant (-1: engine default)")
     ap.add_argument("--max-wgs", type=int, default=0, help="workgroups per training step (0: engine default)")
-    ap.add_argument("--feature-norm", default=None, choices=["none", "global", "date"],
+    ap.add_argument("--feature-norm", default=None, choices=["none", "global", "date", "horizon"],
                     help="input standardisation fused into the kernels (default: preset)")
+    ap.add_argument("--feature-norm-floor", type=float, default=None,
+                    help="horizon standardisation: scale >= this x the date spread (default: preset)")
     ap.add_argument("--optimizer", default=None, choices=["adam", "lm"],
                     help="MSE fits: Keras-Adam minibatches or full-batch Levenberg-Marquardt (default: preset)")
     ap.add_argument("--lm-passes-first", type=int, default=None)
@@ -200,6 +217,8 @@ def parse(argv=None):
         a.hidden = pre.get("hidden", 8)
     if a.feature_norm is None:
         a.feature_norm = pre.get("feature_norm", "date")
+    if a.feature_norm_floor is None:
+        a.feature_norm_floor = pre.get("feature_norm_floor", 0.0)
     if a.optimizer is None:
         a.optimizer = pre.get("optimizer", "adam")
     if a.init is None:
@@ -226,6 +245,7 @@ def build_run(a, world: int):
                         lr=a.lr, lr_rest=a.lr_rest, lr_decay=a.lr_decay, lr_schedule_first=False, early_stopping=False, q99=False, shuffle=True,
                         chunk_log2=6, seed=a.seed, hidden=a.hidden, mfma_precision=a.mfma_precision,
                         variant=a.variant, max_wgs=a.max_wgs, feature_norm=a.feature_norm,
+                        feature_norm_floor=a.feature_norm_floor,
                         optimizer=a.optimizer, lm_passes_first=a.lm_passes_first, lm_passes_rest=a.lm_passes_rest,
                         lm_gram_paths=a.lm_gram_paths, lm_damping=a.lm_damping, lm_lam0=a.lm_lam0,
                         lm_lam_up=a.lm_lam_up, lm_lam_down=a.lm_lam_down, lm_stop_tol=a.lm_stop_tol,
@@ -491,7 +511,8 @@ def main(argv=None):
                             + PRESETS[a.preset]["label"],
                    "preset": a.preset,
                    "global_batch": cfg.train.batch_size, "seq_len": n_dates,
-                   "substeps": a.substeps, "feature_norm": a.feature_norm, "option": {k: getattr(cfg, k) for k in
+                   "substeps": a.substeps, "feature_norm": a.feature_norm,
+                   "feature_norm_floor": a.feature_norm_floor if a.feature_norm == "horizon" else None, "option": {k: getattr(cfg, k) for k in
                                                       ("Y", "K", "T", "r", "sigma", "kappa", "theta", "xi",
                                                        "rho", "v0", "n_assets", "basket_corr")
                                                       if cfg.model in ("heston", "basket") or

@@ -141,8 +141,9 @@ class TrainingParams:
     lm_diag_floor: float = 0.0       # LM damping diagonal floor, relative to mean diag 2G (0: Marquardt scaling)
     mean_refit: bool = True          # after each Adam MSE fit: exact refit of the bond holding's bias (the
                                      # residual mean over all paths -> 0; no mean error drifts into V0)
-    feature_norm: str = "date"       # input standardisation: none | global | date (driver.feature_norms);
+    feature_norm: str = "date"       # input standardisation: none | global | date | horizon (driver.feature_norms);
                                      # ParityFlags.raw_features forces none (reference)
+    feature_norm_floor: float = 0.0  # horizon mode: the remaining-horizon scale >= this x the date spread
 
 
 @dataclass

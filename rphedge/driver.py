@@ -56,6 +56,8 @@ class InductionConfig:
     # "none" = raw features (reference), "global" = one mean/std per feature
     # pooled over all fitted dates, "date" = per-date mean/std
     feature_norm: str = "none"
+    feature_centers: tuple | None = None  # horizon mode: the payoff kink per price feature (None: date mean)
+    feature_norm_floor: float = 0.0      # horizon mode: scale >= this x the date spread
     optimizer: str = "adam"              # MSE fits: adam | lm (engine.FitConfig.optimizer)
     q99_optimizer: str = "adam"          # pinball fits (two networks): adam | lm (IRLS Gauss-Newton LM)
     lm_q_passes_first: int = 40
@@ -204,7 +206,8 @@ class BackwardInduction:
                 if icfg.lr_decay != 1.0 else None
         self.lr_rest = geometric_lr_schedule(icfg.lr_rest or icfg.lr, icfg.epochs_rest, icfg.lr_decay) \
             if (icfg.lr_rest > 0 or icfg.lr_decay != 1.0) else None
-        self.norms = feature_norms(paths, icfg.feature_norm, world)
+        self.norms = feature_norms(paths, icfg.feature_norm, world, centers=icfg.feature_centers,
+                                   floor=icfg.feature_norm_floor)
         # pinball LM fits: the IRLS floor in target units (one sync at build time)
         self.q_lm = icfg.q99 and not icfg.shared_q99_model and str(icfg.q99_optimizer).lower() == "lm"
         self.q_delta = 0.0
@@ -270,9 +273,14 @@ class BackwardInduction:
     def explore_data(self, t: int) -> DateData | None:
         """The multi-start exploration's data at date t: the global path prefix
         simulated on this rank (FitConfig.lm_explore_data), or None when the
-        shard prefix is the global one (one rank)."""
+        shard prefix is the global one (one rank).  Only for the FIRST fitted
+        date (t = n_coarse - 2): the prefix carries the terminal payoff as its
+        target, which is V_{t+1} only there."""
         if self.explore_paths is None:
             return None
+        if t != self.paths.n_coarse - 2:
+            raise ValueError(f"explore_data(t={t}): the exploration prefix holds the terminal payoff, the target of "
+                             f"the first fitted date t = {self.paths.n_coarse - 2} only")
         xp, xv = self.explore_paths
         mu, isd = self.norms[t] if self.norms else ((), ())
         return DateData(feats=xp.features(t), prices_next=xp.prices(t + 1), bond_next=float(xp.bond[t + 1]),
@@ -377,16 +385,33 @@ class BackwardInduction:
         return res
 
 
-def feature_norms(paths: Paths, mode: str, world: int = 1) -> list:
+def price_features(paths: Paths) -> list:
+    """Indices of the features that are traded-asset prices (their hedge ratio
+    has a payoff kink): every feature of a GBM / basket run, feature 0 of an
+    SV / Heston / pension run (its other features are variance / survivors)."""
+    nin = len(paths.features(0))
+    return list(range(nin)) if paths.kind not in ("pension", "heston", "sv") else [0]
+
+
+def feature_norms(paths: Paths, mode: str, world: int = 1, centers=None, floor: float = 0.0) -> list:
     """Per-date ``(fmu, fisd)`` tuples for :class:`DateData` (empty list = raw
     inputs).  Moments are pooled over ranks (one host sync at build time);
     a feature with (near-)zero spread at a date (e.g. S_0 on every path) keeps
-    unit scale so it maps to the constant 0."""
+    unit scale so it maps to the constant 0.
+
+    ``mode="horizon"``: the price features are centred at the payoff kink
+    (``centers[i]``; None: the date mean) and scaled by the REMAINING-horizon
+    spread m_t * sd(log S_T - log S_t) (m_t the date mean; for GBM F_t sigma
+    sqrt(T - t)), the width of the hedge ratio's transition at date t - so the
+    kink the net draws has unit width at every date instead of narrowing like
+    sqrt((T - t) / t) under the date spread (``date``: sigma sqrt(t)).  The
+    scale is floored at ``floor`` x the date spread.  Other features keep the
+    date standardisation."""
     mode = (mode or "none").lower()
     if mode == "none":
         return []
-    if mode not in ("global", "date"):
-        raise ValueError(f"feature_norm must be none | global | date, got {mode!r}")
+    if mode not in ("global", "date", "horizon"):
+        raise ValueError(f"feature_norm must be none | global | date | horizon, got {mode!r}")
     nd = paths.n_coarse - 1
     nin = len(paths.features(0))
     # per (date, feature): fp64-accumulated full sums of x and x*x (fast full
@@ -416,8 +441,48 @@ def feature_norms(paths: Paths, mode: str, world: int = 1) -> list:
         sd = np.sqrt(var)
         ok = sd > 1e-6 * (np.abs(mu) + 1.0)
         isd = np.where(ok, 1.0 / np.where(ok, sd, 1.0), 1.0)
-        out.append((tuple(float(v) for v in mu), tuple(float(v) for v in isd)))
-    return out
+        out.append([mu, isd, sd])
+    if mode == "horizon":
+        _horizon_norms(paths, out, world, centers, floor)
+    return [(tuple(float(v) for v in mu), tuple(float(v) for v in isd)) for mu, isd, _ in out]
+
+
+def _horizon_norms(paths: Paths, out: list, world: int, centers, floor: float):
+    """feature_norms(mode="horizon") for the price features, in place: per
+    (date, price feature) fp64 sums of r = log S_T - log S_t and r^2 over the
+    paths (pooled over ranks), one date at a time (no [dates x paths]
+    temporary: basket5 holds 2^23 paths x 253 dates x 5 assets)."""
+    nd = paths.n_coarse - 1
+    pf = price_features(paths)
+    nin = len(paths.features(0))
+    last = paths.features(nd)
+    lT = [torch.log(last[i].double()) for i in pf]
+    s = []
+    for t in range(nd):
+        ft = paths.features(t)
+        for k, i in enumerate(pf):
+            r = lT[k] - torch.log(ft[i].double())
+            s.append(r.sum())
+            s.append((r * r).sum())
+    mom = torch.stack(s).view(nd, len(pf), 2)
+    if world > 1:
+        from .parallel import dist as D
+
+        D.all_reduce_(mom)
+    m = mom.cpu().numpy()
+    cnt = float(paths.features(0)[0].numel()) * world
+    for t in range(nd):
+        mu, isd, sd = out[t]
+        mu, isd = np.array(mu, dtype=np.float64), np.array(isd, dtype=np.float64)
+        for k, i in enumerate(pf):
+            rm = m[t, k, 0] / cnt
+            rsd = math.sqrt(max(m[t, k, 1] / cnt - rm * rm, 0.0))
+            scale = max(abs(mu[i]) * rsd, float(floor) * float(sd[i]))
+            if scale > 1e-12 * (abs(mu[i]) + 1.0):
+                c = centers[i] if (centers is not None and i < len(centers) and centers[i] is not None) else mu[i]
+                mu[i], isd[i] = float(c), 1.0 / scale
+        out[t] = [mu, isd, sd]
+    assert len(out) == nd and all(len(o[0]) == nin for o in out)
 
 
 def expected_value_trajectory(result: InductionResult, e_payoff: float, mu: float, r: float, dt: float) -> np.ndarray:

@@ -42,9 +42,9 @@ def mts_lm_parameters(**over) -> dict:
     one MI355X vs 10-23 s with Keras-Adam, with V0 / phi0 / psi0 inside the
     Adam seed band and a lower pinball loss on every date (BENCHMARKS.md round 5,
     profiles/r5/pension_lm_vs_adam.jsonl)."""
-    p = mts_parameters(optimizer="lm", q99_optimizer="lm", lm_starts=16, lm_explore_passes=40, lm_explore_log2=15,
-                       lm_passes_first=60, lm_passes_rest=3, lm_lam_carry=3.0, lm_out_fix=True,
-                       lm_q_passes_first=200, lm_q_passes_rest=20, lm_q_start="warm")
+    from .api import LM_PROFILE
+
+    p = mts_parameters(**LM_PROFILE)
     p.update(over)
     return p
 

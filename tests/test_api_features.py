@@ -31,6 +31,29 @@ def test_replicating_portfolio_returns_two_floats():
     assert 4e5 < phi + psi < 1.6e6
 
 
+def test_public_entry_points_default_optimizer_per_mode():
+    """Replicating_Portfolio(_SV) defaults (api.default_params): corrected mode
+    on a GPU fits both networks with Levenberg-Marquardt (LM_PROFILE);
+    parity=True keeps the reference's Keras-Adam (RP:149-175); the CPU torch
+    oracle keeps Adam; a caller's own optimizer always wins."""
+    from rphedge.api import LM_PROFILE, default_params
+    from rphedge.config import parse_params
+    from rphedge.experiments import mts_parameters, sv_parameters
+
+    for sv, base in ((False, mts_parameters()), (True, sv_parameters())):
+        tr = parse_params(default_params(base, gpu=True), sv=sv).train
+        assert (tr.optimizer, tr.q99_optimizer) == ("lm", "lm")
+        assert tr.lm_starts == LM_PROFILE["lm_starts"] and tr.lm_out_fix
+        tr = parse_params(default_params(dict(base, parity=True), gpu=True), sv=sv).train
+        assert (tr.optimizer, tr.q99_optimizer) == ("adam", "adam")
+        tr = parse_params(default_params(base, gpu=False), sv=sv).train
+        assert (tr.optimizer, tr.q99_optimizer) == ("adam", "adam")
+        tr = parse_params(default_params(dict(base, optimizer="adam"), gpu=True), sv=sv).train
+        assert tr.optimizer == "adam"
+    # explicit device="cpu" on a GPU machine: the CPU oracle, Adam
+    assert "optimizer" not in default_params(dict(mts_parameters(), device="cpu"))
+
+
 def test_replicating_portfolio_sv_parity():
     from rphedge import Replicating_Portfolio_SV
     from rphedge.experiments import sv_parameters

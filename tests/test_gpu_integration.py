@@ -48,6 +48,33 @@ def test_sv_reference_config():
     assert 8.0e5 < phi + psi < 1.2e6
 
 
+@pytest.mark.parametrize("sv", [False, True])
+def test_public_entry_points_run_lm_by_default(sv, monkeypatch):
+    """Corrected mode: Replicating_Portfolio(_SV)(notebook dict) on the GPU fits
+    BOTH networks with Levenberg-Marquardt (api.LM_PROFILE) - the run's
+    config says so - and lands in the same holdings band as the Keras-Adam
+    reference config (test_pension_reference_config; RP:29-235, :237-459)."""
+    from rphedge import api
+    from rphedge.experiments import mts_parameters, sv_parameters
+
+    seen = {}
+    orig = api.HedgeRun.build
+
+    def spy(self, *a, **kw):
+        seen["opt"] = (self.cfg.train.optimizer, self.cfg.train.q99_optimizer, self.backend_kind)
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(api.HedgeRun, "build", spy)
+    fn = api.Replicating_Portfolio_SV if sv else api.Replicating_Portfolio
+    phi, psi = fn((sv_parameters if sv else mts_parameters)(verbose=False))
+    _record(f"default_lm_sv={sv}", {"phi0": phi, "psi0": psi})
+    assert seen["opt"] == ("lm", "lm", "hip")
+    assert math.isfinite(phi) and math.isfinite(psi)
+    assert 8.0e5 < phi + psi < 1.2e6
+    if not sv:
+        assert 4.5e5 < phi < 8.5e5 and 1.5e5 < psi < 5.5e5
+
+
 def test_european_eo_parity_head():
     """EO notebook config with the psi = 1 - phi head (Q13): reference V0 = 11.352."""
     import rphedge

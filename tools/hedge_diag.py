@@ -6,7 +6,7 @@ reported as E[(e_t dS_t)^2] per date (the terms are uncorrelated across dates
 under the martingale measure up to the drift) and the RMS of e_t, grouped into
 date bands, plus the totals.  Needs the per-date holdings (keep_paths).
 
-usage: python tools/r5/hedge_diag.py OUT.json <bench args...>"""
+usage: python tools/hedge_diag.py OUT.json <bench args...>"""
 import json
 import math
 import os
@@ -15,7 +15,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..")))
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
 import bench  # noqa: E402
 from rphedge.api import HedgeRun  # noqa: E402
 
