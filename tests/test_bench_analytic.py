@@ -102,8 +102,12 @@ def test_bench_bare_two_ranks_one_gpu_lm():
                nproc=2, bare=True)
     c = r["config"]
     assert r["n_gpus"] == 2 and c["dist_world"] == 2 and c["optimizer"] == "lm" and c["backend"] == "hip"
-    clean = {"local_ok": True, "all_ok": True, "bitwise_equal_weights": True, "chosen": "xgmi"}
-    assert c["dp_probe"] == {"packet": clean, "lm": clean}
+    clean = {"local_ok": True, "all_ok": True, "bitwise_equal_weights": True, "chosen": "xgmi", "clean": True}
+    pk, lm = c["dp_probe"]["packet"], c["dp_probe"]["lm"]
+    assert {k: pk.get(k) for k in clean} == clean and {k: lm.get(k) for k in clean} == clean, c["dp_probe"]
+    # the LM probe ran the production exchange (summed inside k_lm_reduce) and
+    # matched the same fit over an independent all-reduce
+    assert lm["fused"] is True and lm["max_rel_dev_vs_allreduce"] <= lm["rtol"], lm
     assert c["dp_transport"] == "xgmi" and c["lm_dp_transport"] == "xgmi" and c["paths_global"] == 2 << 16
     assert abs(r["quality"]["V0"] - 10.3896) < 0.1, r["quality"]
     assert math.isfinite(r["quality"]["terminal_pnl_std"]) and r["quality"]["terminal_pnl_std"] < 3.5  # 2^17 paths, 30 passes: 2.57 measured

@@ -36,7 +36,7 @@ def main():
             ha = q.get("hedge_anchor") or {}
             rec = {"seed": s, "args": " ".join(rest), "ms": r["ms_per_step"], "pnl": q["terminal_pnl_std"],
                    "resid": q["terminal_residual_std"], "V0": q["V0"], "anchor_pnl": ha.get("pnl_std"),
-                   "anchor_price": (q.get("anchor") or {}).get("price"),
+                   "anchor_price": (q.get("anchor") or {}).get("price"), "hedge_price": ha.get("price"),
                    "first_best": ((r.get("lm") or {}).get("first_date") or {}).get("best_loss"),
                    "ms_pick": ((r.get("lm") or {}).get("multistart") or {}).get("pick"),
                    "wall_s": time.perf_counter() - t0}
