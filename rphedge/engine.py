@@ -140,7 +140,7 @@ class TrainConfig:
     eps: float = 1e-7              # Keras epsilon
     max_wgs: int = 0               # workgroups per training step; 0 = auto: 256 (one per CU), 512 for
                                    # the 1-input 32-unit bf16 net (2 resident waves/SIMD:
-                                   # the MFMA tile chain is latency-bound, profiles/sweep_r1n_wide_wgs.jsonl)
+                                   # the MFMA tile chain is latency-bound, profiles/r1/sweep_r1n_wide_wgs.jsonl)
     paths_per_thread: int = 1      # target work per thread per step
     deterministic: bool = False    # fixed-order slab reduction instead of float atomics
     split_update: bool = False     # force the standalone update kernel (the world_size>1 path)
@@ -506,12 +506,12 @@ class HipBackend:
         # VGPRs + the rest from LDS, 2 waves/SIMD at 512 WGs (1-2 input nets:
         # 9.83 -> 9.64 / 10.05 -> 9.69 us per 2^18 step; the 3-input net is
         # slower that way), 4 = all weights from LDS (256-wide packets),
-        # 0 = all weights hoisted (profiles/stamp_r1u_hybrid.jsonl)
+        # 0 = all weights hoisted (profiles/r1/stamp_r1u_hybrid.jsonl)
         # 512 workgroups only on one rank (with the in-kernel xGMI exchange every
         # workgroup polls the mailbox, so data-parallel runs keep 256) and only
         # where the hybrid body fits 2 waves/SIMD (<= 3 inputs, 128-wide packet);
         # the 256-wide-packet nets (basket 5-8-6) run it at 1 wave/SIMD, still
-        # faster than all-LDS weights (16.6 -> 14.8 us, profiles/stamp_r1v_masks.jsonl)
+        # faster than all-LDS weights (16.6 -> 14.8 us, profiles/r1/stamp_r1v_masks.jsonl)
         hyb512 = spec.hidden == 8 and spec.nin <= 3 and self.R <= 128 and world == 1
         auto_v = 5 if (hyb512 or (spec.hidden == 8 and self.R > 128)) else 0
         self.variant = int(tcfg.variant) if int(tcfg.variant) >= 0 else auto_v
@@ -520,7 +520,7 @@ class HipBackend:
         if mw <= 0:
             # 512 workgroups = 2 per CU only where two fit (the 1-input bf16
             # net); the wider-input nets run 1 per CU, so a 512 grid starts in
-            # two waves (+15 us start spread, profiles/stamp_r1s_wide_wgs.jsonl)
+            # two waves (+15 us start spread, profiles/r1/stamp_r1s_wide_wgs.jsonl)
             mw = 512 if (spec.hidden == 32 and not tcfg.mfma_fp32 and spec.nin == 1) else 256
             if (self.variant == 5 and hyb512 and tcfg.step_mode in ("auto", "lag") and not tcfg.deterministic
                     and not tcfg.split_update):
@@ -1049,7 +1049,7 @@ class HipBackend:
             return "lag"
         # small grids (the reference's batch 512 = 2 workgroups): the persistent
         # kernel's in-kernel barrier is cheaper than a kernel boundary below ~96
-        # workgroups (profiles/crossover_r1g.jsonl) and one launch per fit
+        # workgroups (profiles/r1/crossover_r1g.jsonl) and one launch per fit
         # removes the per-step host launch from eager runs
         if (t.step_mode == "auto" and atomic and self.world == 1 and not poll_every
                 and self.spec.hidden == 8 and self.num_wgs <= PERSISTENT_MAX_WGS):

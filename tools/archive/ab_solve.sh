@@ -9,7 +9,7 @@ T="python -u -m pytest --timeout 120 --timeout-method thread -p no:cacheprovider
 timeout -k 10 600 $T tests/test_gpu_lm_solve.py ${EXTRA_TESTS} -v > gpurun_out/solve_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; [ $rc -gt 1 ] && exit $rc
 if [ -n "$STAMPS" ]; then
-  timeout -k 10 200 python -u tools/solve_stamps.py > gpurun_out/solve_stamps.jsonl 2> gpurun_out/solve_stamps.err
+  timeout -k 10 200 python -u tools/archive/solve_stamps.py > gpurun_out/solve_stamps.jsonl 2> gpurun_out/solve_stamps.err
   echo "stamps rc=$?"
 fi
 if [ -n "$AB_LIB" ]; then

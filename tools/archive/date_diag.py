@@ -1,7 +1,7 @@
 """Diagnostic: per-date fit record of one bench configuration (eager run):
 best loss, passes, accepted trials, one-step residual std and the fitted
 holdings' means, to find the date that breaks a self-financing P&L.
-usage: python tools/date_diag.py <bench args...>"""
+usage: python tools/archive/date_diag.py <bench args...>"""
 import json
 import sys
 

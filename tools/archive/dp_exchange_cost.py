@@ -5,7 +5,7 @@ co-resident), and the per-step time is compared with one process.  This
 isolates the protocol (push, sentinel wait, tagged reads, fixed-order sum);
 xGMI link latency comes on top on a real multi-GPU node.
 
-usage: python tools/dp_exchange_cost.py [W] [batch_log2_per_rank]"""
+usage: python tools/archive/dp_exchange_cost.py [W] [batch_log2_per_rank]"""
 import json
 import os
 import socket

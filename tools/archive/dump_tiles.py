@@ -1,6 +1,6 @@
 """Diagnostic: factor one LM system with the RPH_DUMP_T library and compare
 the tile store (L of the augmented matrix, tile by tile) with numpy's
-Cholesky factor.  usage: RPH_NATIVE_LIB=... python tools/dump_tiles.py [P_index]"""
+Cholesky factor.  usage: RPH_NATIVE_LIB=... python tools/archive/dump_tiles.py [P_index]"""
 import json
 import sys
 

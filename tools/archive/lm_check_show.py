@@ -1,4 +1,4 @@
-"""Summarise tools/lm_check.sh outputs (host side)."""
+"""Summarise tools/archive/lm_check.sh outputs (host side)."""
 import csv
 import json
 import re

@@ -1,7 +1,7 @@
 """CPU laboratory: multi-start first-date LM fits and damping carried across
 dates (float64 torch oracle, bench.py --cpu).
 
-  python tools/lm_ms_lab.py --seeds 1,2,3 --variants base,ms4,ms4+carry3
+  python tools/archive/lm_ms_lab.py --seeds 1,2,3 --variants base,ms4,ms4+carry3
 
 Variant flags ('+'-joined):
   msK        first date: K starts (init seeds seed, seed+1, ...) explored for

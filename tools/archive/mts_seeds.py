@@ -2,7 +2,7 @@
 GPU: V0 / phi0 / psi0 / VaR for several training seeds (Keras-Adam, the
 reference's optimiser) and for the full-batch LM fit, one JSON line each.
 
-usage: python tools/mts_seeds.py [n_seeds] [log2 paths ...] > out.jsonl
+usage: python tools/archive/mts_seeds.py [n_seeds] [log2 paths ...] > out.jsonl
 """
 import json
 import sys

@@ -5,7 +5,7 @@ bands: LeakyReLU slope 0.2 (Keras 3) instead of 0.3 (Keras 2),
 Keras-3 EarlyStopping restore at the end of every fit, and the Adam state
 reset per date instead of carried (Q18).  One JSON line per (variant, seed).
 
-usage: python tools/mts_variants.py [--backend torch] [--seeds 4] [variants...] > out.jsonl
+usage: python tools/archive/mts_variants.py [--backend torch] [--seeds 4] [variants...] > out.jsonl
 """
 import argparse
 import json

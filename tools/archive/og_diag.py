@@ -2,7 +2,7 @@
 k_lm_reduce): one output-Gram pass at several path counts, the packed Gram
 matrix and the gradient against fp64 torch on the same data.
 
-    python tools/og_diag.py [log2 ...]
+    python tools/archive/og_diag.py [log2 ...]
 """
 import os
 import sys

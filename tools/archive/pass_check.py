@@ -1,6 +1,6 @@
 """Diagnostic: one LM pass (pass 0) on n paths vs fp64 torch: relative error
 of the gradient, the loss sum and the path count of the reduced block.
-usage: python tools/pass_check.py [n_log2]"""
+usage: python tools/archive/pass_check.py [n_log2]"""
 import json
 import sys
 

@@ -4,7 +4,7 @@ the closed-form anchor of SURVEY §6.1: N·P·max(1, Y_T) under Q with
 independent mortality ≈ 917,112 EUR (Δ-hedge ≈ 696,036 fund + 221,076 bond).
 One JSON line per (optimizer, capital-charge blend, paths, seed): V0, phi0, psi0, VaR, P&L.
 
-usage: python tools/pension_corrected.py [n_seeds] [log2 paths ...]
+usage: python tools/archive/pension_corrected.py [n_seeds] [log2 paths ...]
 """
 import json
 import sys

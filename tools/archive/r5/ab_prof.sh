@@ -2,8 +2,8 @@
 # Same-box A/B of native-library builds: the in-tree library ("default") and
 # rphedge/_lib/ab/librphedge_<name>.so for every name given.  Per build: the
 # euro30 bench (20 timed steps) and a rocprofv3 kernel-stats run (its own
-# process; kernel means from tools/r5/kstats.py).  Output under gpurun_out/ab/.
-# usage: bash tools/r5/ab_prof.sh NAME [NAME ...] [-- extra bench args]
+# process; kernel means from tools/kstats.py).  Output under gpurun_out/ab/.
+# usage: bash tools/archive/r5/ab_prof.sh NAME [NAME ...] [-- extra bench args]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 names=(default)
 extra=()
@@ -29,5 +29,5 @@ b = json.loads([l for l in open(f"{out}/bench_{lib}.log") if l.startswith("{")][
 print(lib, "ms", round(b["ms_per_step"], 3), "pnl", repr(b["quality"]["terminal_pnl_std"]), "V0", b["quality"]["V0"])
 PY
   db=$(find $OUT/prof_$lib -name "*results.db" | head -1)
-  [ -n "$db" ] && python3 tools/r5/kstats.py "$db" rph | head -6
+  [ -n "$db" ] && python3 tools/kstats.py "$db" rph | head -6
 done

@@ -5,7 +5,7 @@ sum_k phi_t,k (S_t+1,k - S_t,k B_t+1/B_t), the largest |holding| and the mean
 Reductions run on the device (the holdings of 2^23 paths x 252 dates do not
 leave the GPU).
 
-usage: python tools/r5/basket_diag.py OUT.jsonl <bench args...>"""
+usage: python tools/archive/r5/basket_diag.py OUT.jsonl <bench args...>"""
 import json
 import os
 import sys

@@ -13,6 +13,6 @@ tail -c 400 $OUT/bench.log
 rm -rf $OUT/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --steps 6 --warmup 1 > $OUT/prof.log 2>&1 || { echo prof failed; exit 1; }
 db=$(find $OUT/prof -name "*results.db" | head -1)
-python3 tools/r5/kstats.py "$db" > $OUT/kernel_stats.txt
-python3 tools/r5/phases.py "$db" > $OUT/phases.txt
+python3 tools/kstats.py "$db" > $OUT/kernel_stats.txt
+python3 tools/phases.py "$db" > $OUT/phases.txt
 head -8 $OUT/kernel_stats.txt

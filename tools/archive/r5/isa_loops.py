@@ -5,8 +5,8 @@ so hedge_lm.hip compiles in ~1 min instead of 5), finds every loop
 (back-edge) of the kernel whose mangled name contains KEY, and prints its
 instruction count by class and the most frequent opcodes.
 
-usage: python tools/r5/isa_loops.py FILE KEY [--shape 1,8,2,HEAD_FREE] [--keep DIR]
-  e.g. python tools/r5/isa_loops.py hedge_lm.hip 'k_lm_passINS_14NarrowPairBodyILi1ELi8ELi2ELi0ELb0E'"""
+usage: python tools/archive/r5/isa_loops.py FILE KEY [--shape 1,8,2,HEAD_FREE] [--keep DIR]
+  e.g. python tools/archive/r5/isa_loops.py hedge_lm.hip 'k_lm_passINS_14NarrowPairBodyILi1ELi8ELi2ELi0ELb0E'"""
 import argparse
 import collections
 import re

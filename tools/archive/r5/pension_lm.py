@@ -7,7 +7,7 @@ the end), V0 / phi0 / psi0, and the Q99 net's one-step residual quantiles per
 date (the sign condition of "Single Time Step.ipynb":656-662: the 99 % quantile
 of V_{t+1} - h_q(state_t) . prices_{t+1} should sit at ~0).
 
-usage: python tools/r5/pension_lm.py OUT.jsonl n_log2 seeds opt [opt ...]
+usage: python tools/archive/r5/pension_lm.py OUT.jsonl n_log2 seeds opt [opt ...]
   opt: lm | adam
 """
 import json

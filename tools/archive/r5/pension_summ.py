@@ -1,8 +1,8 @@
-"""Summarise tools/r5/pension_lm.py records: per run and per variant
+"""Summarise tools/archive/r5/pension_lm.py records: per run and per variant
 (mean +- sd over seeds of V0 / phi0 / psi0, last-date one-step residual std,
 self-financing P&L std, Q99 fraction above, median wall time).
 
-usage: python tools/r5/pension_summ.py FILE.jsonl [FILE ...]"""
+usage: python tools/archive/r5/pension_summ.py FILE.jsonl [FILE ...]"""
 import collections
 import json
 import sys

@@ -1,7 +1,7 @@
 """Seed sweep of a bench.py preset in ONE process (no per-seed torch import /
 library load): one JSON line per seed with the timing and quality fields.
 
-usage: python tools/r5/seeds.py OUT.jsonl SEEDS [bench.py args...]
+usage: python tools/archive/r5/seeds.py OUT.jsonl SEEDS [bench.py args...]
   SEEDS: comma list or a-b range, e.g. 1-8
 """
 import contextlib

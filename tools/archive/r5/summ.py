@@ -1,4 +1,4 @@
-"""Summarise seed-sweep JSONL files (tools/r5/seeds.py): per file mean / worst
+"""Summarise seed-sweep JSONL files (tools/archive/r5/seeds.py): per file mean / worst
 P&L std, residual, |V0 - analytic|, ms."""
 import json
 import sys

@@ -3,7 +3,7 @@ over training seeds, in parity mode (the reference's quirks: shared Q99 model,
 raw features, Keras schedule) and in the corrected default mode: one JSON line
 per (mode, seed) with the [sigma, Phi, Psi, sum] rows.
 
-usage: python tools/sigma_sweep_seeds.py [n_seeds] > out.jsonl
+usage: python tools/archive/sigma_sweep_seeds.py [n_seeds] > out.jsonl
 """
 import json
 import sys

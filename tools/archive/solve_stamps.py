@@ -3,7 +3,7 @@ from in-kernel s_memrealtime stamps (100 MHz ticks), per net shape, median
 over repeats.  Diagnostic build of nothing: the production kernel writes the
 stamps only when TrainDesc.stamps is set.
 
-usage: python tools/solve_stamps.py > out.jsonl
+usage: python tools/archive/solve_stamps.py > out.jsonl
 """
 import json
 import sys

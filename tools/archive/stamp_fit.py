@@ -2,7 +2,7 @@
 from in-kernel s_memrealtime stamps of the LAST step (100 MHz), plus the
 event-timed per-step cost of whole fits.  Diagnostic only.
 
-usage: python tools/stamp_fit.py '[{"batch_log2": 18}, {"batch_log2": 18, "hidden": 32}]'
+usage: python tools/archive/stamp_fit.py '[{"batch_log2": 18}, {"batch_log2": 18, "hidden": 32}]'
 """
 import json
 import sys

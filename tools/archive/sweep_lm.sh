@@ -1,6 +1,6 @@
 #!/bin/bash
 # LM pass-budget sweep of a preset (quality vs time), one JSON line per config.
-# usage: PRESET=euro30 CFGS="40 2;60 3" bash tools/sweep_lm.sh
+# usage: PRESET=euro30 CFGS="40 2;60 3" bash tools/archive/sweep_lm.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 IFS=';' read -ra LIST <<< "${CFGS:-30 2;40 2;50 2;50 3;60 2;60 3;80 3;80 2}"

@@ -1,6 +1,6 @@
 """Per-kernel statistics (calls, total / mean / min us, share) from a rocprofv3
 results database (rocpd sqlite, the default output format) or a
-kernel_stats.csv.  usage: python tools/r5/kstats.py FILE [name-filter]"""
+kernel_stats.csv.  usage: python tools/kstats.py FILE [name-filter]"""
 import collections
 import csv
 import sqlite3

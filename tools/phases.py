@@ -2,7 +2,7 @@
 results database: kernels of the first date's multi-start exploration (grid
 y > 1), the first date's polish, and the later dates, with totals / counts /
 means per kernel, and the idle time between kernels.
-usage: python tools/r5/phases.py RESULTS.db"""
+usage: python tools/phases.py RESULTS.db"""
 import collections
 import sqlite3
 import sys
