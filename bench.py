@@ -78,11 +78,14 @@ PRESETS = {
                    # at 7.49 ms for the round-4 single start (profiles/r5/seeds_*.jsonl)
                    lm_lam0_first=LAM0_FIRST, lm_starts=16, lm_explore_passes=20, lm_explore_log2=15,
                    lm_passes_first=25,
-                   lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                   lm_passes_rest=1, lm_lam_carry=3.0, lm_out_fix=1,
                    # round 6: inputs centred at the strike and scaled by the remaining-horizon
                    # spread (feature_norm "horizon", floor 0.1 x the date spread), first-layer
                    # breakpoints spread over [-1.5, 1.5] (init "spread"): seeds 1-16 P&L mean
-                   # 0.881 / worst 0.898 vs 0.891 / 0.901 (profiles/r6/norm/)
+                   # 0.881 / worst 0.898 vs 0.891 / 0.901 (profiles/r6/norm/).  On that scale the
+                   # previous date's net is nearly the next date's optimum, so ONE LM trial per
+                   # later date (+ the output-layer step) suffices: 0.882 / 0.901 at 5.71 vs
+                   # 7.03 ms (profiles/r6/rest1/; 0 trials: 0.920 / 1.083)
                    feature_norm="horizon", feature_norm_floor=0.1, init="spread",
                    label="European call, 30-step GBM, 1M Sobol paths per GPU"),
     # the round-4 default: one start, 33 warm-up passes on the 2^16-path prefix, 35 on every path
@@ -105,14 +108,15 @@ PRESETS = {
     "heston30": dict(model="heston", dates=30, substeps=10, paths_log2=20, epochs_first=1024, epochs_rest=16,
                      batch_log2=18, lr=5e-2, lr_rest=4e-3, lr_decay=0.1,
                      extra=dict(mu=0.05, r=0.05, kappa=2.0, theta=0.04, xi=0.5, rho=-0.7, v0=0.04, sigma=0.2),
-                     optimizer="lm", lm_passes_first=35, lm_passes_rest=2, lm_lam_carry=3.0, lm_out_fix=1,
+                     optimizer="lm", lm_passes_first=35, lm_passes_rest=1, lm_lam_carry=3.0, lm_out_fix=1,
                      # first date: 16 starts x 25 passes on the global 2^15-path prefix, the best
                      # polished for 35 passes on every path (3 seeds: 11.38 ms, P&L 1.0024 /
                      # 1.0038 / 1.0052 x the minimum-variance hedge, against 11.18 ms and
                      # 1.0075 / 1.0042 / 1.0061 for one start: profiles/r5/seeds_presets.jsonl)
                      lm_lam0_first=LAM0_FIRST, lm_starts=16, lm_explore_passes=25, lm_explore_log2=15,
-                     # round 6: the price input on the remaining-horizon scale (seeds 1-8: 1.0045 x
-                     # the minimum-variance hedge, worst 1.0076; the variance input keeps the date scale)
+                     # round 6: the price input on the remaining-horizon scale (the variance input keeps
+                     # the date scale) and one LM trial per later date: 16 seeds 1.0070 x the minimum-
+                     # variance hedge, worst 1.0108, 9.71 ms (2 trials: 1.0048 / 1.0098, 11.17 ms)
                      feature_norm="horizon", feature_norm_floor=0.1,
                      label="Heston stochastic-vol call, 30 dates x 10 substeps, 1M paths per GPU"),
     "euro252": dict(model="gbm_log", dates=252, substeps=1, paths_log2=21, epochs_first=256, epochs_rest=8,
