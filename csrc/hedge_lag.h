@@ -288,7 +288,7 @@ RPH_INLINE int lag_apply(LagState<P>& st, const float* red, const TrainDesc& d, 
 // summed packet of accumulator `buf` (NREP replicas) into LDS red[0..R)
 // PLAIN: cached loads of the previous launch's accumulator (see sum_replicas);
 // measured faster for the 128-float packets of the 8-unit nets, slower for the
-// 1280-float packets of the 32-unit nets (profiles/stamp_r1q_acc_loads.jsonl)
+// 1280-float packets of the 32-unit nets (profiles/r1/stamp_r1q_acc_loads.jsonl)
 template <int R, int NREP, bool PLAIN = false>
 RPH_INLINE void lag_sums(const float* buf, float* red) {
   for (int i = threadIdx.x; i < R; i += 256) red[i] = sum_replicas<NREP, !PLAIN>(buf, R, i);

@@ -237,15 +237,16 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
     // 1 / (2 sqrt(max(|r_p|, delta))); delta = max(q_delta, q_kappa x the mean
     // |r| of this 64-path tile) keeps the weights of the small residuals
     // bounded (a near-zero residual would otherwise dominate the step).  The
-    // shard-subsample Gram only (the host keeps pinball fits off the simulated
-    // subsample, which has no targets)
+    // targets: the shard's (shard subsample) or the simulated subsample's own
+    // (gram_side: LmDesc.gtarget, the same on every rank)
     float wq = 1.f;
-    if (d.loss == LOSS_PINBALL && !lm.gram_side) {
+    if (d.loss == LOSS_PINBALL) {
       const long long p = (slot / lm.gram_blk) * lm.gram_blk_stride + slot % lm.gram_blk;
       float V = 0.f;
 #pragma unroll
       for (int k = 0; k < NHOLD; ++k) V = fmaf(hold[k], pr[k], V);
-      const float ra = ok ? fabsf(V - d.target[ok ? p : 0]) : 0.f;
+      const float y = lm.gram_side ? lm.gtarget[slot] : d.target[ok ? p : 0];
+      const float ra = ok ? fabsf(V - y) : 0.f;
       float sa = ra, sc = ok ? 1.f : 0.f;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) {
@@ -1097,9 +1098,10 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (lm->red_wgs != nblk * 1024 / 64 + R / 4 + lm_og_wgs(nu)) return rph_report("rph_lm", "bad red_wgs");
   if (lm->out_gram && (!lm->slab_o || nu > LM_OG_MAX)) return rph_report("rph_lm", "output Gram needs slab_o (<= 64 output parameters)");
   if (d->loss != LOSS_MSE && d->loss != LOSS_PINBALL) return rph_report("rph_lm", "LM fits: MSE or pinball loss");
-  if (d->loss == LOSS_PINBALL && (lm->gram_side || lm->out_gram || lm->out_n > 0 || lm->bias_index >= 0 ||
-                                  !(lm->q_delta > 0.f)))
-    return rph_report("rph_lm", "pinball LM fits: shard Gram subsample, no output / bias step, q_delta > 0");
+  if (d->loss == LOSS_PINBALL && ((lm->gram_side && !lm->gtarget) || lm->out_gram || lm->out_n > 0 ||
+                                  lm->bias_index >= 0 || !(lm->q_delta > 0.f)))
+    return rph_report("rph_lm", "pinball LM fits: subsample targets with a simulated subsample, no output / "
+                                "bias step, q_delta > 0");
   if (R != 128 && R != 256) return rph_report("rph_lm", "packet width must be 128 or 256");
   if (lm->inst < 1 || lm->inst > LM_SEL_MAX) return rph_report("rph_lm", "bad instance count");
   if (lm->inst > 1 && !lm->explore) return rph_report("rph_lm", "several instances are exploration fits only");

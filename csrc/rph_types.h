@@ -344,6 +344,11 @@ struct LmDesc {
   // leaves), and with the reduce's contiguous-halves trees the summed
   // gradient is bitwise independent of the world size.  0: cyclic blocks
   int leaf_blocks;
+  // pinball fits on the simulated global subsample (gram_side): the targets
+  // of its paths ([gram_wgs x 64]: V_{t+1} evaluated on the subsample at the
+  // date boundary, driver.BackwardInduction), so the IRLS weights - and the
+  // Gram - are the same on every rank; nullptr for MSE fits (J needs no target)
+  const float* gtarget;
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)

@@ -88,6 +88,7 @@ class HedgeRun:
         self.spec = self._spec()
         self.paths = None
         self.gpaths = None  # LM Gram subsample paths (engine.gram_subsample), simulated on every rank
+        self.gv_terminal = None  # ... their terminal values (pinball LM fits: the subsample's targets)
         self.xpaths = None  # LM multi-start exploration: (global prefix paths, their terminal values)
         self.induction = None
         self.graph = None
@@ -139,6 +140,10 @@ class HedgeRun:
             if str(tr.optimizer).lower() == "lm":
                 ns, blk, stride = gram_subsample(self.n_total, tr.lm_gram_paths)
                 self.gpaths = self._simulate_paths(ns, 0, (blk, stride), self.gpaths if into is not None else None)
+                if self._q_lm():
+                    # pinball LM fits: the subsample's own terminal values (its
+                    # later targets come from the date-boundary evaluations)
+                    self.gv_terminal = self._payoff(self.gpaths, self.gv_terminal if into is not None else None)
                 if self.di.world > 1 and (int(tr.lm_starts) > 1 or bool(getattr(tr, "lm_explore_one", False))):
                     # the multi-start exploration's global path prefix (every
                     # rank explores the same starts on the same paths)
@@ -148,6 +153,11 @@ class HedgeRun:
                     self.xpaths = (xp, xv)
         self.paths, self.v_terminal = p, v_t
         return p, v_t
+
+    def _q_lm(self) -> bool:
+        """Both networks with the pinball fit on Levenberg-Marquardt."""
+        tr, pf = self.cfg.train, self.cfg.parity
+        return bool(tr.q99) and not pf.shared_q99_model and str(getattr(tr, "q99_optimizer", "adam")).lower() == "lm"
 
     def _payoff(self, p: P.Paths, out=None) -> torch.Tensor:
         """Terminal value V_T of paths ``p`` (K7; ``out``: into that buffer)."""
@@ -337,7 +347,8 @@ class HedgeRun:
                 backend_q = None
         self.induction = BackwardInduction(self.paths, self.v_terminal, self.spec, self.w0, self.backend, icfg,
                                            world=self.di.world, rank=self.di.rank, backend_q=backend_q,
-                                           gram_paths=self.gpaths, explore_paths=self.xpaths)
+                                           gram_paths=self.gpaths, explore_paths=self.xpaths,
+                                           gram_terminal=self.gv_terminal)
         return self
 
     # ------------------------------------------------------------------ run
@@ -347,6 +358,8 @@ class HedgeRun:
         if resimulate:
             self.simulate()  # same buffers are re-created; only used outside capture
         ind.values[-1].copy_(self.v_terminal)
+        if ind.gvalues is not None:
+            ind.gvalues[-1].copy_(ind.g_terminal)
         ind.w_mse.copy_(ind.w_init)
         ind.opt_mse.copy_(ind.opt_init)
         if ind.cfg.q99:

@@ -149,7 +149,7 @@ class BackwardInduction:
 
     def __init__(self, paths: Paths, v_terminal: torch.Tensor, spec: NetSpec, w0: np.ndarray, backend,
                  icfg: InductionConfig, world: int = 1, rank: int = 0, backend_q=None, gram_paths: Paths | None = None,
-                 explore_paths: tuple | None = None):
+                 explore_paths: tuple | None = None, gram_terminal: torch.Tensor | None = None):
         self.paths, self.spec, self.backend, self.cfg = paths, spec, backend, icfg
         # LM fits: the global Gram subsample simulated on this rank (engine.gram_subsample)
         self.gram_paths = gram_paths
@@ -208,6 +208,22 @@ class BackwardInduction:
             if (icfg.lr_rest > 0 or icfg.lr_decay != 1.0) else None
         self.norms = feature_norms(paths, icfg.feature_norm, world, centers=icfg.feature_centers,
                                    floor=icfg.feature_norm_floor)
+        # pinball LM fits on the global Gram subsample: its values V_t at every
+        # date (the two-network blend evaluated on the subsample paths at the
+        # date boundary, like values[t] on the shard), so the IRLS weights need
+        # no shard data - every rank builds the same pinball Gram and the fit
+        # takes the fused exchange (world-invariant, no per-pass exchange launch)
+        self.gvalues = None
+        q_lm_side = (icfg.q99 and not icfg.shared_q99_model and str(icfg.q99_optimizer).lower() == "lm"
+                     and gram_paths is not None and gram_terminal is not None)
+        if q_lm_side:
+            ns = gram_terminal.numel()
+            self.gvalues = torch.empty(nc, ns, dtype=torch.float32, device=dev)
+            self.gvalues[nc - 1].copy_(gram_terminal)
+            self.g_terminal = gram_terminal
+            self.ggbuf = torch.empty(ns, dtype=torch.float32, device=dev)
+            # (per-workgroup statistics of the subsample evaluations: not reported)
+            self.gstats = [backend.new_stats(), backend.new_stats()]
         # pinball LM fits: the IRLS floor in target units (one sync at build time)
         self.q_lm = icfg.q99 and not icfg.shared_q99_model and str(icfg.q99_optimizer).lower() == "lm"
         self.q_delta = 0.0
@@ -293,7 +309,16 @@ class BackwardInduction:
         return DateData(feats=p.features(t), prices_next=p.prices(t + 1), bond_next=float(p.bond[t + 1]),
                         target=self.values[t + 1], prices_now=p.prices(t), bond_now=float(p.bond[t]),
                         fmu=mu, fisd=isd, gram_feats=gp.features(t) if gp is not None else None,
-                        gram_prices_next=gp.prices(t + 1) if gp is not None else None)
+                        gram_prices_next=gp.prices(t + 1) if gp is not None else None,
+                        gram_target=self.gvalues[t + 1] if self.gvalues is not None else None)
+
+    def gram_date_data(self, t: int) -> DateData:
+        """The Gram subsample as a date's eval input (its V_t for the pinball fits)."""
+        gp = self.gram_paths
+        mu, isd = self.norms[t] if self.norms else ((), ())
+        return DateData(feats=gp.features(t), prices_next=gp.prices(t + 1), bond_next=float(gp.bond[t + 1]),
+                        target=self.gvalues[t + 1], prices_now=gp.prices(t), bond_now=float(gp.bond[t]),
+                        fmu=mu, fisd=isd)
 
     def enqueue(self, start: int | None = None):
         """Enqueue dates ``start, start-1, ..., 0`` (default: all, from n-2).
@@ -351,6 +376,14 @@ class BackwardInduction:
                 be.eval(self.w_mse, data, s_q, wts_b=self.w_q, g_base=self.gbuf, blend_c=c.cost_of_capital,
                         hold_c=self.hold_c, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out,
                         snap_a=self.snap[t, 0], snap_b=self.snap[t, 1])
+                if self.gvalues is not None and t > 0:
+                    # the same blend on the Gram subsample: V_t there, the next
+                    # date's pinball-fit targets
+                    gd = self.gram_date_data(t)
+                    ns = self.ggbuf.numel()
+                    be.eval(self.w_mse, gd, self.gstats[0], v_out=self.ggbuf, n_local=ns)
+                    be.eval(self.w_mse, gd, self.gstats[1], wts_b=self.w_q, g_base=self.ggbuf,
+                            blend_c=c.cost_of_capital, hold_c=self.hold_c, v_out=self.gvalues[t], n_local=ns)
             else:
                 be.eval(self.w_mse, data, s_q, v_out=self.values[t], hold_out=hold_out, resid_out=resid_out,
                         snap_a=self.snap[t, 0])
@@ -449,27 +482,30 @@ def feature_norms(paths: Paths, mode: str, world: int = 1, centers=None, floor: 
 
 def _horizon_norms(paths: Paths, out: list, world: int, centers, floor: float):
     """feature_norms(mode="horizon") for the price features, in place: per
-    (date, price feature) fp64 sums of r = log S_T - log S_t and r^2 over the
+    (date, price feature) sums of r = log S_T - log S_t and r^2 over the
     paths (pooled over ranks), one date at a time (no [dates x paths]
-    temporary: basket5 holds 2^23 paths x 253 dates x 5 assets)."""
+    temporary: basket5 holds 2^23 paths x 253 dates x 5 assets).  The sums are
+    int64 fixed point (2^-32 units): exact, so the scales - and a data-parallel
+    fit - do not depend on the summation order or the world size."""
     nd = paths.n_coarse - 1
     pf = price_features(paths)
     nin = len(paths.features(0))
     last = paths.features(nd)
     lT = [torch.log(last[i].double()) for i in pf]
     s = []
+    q = float(2 ** 32)
     for t in range(nd):
         ft = paths.features(t)
         for k, i in enumerate(pf):
             r = lT[k] - torch.log(ft[i].double())
-            s.append(r.sum())
-            s.append((r * r).sum())
+            s.append(torch.round(r * q).to(torch.int64).sum())
+            s.append(torch.round(r * r * q).to(torch.int64).sum())
     mom = torch.stack(s).view(nd, len(pf), 2)
     if world > 1:
         from .parallel import dist as D
 
         D.all_reduce_(mom)
-    m = mom.cpu().numpy()
+    m = mom.cpu().numpy().astype(np.float64) / q
     cnt = float(paths.features(0)[0].numel()) * world
     for t in range(nd):
         mu, isd, sd = out[t]

@@ -231,6 +231,10 @@ class DateData:
     # (None: the Gram reads the shard; data parallel it is then summed over ranks)
     gram_feats: list | None = None
     gram_prices_next: list | None = None
+    # pinball LM fits: V_{t+1} on the same subsample paths ([ns]), so the IRLS
+    # Gram weights need no shard data and the fit is world-invariant (None:
+    # pinball fits read the subsample from the shard)
+    gram_target: torch.Tensor | None = None
 
 
 @dataclass
@@ -739,6 +743,7 @@ class HipBackend:
         (without it: this rank's part of the subsample, Gram summed over ranks)."""
         g = self._lm_buffers()["gram"]
         side = allow_side and data.gram_feats is not None and data.gram_prices_next is not None
+        lm.gtarget = data.gram_target.data_ptr() if (side and data.gram_target is not None) else None
         if side:
             gw, blk, stride, inv = g["side"]
             if data.gram_feats[0].numel() != gw * L.LM_TILE:
@@ -801,9 +806,10 @@ class HipBackend:
             raise ValueError("pinball LM fits have no multi-start exploration")
         b = self._lm_buffers(fcfg.loss)
         lm = b["desc"]
-        # (pinball: the Gram weights need the targets of the subsample paths,
-        # which the simulated global subsample does not carry: shard subsample)
-        self._lm_same_gram = self._lm_gram_mode(lm, data, allow_side=not pin)
+        # (pinball: the IRLS Gram weights need the targets of the subsample
+        # paths - the simulated subsample's own when the driver evaluated them
+        # (DateData.gram_target), else the shard subsample)
+        self._lm_same_gram = self._lm_gram_mode(lm, data, allow_side=(not pin or data.gram_target is not None))
         lm.q_delta = float(fcfg.lm_q_delta) if float(fcfg.lm_q_delta) > 0.0 else 1e-6
         lm.q_kappa = float(fcfg.lm_q_kappa)
         lm.passes = int(fcfg.epochs)
@@ -827,7 +833,7 @@ class HipBackend:
             lm.lam_carry = 1.0  # the polish starts at the chosen exploration's damping
         # data parallel on the shared Gram subsample with the xGMI mailbox: the
         # gradient region is summed inside k_lm_reduce (no extra launch per pass)
-        fused = (self.world > 1 and self.lm_mailbox is not None and self._lm_same_gram and not pin
+        fused = (self.world > 1 and self.lm_mailbox is not None and self._lm_same_gram
                  and not self.tcfg.lm_split)
         lm.dp_fused = 1 if fused else 0
         self.lm_last_fused = fused  # (transport probe record: which exchange this fit ran)
@@ -1117,7 +1123,10 @@ class HipBackend:
         n.pnl(d, self.stream)
 
     def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
-             v_out=None, hold_out=None, resid_out=None, pred1_out=None, snap_a=None, snap_b=None):
+             v_out=None, hold_out=None, resid_out=None, pred1_out=None, snap_a=None, snap_b=None,
+             n_local: int | None = None):
+        """k_hedge_eval over ``data`` (``n_local``: its path count when it is
+        not this backend's shard, e.g. the Gram subsample)."""
         n = self.native
         d = n.EvalDesc()
         d.snap_a = snap_a.data_ptr() if snap_a is not None else None
@@ -1142,7 +1151,9 @@ class HipBackend:
         d.bond_t, d.bond_t1 = float(data.bond_now), float(data.bond_next)
         d.alpha = float(self.spec.alpha)
         d.blend_c, d.hold_c = float(blend_c), float(hold_c)
-        d.n_local = self.n_local
+        d.n_local = self.n_local if n_local is None else int(n_local)
+        if d.n_local != int(data.feats[0].numel()):
+            raise ValueError(f"eval over {data.feats[0].numel()} paths with n_local {d.n_local}")
         d.num_wgs = self.eval_wgs
         d.nin, d.h, d.nout, d.head = self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head
         _set_norm(d, data)
@@ -1219,12 +1230,14 @@ class TorchBackend:
             return (torch_forward(spec, w, x[None])[0] * p).sum()
 
         side = None
-        if data.gram_feats is not None and data.gram_prices_next is not None and not pin:
-            # the simulated global Gram subsample (identical on every rank)
+        if data.gram_feats is not None and data.gram_prices_next is not None and (
+                not pin or data.gram_target is not None):
+            # the simulated global Gram subsample (identical on every rank; a
+            # pinball fit also needs its targets for the IRLS weights)
             Xs = _normalise(torch.stack([f.to(dt) for f in data.gram_feats], dim=1), data)
             ps = torch.stack([p.to(dt) for p in data.gram_prices_next] +
                              [torch.full((Xs.shape[0],), float(data.bond_next), dtype=dt)], dim=1)
-            side = (Xs, ps)
+            side = (Xs, ps, data.gram_target.to(dt) if data.gram_target is not None else None)
 
         def make_eval(n_loc: int, world: int, main: bool = False):
             """evaluate(w) -> (G, g, stats) over the first n_loc local paths
@@ -1240,7 +1253,7 @@ class TorchBackend:
                 ns, blk, bstride = gram_subsample(n_loc * world, t.lm_gram_paths)
                 inv_ns = 1.0 / float(ns)
                 if side is not None:
-                    Xg, pg, yg = side[0], side[1], None
+                    Xg, pg, yg = side
                 else:
                     sub = torch.tensor([(j // blk) * bstride + j % blk for j in range(ns)], dtype=torch.long)
                     Xg, pg, yg = Xn[sub], prn[sub], yn[sub]
@@ -1636,7 +1649,8 @@ class TorchBackend:
             stats[0].copy_(st)
 
     def eval(self, wts, data: DateData, stats, wts_b=None, g_base=None, blend_c=0.0, hold_c=0.0,
-             v_out=None, hold_out=None, resid_out=None, pred1_out=None, snap_a=None, snap_b=None):
+             v_out=None, hold_out=None, resid_out=None, pred1_out=None, snap_a=None, snap_b=None,
+             n_local: int | None = None):
         spec, dt = self.spec, torch.float32
         P = spec.nparams
         if snap_a is not None:

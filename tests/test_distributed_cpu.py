@@ -293,3 +293,57 @@ def test_dp_lm_multistart_two_ranks():
     x = run.backend.lm_explore_last
     assert x["losses"] == r0["losses"] and x["pick"] == r0["pick"]
     assert res.v0 == pytest.approx(r0["v0"], rel=1e-5)
+
+
+def _pin_params():
+    from rphedge import experiments
+
+    return experiments.mts_lm_parameters(n_paths=11, dt=0.25, rebalancing=1.0, T=4, device="cpu", backend="torch",
+                                         verbose=False, lm_starts=1, lm_explore_passes=0, lm_passes_first=10,
+                                         lm_passes_rest=2, lm_q_passes_first=8, lm_q_passes_rest=3,
+                                         lm_gram_paths=1024, concurrent_q99=False)
+
+
+def _pin_worker(rank, world, port, out):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.parallel import dist as D
+
+    di = D.init(device="cpu")
+    run = HedgeRun(parse_params(_pin_params()), dist_info=di)
+    res = run.run()
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump({"phi": res.phi, "psi": res.psi, "v0": res.v0}, f)
+    D.shutdown()
+
+
+def test_dp_pinball_lm_two_ranks_matches_single_process():
+    """Both fits on LM (pension, two networks) on 2 gloo ranks: the pinball
+    fits' IRLS Gram is built on the simulated global subsample with its own
+    targets (DateData.gram_target, evaluated at every date boundary), so only
+    the gradient region is all-reduced and the 2-rank run is the 1-process
+    run (torch oracle; RP:138-145, :217-221)."""
+    world, port = 2, _free_port()
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "pin.json")
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=_pin_worker, args=(r, world, port, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        dp = json.load(open(out))
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.parallel import dist as D
+
+    run = HedgeRun(parse_params(_pin_params()), dist_info=D.DistInfo(device=torch.device("cpu")))
+    assert run.build().induction.gvalues is not None   # the subsample carries its targets
+    ref = run.run()
+    for k in ("phi", "psi", "v0"):
+        assert dp[k] == pytest.approx(getattr(ref, k), rel=1e-5), (k, dp[k], getattr(ref, k))

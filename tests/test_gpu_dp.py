@@ -395,3 +395,93 @@ def test_transport_probe_catches_a_symmetric_wrong_sum():
         assert lm["max_rel_dev_vs_allreduce"] > lm["rtol"], lm
         assert r["lm_dp_mode"] == "rccl" and r["lm_comm"] == "TorchComm", r
         assert r["probe"]["packet"]["chosen"] == "xgmi"
+
+
+def _mts_lm_run(di, leaf, graph):
+    """experiments.mts_lm_parameters (both fits of every date on LM, 2^16
+    paths, 40 quarterly dates) in leaf mode: (result, snapshots, graph nodes,
+    k_lm_dp_exchange launches, whether the last pinball fit ran fused)."""
+    from rphedge import experiments
+    from rphedge.api import HedgeRun
+    from rphedge.config import parse_params
+    from rphedge.ops import native
+
+    calls = [0]
+    orig = native.lm_dp_exchange
+
+    def counted(*a, **kw):
+        calls[0] += 1
+        return orig(*a, **kw)
+
+    native.lm_dp_exchange = counted
+    try:
+        cfg = parse_params(experiments.mts_lm_parameters(n_paths=16, verbose=False, device="cuda:0",
+                                                         lm_leaf_paths=leaf, concurrent_q99=False,
+                                                         keep_paths=False))
+        run = HedgeRun(cfg, dist_info=di) if di is not None else HedgeRun(cfg)
+        res = run.run()
+        torch.cuda.synchronize()
+        fused = bool(run.backend.lm_last_fused)
+        nodes = None
+        if graph:
+            run.capture(include_simulation=True)
+            nodes = int(run.graph.num_nodes)
+        snap = run.induction.snap.cpu().numpy().copy()
+        out = dict(phi=res.phi, psi=res.psi, v0=res.v0, nodes=nodes, exchanges=calls[0], fused=fused)
+        run.close()
+        return out, snap
+    finally:
+        native.lm_dp_exchange = orig
+
+
+def _worker_mts(rank, world, port, out, leaf):
+    import json
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    from rphedge.parallel import dist as D
+
+    di = D.init()
+    rec, snap = _mts_lm_run(di, leaf, graph=True)
+    np.save(out + f".{rank}.npy", snap)
+    with open(out + f".{rank}.json", "w") as fh:
+        json.dump(rec, fh)
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_pension_both_fits_lm_world_invariant(world):
+    """The pension run with BOTH fits on LM, data parallel on one card: the
+    pinball (Q99) fits build their IRLS Gram on the simulated global subsample
+    with its own targets (V_{t+1} evaluated on the subsample at every date
+    boundary: DateData.gram_target), so every rank builds the same Gram and
+    the gradient region is summed inside k_lm_reduce - no k_lm_dp_exchange
+    launch at all, the same graph node count as one rank, and in leaf mode
+    every date's weights are bit for bit those of the one-rank run
+    (Replicating_Portfolio.py:138-145, :217-221)."""
+    import json
+
+    leaf = 256
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "m")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_mts, args=(r, world, port, out, leaf)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        recs = [json.load(open(out + f".{r}.json")) for r in range(world)]
+        snaps = [np.load(out + f".{r}.npy") for r in range(world)]
+    ref, snap1 = _mts_lm_run(None, leaf, graph=True)
+    for r in range(world):
+        assert recs[r]["exchanges"] == 0 and recs[r]["fused"] is True, recs[r]
+        assert np.array_equal(snaps[r], snap1), np.abs(snaps[r] - snap1).max()
+        for k in ("phi", "psi", "v0"):   # (per-rank eval statistics: summed in another order)
+            assert recs[r][k] == pytest.approx(ref[k], rel=1e-9), (k, recs[r][k], ref[k])
+        # no node per pass or per date: the only extra nodes are the 3 kernels
+        # simulating the multi-start's global path prefix once per run (path
+        # scan, mortality, payoff), which one rank reads from its own shard
+        assert recs[r]["nodes"] == ref["nodes"] + 3, (recs[r]["nodes"], ref["nodes"])
