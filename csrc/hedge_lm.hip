@@ -611,12 +611,27 @@ template <int P>
 RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, const float ridge, const float mu,
                               double* A, double* out, double* dl) {
 #pragma clang fp contract(off)
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int o0 = P - N, LDA = 65;
   __shared__ double s_rid;
-  for (int e = tid; e < N * N; e += 256) {
-    const int i = e / N, j = e % N;
-    A[i * LDA + j] = 2.0 * lm_og(gog, N, i, j);
+  double* const G2d = out + 64;  // the undamped diagonal 2 G_ii (the elimination overwrites A's)
+  // (row i = wid + 4 s, column j = lane: no integer division; every load of
+  // the packed Gram in flight before the first store)
+  {
+    double v[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int i = wid + 4 * s;
+      v[s] = (i < N && lane < N) ? lm_og(gog, N, i, lane) : 0.0;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int i = wid + 4 * s;
+      if (i < N && lane < N) {
+        A[i * LDA + lane] = 2.0 * v[s];
+        if (i == lane) G2d[i] = 2.0 * v[s];
+      }
+    }
   }
   __syncthreads();
   if (tid < 64) {
@@ -634,14 +649,18 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
   // LDL^T elimination over the whole workgroup (lower triangle): step k
   // subtracts A_ik A_jk / A_kk from every (i, j), k < j <= i; D_k = A_kk
   bool ok = true;
+  // (column j = k + 1 + lane, rows i = k + 1 + wid + 4 s >= j: the same
+  // update per entry as an e -> (i, j) enumeration, without its divisions;
+  // the upper triangle stays 2 G for the exact loss change below)
   for (int k = 0; k < N; ++k) {
     const double akk = A[k * LDA + k];
     ok = ok && akk > 0.0;
     const double inv = lm_rcp(akk);
-    const int m = N - k - 1;
-    for (int e = tid; e < m * m; e += 256) {
-      const int i = k + 1 + e / m, j = k + 1 + e % m;
-      if (j <= i) A[i * LDA + j] -= (A[i * LDA + k] * A[j * LDA + k]) * inv;
+    const int j = k + 1 + lane;
+    if (j < N) {
+      const double ajk = A[j * LDA + k];
+      for (int i = k + 1 + wid; i < N; i += 4)
+        if (j <= i) A[i * LDA + j] -= (A[i * LDA + k] * ajk) * inv;
     }
     __syncthreads();
   }
@@ -663,9 +682,14 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
     }
     if (lane >= N) b = 0.0;
     if (lane < N) out[lane] = b;
-    // exact loss change of the quadratic: g.d + d.G d (G undamped, full batch)
+    // exact loss change of the quadratic: g.d + d.G d (G undamped, full
+    // batch: A's untouched upper triangle and the saved diagonal, from LDS)
     double gd = 0.0;
-    for (int j = 0; j < N; ++j) gd += (lane < N ? lm_og(gog, N, lane, j) : 0.0) * lmc_readlane(b, j);
+    for (int j = 0; j < N; ++j) {
+      const int lo = lane < j ? lane : j, hi = lane < j ? j : lane;
+      const double gj = lane < N ? (lane == j ? G2d[lane] : A[lo * LDA + hi]) : 0.0;
+      gd += (0.5 * gj) * lmc_readlane(b, j);
+    }
     double t = b * (gi + gd);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
