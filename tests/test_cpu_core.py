@@ -205,6 +205,45 @@ def test_feature_norms_modes():
     assert ParityFlags.reference().raw_features and not ParityFlags().raw_features
 
 
+def test_feature_norms_horizon():
+    """feature_norm="horizon": price inputs centred at the kink, scaled by the
+    remaining-horizon spread m_t sd(log S_T - log S_t) (GBM: F_t sigma
+    sqrt(T - t)) floored at floor x the date spread; the fixed-point moment
+    sums make the scales independent of the path order (hence of the world
+    size); Heston's variance input keeps the date scale."""
+    from rphedge.driver import feature_norms
+    from rphedge.ops import paths as P
+
+    g = P.Grid(1.0, 0.1, 0.1)
+    sig = 0.2
+    p = P.simulate_gbm(g, 1 << 14, 1.0, 0.08, sig, device="cpu", scheme="log")
+    nd = p.n_coarse - 1
+    hz = feature_norms(p, "horizon", centers=(1.0,))
+    dt = feature_norms(p, "date")
+    tt = g.times()
+    for t in range(nd):
+        mu, isd = hz[t][0][0], hz[t][1][0]
+        assert mu == 1.0                                     # the strike
+        m = float(p.features(t)[0].double().mean())
+        want = m * sig * math.sqrt(1.0 - tt[t])              # F_t sigma sqrt(T - t)
+        assert 1.0 / isd == pytest.approx(want, rel=0.03), (t, 1.0 / isd, want)
+    # the floor binds late: scale >= 0.5 x the date spread
+    fl = feature_norms(p, "horizon", centers=(1.0,), floor=0.5)
+    t = nd - 1
+    assert 1.0 / fl[t][1][0] == pytest.approx(max(1.0 / hz[t][1][0], 0.5 / dt[t][1][0]), rel=1e-12)
+    # order-independent (exact int64 sums): a permuted path set gives the same bits
+    perm = torch.randperm(1 << 14, generator=torch.Generator().manual_seed(3))
+    q = P.simulate_gbm(g, 1 << 14, 1.0, 0.08, sig, device="cpu", scheme="log")
+    q.S = q.S[:, perm].contiguous()
+    assert feature_norms(q, "horizon", centers=(1.0,)) == hz
+    # Heston: the variance input keeps the date standardisation
+    h = P.simulate_sv(g, 1 << 12, 1.0, 0.05, 0.04, model="heston", kappa=2.0, theta=0.04, xi=0.5, rho=-0.7,
+                      device="cpu")
+    hh, hd = feature_norms(h, "horizon", centers=(1.0, None)), feature_norms(h, "date")
+    assert all(hh[t][0][1] == hd[t][0][1] and hh[t][1][1] == hd[t][1][1] for t in range(h.n_coarse - 1))
+    assert hh[3][0][0] == 1.0 and hh[3][1][0] != hd[3][1][0]
+
+
 def test_keras_adam_matches_torch_optim_adam_cpu():
     """Torch reference backend's Keras-Adam (K10 semantics) vs torch.optim.Adam
     for 3 full-batch steps; the per-step matching torch eps is eps/sqrt(1-b2^t)."""
