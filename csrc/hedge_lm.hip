@@ -128,7 +128,10 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   // than 64 x the path grid: the subsample is the same at every world size)
   const bool path_wg = (int)blockIdx.x < lm.num_wgs;
   typename B::Pre pre;
-  const typename B::Sched sc = B::sched(d, lm.num_wgs, lm.gram_wgs, lm.gram_skip, lm.leaf_blocks);
+  // (the output-Gram instantiation does not fit twice on a CU: its Gram tiles
+  // stay in the path workgroups)
+  const int gram_base = B::OGM ? 0 : lm.gram_base;
+  const typename B::Sched sc = B::sched(d, lm.num_wgs, gram_base > 0 ? 0 : lm.gram_wgs, lm.gram_skip, lm.leaf_blocks);
   if (path_wg) B::load(d, 0, perm, sc.b0 * 128, lane, pre);
   for (int i = tid; i < P; i += 256) {
     float w;
@@ -205,10 +208,11 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
       if (tid + 256 * j < R) slab_b[(size_t)blockIdx.x * R + tid + 256 * j] = val[j];
   }
   RPH_STAMPP(2);
-  if ((int)blockIdx.x >= lm.gram_wgs) return;
+  const int gtile = (int)blockIdx.x - gram_base;  // this workgroup's Gram tile
+  if (gtile < 0 || gtile >= lm.gram_wgs) return;
   // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
   if (wid == 0) {
-    const long long slot = (long long)blockIdx.x * LM_TILE + lane;
+    const long long slot = (long long)gtile * LM_TILE + lane;
     float x[NIN], pr[NHOLD];
     bool ok;
     if (lm.gram_side) {
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
       const float* row = jt + (2 * s + h) * JP;
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(row[mb * 32 + r], row[nb * 32 + r], acc, 0, 0, 0);
     }
-    float* out = slab_g + ((size_t)blockIdx.x * NBLK + b) * 1024;
+    float* out = slab_g + ((size_t)gtile * NBLK + b) * 1024;
 #pragma unroll
     for (int q = 0; q < 16; ++q) out[q * 64 + lane] = acc[q];
   }
@@ -373,7 +377,10 @@ RPH_INLINE double lm_dp_sum_wave(const LmDpDesc& x, const unsigned seq, const in
 // Reduce kernel: red[e] = fixed-order sums of the slabs.
 // ---------------------------------------------------------------------------
 // workgroups of the output-Gram part of k_lm_reduce (64 packed entries each)
-constexpr int lm_og_wgs(int NU) { return NU <= LM_OG_MAX ? (NU * (NU + 1) / 2 + 63) / 64 : 0; }
+// (16 packed entries per workgroup - every thread loads 4 rows, one round
+// trip - unless that needs more than 32 workgroups: then 64 entries x 16 rows)
+constexpr int lm_og_epw(int NU) { return NU * (NU + 1) / 2 <= 512 ? 16 : 64; }
+constexpr int lm_og_wgs(int NU) { return NU <= LM_OG_MAX ? (NU * (NU + 1) / 2 + lm_og_epw(NU) - 1) / lm_og_epw(NU) : 0; }
 
 // Gram slabs up to this many (the multi-start exploration's 16-workgroup
 // instances): k_lm_reduce sums each Gram entry in ONE thread (1,024 entries
@@ -412,9 +419,59 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       if (ob == 0 && tid == 0) red[LM_RED_OUTG] = -1.0;
       return;
     }
+    constexpr int NPK = NU * (NU + 1) / 2;
+    constexpr int EPW = lm_og_epw(NU);
+    auto slab_off = [&](const int e) {
+      int off = 0;
+      if (e < NPK) {
+        int i = 0, r = e;  // e -> (i, j), row-major upper triangle
+        while (r >= NU - i) {
+          r -= NU - i;
+          ++i;
+        }
+        const int j = i + r;
+        const int b = (i >> 5) == 0 ? ((j >> 5) == 0 ? 0 : 1) : 2;
+        const int ii = i & 31, jj = j & 31;
+        off = b * 1024 + ((ii & 3) + 4 * (ii >> 3)) * 64 + ((ii >> 2) & 1) * 32 + jj;
+      }
+      return off;
+    };
+    if constexpr (EPW == 16) {
+      // thread (wave w, k = lane / 16, le = lane % 16): entry 16 ob + le, rows
+      // 16 w + 4 k + [0, 4); the 4 rows, then the k pairs (xor 16, 32), then
+      // the 16 waves, each by an adjacent-pairs tree - the same perfect binary
+      // tree over the (<= 256) rows as the 64-entry form below, bit for bit
+      const int lane = tid & 63, w = tid >> 6, le = lane & 15, k = lane >> 4;
+      const int e = ob * 16 + le;
+      const float* const so = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024 + slab_off(e);
+      double r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = 16 * w + 4 * k + u;
+        r[u] = (e < NPK && row < lm.num_wgs) ? (double)so[(size_t)row * 3 * 1024] : 0.0;
+      }
+      double v = (r[0] + r[1]) + (r[2] + r[3]);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (k == 0) part[w * 16 + le] = v;
+      __syncthreads();
+      if (w == 0) {
+        double c[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) c[q] = part[q * 16 + le];
+#pragma unroll
+        for (int st = 1; st < 16; st <<= 1)
+#pragma unroll
+          for (int q = 0; q < 16; q += 2 * st) c[q] += c[q + st];
+        double t = c[0];
+        const bool act = k == 0 && e < NPK;
+        if (lm.dp_fused) t = lm_dp_sum_wave(lm.dp, seq, R / 4 + ob, t, LM_RED_OUTG - LM_GBLK_MAX + e, act);
+        if (act) red[LM_RED_OUTG + e] = t * (double)lm.inv_n;
+      }
+      return;
+    }
     const int l = tid & 63, g = tid >> 6;
     const int e = ob * 64 + l;
-    constexpr int NPK = NU * (NU + 1) / 2;
     int off = 0;
     if (e < NPK) {
       int i = 0, r = e;  // e -> (i, j), row-major upper triangle
@@ -1104,6 +1161,8 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (lm->leaf_blocks < 0 || (lm->leaf_blocks > 0 && (long long)lm->leaf_blocks * 128 * 4 * lm->num_wgs < d->batch))
     return rph_report("rph_lm", "leaf_blocks: the waves' leaves must cover the shard");
   if (lm->gram_wgs < 1 || lm->gram_wgs > 65535) return rph_report("rph_lm", "bad Gram workgroup count");
+  if (lm->gram_base != 0 && (lm->gram_base != lm->num_wgs || lm->inst != 1))
+    return rph_report("rph_lm", "gram_base: 0 or the path grid (one instance)");
   if (lm->gram_side) {
     // the subsample comes from gfeat / gprice ([gram_wgs x 64] each)
     const int nhold = d->head == HEAD_COMPLEMENT ? 2 : d->nout;
@@ -1148,8 +1207,9 @@ template <int A, int B, int C, int E>
 static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const double* red_new, hipStream_t s) {
   using K = LmKernels<A, B, C, E>;
   // path workgroups + Gram-only workgroups past them (Gram subsample > 64 x path grid)
-  const unsigned grid = (unsigned)(lm->gram_wgs > lm->num_wgs ? lm->gram_wgs : lm->num_wgs);
   const bool og = lm->out_gram && pass > lm->passes - LM_OUTG_TAIL;
+  const int gend = (og && K::BodyOG::OGM ? 0 : lm->gram_base) + lm->gram_wgs;
+  const unsigned grid = (unsigned)(gend > lm->num_wgs ? gend : lm->num_wgs);
   if constexpr (K::BodyOG::OGM) {
     // the last LM_OUTG_TAIL evaluations of an lm_out_fix fit build the output Gram
     if (og) {

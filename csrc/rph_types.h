@@ -349,6 +349,14 @@ struct LmDesc {
   // date boundary, driver.BackwardInduction), so the IRLS weights - and the
   // Gram - are the same on every rank; nullptr for MSE fits (J needs no target)
   const float* gtarget;
+  // first workgroup of the Gram tiles: 0 = the first gram_wgs path workgroups
+  // build them (after their share of the paths, gram_skip balancing);
+  // num_wgs = Gram-only workgroups after the path grid, which a second
+  // workgroup slot of the path workgroups' CUs runs beside them (the pass
+  // kernel fits two workgroups per CU), so every path workgroup takes the
+  // same share of the paths (the contiguous-leaf schedule's balance)
+  int gram_base;
+  int pad4;
 };
 
 // Multi-start selection block (k_lm_select): candidate c = (rank, instance)

@@ -69,7 +69,7 @@ extern "C" int rph_layout(long long* out, int cap) {
       // LmDesc + LM state layout
       (long long)sizeof(LmDesc), OFF(LmDesc, slab_b), OFF(LmDesc, slab_g), OFF(LmDesc, num_wgs),
       OFF(LmDesc, passes), OFF(LmDesc, gram_blk), OFF(LmDesc, inv_ns), OFF(LmDesc, lam0), OFF(LmDesc, ridge), OFF(LmDesc, bias_index), OFF(LmDesc, weights_only), OFF(LmDesc, damping), OFF(LmDesc, stop_tol), OFF(LmDesc, gram_skip),
-      OFF(LmDesc, inst), OFF(LmDesc, lam_carry), OFF(LmDesc, w0), OFF(LmDesc, renorm), OFF(LmDesc, ren_isd), OFF(LmDesc, out_n), OFF(LmDesc, gfeat), OFF(LmDesc, gprice), OFF(LmDesc, gram_side), OFF(LmDesc, q_delta), OFF(LmDesc, dp), OFF(LmDesc, dp_fused), OFF(LmDesc, gtarget), (long long)sizeof(LmDesc), (long long)LMS_LFIN, (long long)LMS_FAILTOT, (long long)LM_SEL_W, (long long)LM_DP_PITCH,
+      OFF(LmDesc, inst), OFF(LmDesc, lam_carry), OFF(LmDesc, w0), OFF(LmDesc, renorm), OFF(LmDesc, ren_isd), OFF(LmDesc, out_n), OFF(LmDesc, gfeat), OFF(LmDesc, gprice), OFF(LmDesc, gram_side), OFF(LmDesc, q_delta), OFF(LmDesc, dp), OFF(LmDesc, dp_fused), OFF(LmDesc, gtarget), OFF(LmDesc, gram_base), (long long)sizeof(LmDesc), (long long)LMS_LFIN, (long long)LMS_FAILTOT, (long long)LM_SEL_W, (long long)LM_DP_PITCH,
       (long long)sizeof(LmDpDesc), OFF(LmDpDesc, counter), OFF(LmDpDesc, world), OFF(LmDpDesc, pitch),
       (long long)LM_NPMAX, (long long)LM_RED, (long long)LMS_BEST, (long long)LMS_FLOATS,
       (long long)LM_SPEC, (long long)LMS_SPEC_W, (long long)LMS_SLOTS, (long long)LM_SLOT, (long long)LSS_LBEST, (long long)LSS_STOP,

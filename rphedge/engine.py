@@ -182,6 +182,9 @@ class TrainConfig:
     # block schedule with lm_gram_skip (default: 0.7 ms faster on the euro30
     # flagship, whose Gram workgroups then take fewer path blocks)
     lm_leaf_paths: int = -1
+    # the Gram tiles in Gram-only workgroups after the path grid (LmDesc.gram_base),
+    # co-resident with the path workgroups, instead of in the first path workgroups
+    lm_gram_overlap: bool = False
     # after the last pass: exact Newton step on the whole output layer (the
     # value is linear in it; 2 G_oo d = -g_o), subsuming the bias step
     lm_out_fix: bool = False
@@ -276,7 +279,9 @@ def lm_out_gram(spec) -> bool:
 def lm_og_wgs(spec) -> int:
     """Output-Gram workgroups of k_lm_reduce (64 packed entries each)."""
     nu = lm_out_nu(spec)
-    return (nu * (nu + 1) // 2 + 63) // 64 if nu <= L.LM_OG_MAX else 0
+    npk = nu * (nu + 1) // 2
+    epw = 16 if npk <= 512 else 64  # (csrc/hedge_lm.hip lm_og_epw)
+    return (npk + epw - 1) // epw if nu <= L.LM_OG_MAX else 0
 
 
 def _lm_out_n(spec, t) -> int:
@@ -758,6 +763,9 @@ class HipBackend:
             gw, blk, stride, inv = g["local"]
         lm.gram_side = 1 if side else 0
         lm.gram_wgs, lm.gram_blk, lm.gram_blk_stride, lm.inv_ns = gw, blk, stride, inv
+        ov = os.environ.get("RPH_LM_GRAM_OVERLAP")  # (env: A/B)
+        ov = bool(int(ov)) if ov is not None else bool(self.tcfg.lm_gram_overlap)
+        lm.gram_base = lm.num_wgs if (ov and int(lm.inst) == 1) else 0
         return side or self.world <= 1
 
     def lm_exchange_bytes(self) -> int:
@@ -900,6 +908,7 @@ class HipBackend:
             lm.w0 = bufs["w0"].data_ptr()
             lm.inst, lm.explore, lm.lam_carry, lm.weights_only, lm.stop_tol, lm.renorm = K, 1, 0.0, 0, 0.0, 0
             lm.out_n, lm.out_gram, lm.gram_side, lm.dp_fused = 0, 0, 0, 0  # (the prefix's own Gram subsample)
+            lm.gram_base = 0
             bufs["w0_rows"] = np.ascontiguousarray(rows).tobytes()
             lm.num_wgs, lm.gram_wgs, lm.leaf_blocks = nw, gw, leaf
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(nsub, gw * L.LM_TILE, 1)
@@ -1001,6 +1010,7 @@ class HipBackend:
             lm = type(src).from_buffer_copy(src)
             lm.passes, lm.weights_only, lm.gram_wgs, lm.stop_tol, lm.out_n, lm.out_gram = 0, 1, 1, 0.0, 0, 0
             lm.renorm, lm.lam_carry, lm.gram_side, lm.dp_fused = 0, 0.0, 0, 0  # (not inherited from the main fit's desc)
+            lm.gram_base = 0
             lm.gram_blk, lm.gram_blk_stride = lm_gram_geometry(self.n_local, L.LM_TILE, self.world)
             lm.inv_ns = 1.0 / float(L.LM_TILE * max(self.world, 1))
             return lm

@@ -102,6 +102,7 @@ class LmDesc(C.Structure):
         ("slab_o", VP),
         ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("q_delta", C.c_float), ("q_kappa", C.c_float),
         ("dp", LmDpDesc), ("dp_fused", C.c_int), ("leaf_blocks", C.c_int), ("gtarget", VP),
+        ("gram_base", C.c_int), ("pad4", C.c_int),
     ]
 
     def __init__(self, *a, **kw):
@@ -151,7 +152,7 @@ def _expected_layout() -> list[int]:
         LmDesc.ridge.offset, LmDesc.bias_index.offset, LmDesc.weights_only.offset, LmDesc.damping.offset, LmDesc.stop_tol.offset, LmDesc.gram_skip.offset,
         LmDesc.inst.offset, LmDesc.lam_carry.offset, LmDesc.w0.offset, LmDesc.renorm.offset,
         LmDesc.ren_isd.offset, LmDesc.out_n.offset, LmDesc.gfeat.offset, LmDesc.gprice.offset,
-        LmDesc.gram_side.offset, LmDesc.q_delta.offset, LmDesc.dp.offset, LmDesc.dp_fused.offset, LmDesc.gtarget.offset, C.sizeof(LmDesc),
+        LmDesc.gram_side.offset, LmDesc.q_delta.offset, LmDesc.dp.offset, LmDesc.dp_fused.offset, LmDesc.gtarget.offset, LmDesc.gram_base.offset, C.sizeof(LmDesc),
         L.LMS_LFIN, L.LMS_FAILTOT, L.LM_SEL_W, L.LM_DP_PITCH,
         C.sizeof(LmDpDesc), LmDpDesc.counter.offset, LmDpDesc.world.offset, LmDpDesc.pitch.offset,
         L.LM_NPMAX, L.LM_RED, L.LMS_BEST, L.LMS_FLOATS,
