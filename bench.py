@@ -209,7 +209,8 @@ def parse(argv=None):
     ap.add_argument("--cpu", action="store_true", help="torch reference backend (plumbing only)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--seed", type=int, default=1234, help="weight-init seed (the reference's 1234)")
-    ap.add_argument("--init", default=None, choices=["reference", "spread"], help="weight init (default: preset)")
+    ap.add_argument("--init", default=None, choices=["reference", "spread", "aligned"],
+                    help="weight init (default: preset); aligned = spread + first layer along the basket weights")
     a = ap.parse_args(argv)
     pre = PRESETS[a.preset]
     for k in ("paths_log2", "dates", "substeps", "epochs_first", "epochs_rest", "batch_log2", "lr", "lr_rest"):

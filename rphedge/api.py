@@ -243,6 +243,15 @@ class HedgeRun:
                            else float(yT.double().sum())) / n * (c.Y if self.kind != "pension" else 1.0)
         return out
 
+    def init_align(self) -> tuple | None:
+        """init="aligned": the first layer's direction in the standardised
+        input space - the basket weights (every asset input is standardised
+        alike); None for single-price nets (aligned = spread there)."""
+        c = self.cfg
+        if str(getattr(c.train, "init", "reference")) != "aligned" or self.kind != "basket":
+            return None
+        return tuple(c.basket_weights or [1.0 / c.n_assets] * c.n_assets)
+
     def feature_centers(self) -> tuple | None:
         """The payoff kink of every price feature in the paths' units
         (feature_norm="horizon"): the strike K / Y of a call / put, K / Y per
@@ -268,7 +277,8 @@ class HedgeRun:
             if self.kind == "basket":
                 bias = [p_itm / c.n_assets] * c.n_assets + [stats["E_payoff"] - p_itm]
         return hm.init_weights(spec, bias[: spec.nout], seed=c.train.seed,
-                               spread=str(getattr(c.train, "init", "reference")) == "spread",
+                               spread=str(getattr(c.train, "init", "reference")) in ("spread", "aligned"),
+                               align=self.init_align(),
                                shared_stream=bool(c.parity.shared_initializer))
 
     def build(self, w0: np.ndarray | None = None):
@@ -333,7 +343,8 @@ class HedgeRun:
                                lm_renorm=bool(tr.lm_renorm),
                                lm_explore_passes=int(tr.lm_explore_passes), lm_explore_log2=int(tr.lm_explore_log2),
                                lm_explore_one=bool(getattr(tr, "lm_explore_one", False)),
-                               init_spread=str(getattr(tr, "init", "reference")) == "spread",
+                               init_spread=str(getattr(tr, "init", "reference")) in ("spread", "aligned"),
+                               init_align=self.init_align(),
                                init_shared_stream=bool(pf.shared_initializer),
                                mean_refit=bool(tr.mean_refit) and not pf.keras_fit_only)
         backend_q = None

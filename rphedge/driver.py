@@ -86,6 +86,7 @@ class InductionConfig:
     # the extra start points use the run's initialiser (TrainingParams.init,
     # ParityFlags.shared_initializer), so candidate 0 is not the odd one out
     init_spread: bool = False
+    init_align: tuple | None = None      # init="aligned": first-layer direction (models.hedge_mlp.init_weights)
     init_shared_stream: bool = False
     # after each Adam MSE fit: exact refit of the bond holding's output bias
     # (engine bias_refit; LM fits do it in their last solve)
@@ -189,7 +190,7 @@ class BackwardInduction:
             o = spec.offsets
             b3 = np.asarray(w0, np.float32)[o["b3"]:o["P"]]
             rows = [np.asarray(w0, np.float32)] + [hm.init_weights(spec, b3, seed=icfg.seed + 1000 * c,
-                                                                   spread=icfg.init_spread,
+                                                                   spread=icfg.init_spread, align=icfg.init_align,
                                                                    shared_stream=icfg.init_shared_stream)
                                                    for c in range(1, icfg.lm_starts)]
             self.lm_w0s = np.stack(rows)

@@ -132,7 +132,7 @@ def philox_normal(n: int, seed: int, stream: int = 0) -> np.ndarray:
 
 
 def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1,
-                 spread: bool = False, shared_stream: bool = False) -> np.ndarray:
+                 spread: bool = False, shared_stream: bool = False, align=None) -> np.ndarray:
     """Reference initialisation: kernels ~ N(0, 0.1) (seed 1234), hidden biases 0,
     output bias data-dependent (Q11: ``[1-p_oom, p_oom]`` pension,
     ``mean(payoff)/S0`` European).
@@ -146,7 +146,14 @@ def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1,
     ``shared_stream``: every kernel is a prefix of ONE normal stream (the
     reference's single seeded initializer instance reused for all layers,
     RP:149 / :154-156, under a stateless seeded generator): W2 and W3 begin
-    with W1's values (ParityFlags.shared_initializer)."""
+    with W1's values (ParityFlags.shared_initializer).
+
+    ``align`` (a direction in the standardised input space, e.g. the basket
+    weights): every first-layer kernel column is turned towards +-align (its
+    norm kept, 0.3 of its random direction left so the units stay distinct),
+    so the hidden units start as functions of the payoff's own coordinate
+    (the basket level) instead of random asset combinations; implies
+    ``spread``."""
     o = spec.offsets
     w = np.zeros(spec.nparams, dtype=np.float32)
     for k, (name, shp) in enumerate(spec.shapes()):
@@ -154,6 +161,17 @@ def init_weights(spec: NetSpec, out_bias, seed: int = 1234, stddev: float = 0.1,
             n = int(np.prod(shp))
             start = {0: o["W1"], 2: o["W2"], 4: o["W3"]}[k]
             w[start:start + n] = (stddev * philox_normal(n, seed, stream=0 if shared_stream else k)).astype(np.float32)
+    if align is not None and spec.nin > 1:
+        u = np.asarray(align, dtype=np.float64)[: spec.nin]
+        u = u / np.linalg.norm(u)
+        W1 = w[o["W1"]:o["b1"]].reshape(spec.nin, spec.hidden).astype(np.float64)
+        nrm = np.linalg.norm(W1, axis=0)
+        r = W1 / np.where(nrm > 0, nrm, 1.0)
+        sg = np.where(u @ r >= 0.0, 1.0, -1.0)
+        d = sg[None, :] * u[:, None] + 0.3 * r
+        W1 = d / np.linalg.norm(d, axis=0) * nrm
+        w[o["W1"]:o["b1"]] = W1.reshape(-1).astype(np.float32)
+        spread = True
     if spread and spec.hidden > 1:
         W1 = w[o["W1"]:o["b1"]].reshape(spec.nin, spec.hidden).astype(np.float64)
         c = np.linspace(-1.5, 1.5, spec.hidden)
