@@ -664,30 +664,38 @@ RPH_INLINE double lm_og(const double* gog, int N, int i, int j) {
   return gog[lo * N - lo * (lo - 1) / 2 + (hi - lo)];
 }
 
+// ``pre`` (N * N <= 512): the caller's prefetched entries e = tid and tid +
+// 256 of the row-major N x N Gram and this lane's gradient entry (loaded in
+// the solve's prologue with everything else: no dependent round trip here)
+struct LmOgPre {
+  double v[2];
+  double gi;
+};
+
 template <int P>
 RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, const float ridge, const float mu,
-                              double* A, double* out, double* dl) {
+                              double* A, double* out, double* dl, const LmOgPre* pre = nullptr) {
 #pragma clang fp contract(off)
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int o0 = P - N, LDA = 65;
   __shared__ double s_rid;
   double* const G2d = out + 64;  // the undamped diagonal 2 G_ii (the elimination overwrites A's)
-  // (row i = wid + 4 s, column j = lane: no integer division; every load of
-  // the packed Gram in flight before the first store)
-  {
-    double v[16];
+  if (pre != nullptr) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int i = wid + 4 * s;
-      v[s] = (i < N && lane < N) ? lm_og(gog, N, i, lane) : 0.0;
-    }
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int i = wid + 4 * s;
-      if (i < N && lane < N) {
-        A[i * LDA + lane] = 2.0 * v[s];
-        if (i == lane) G2d[i] = 2.0 * v[s];
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u;
+      if (e < N * N) {
+        const int i = e / N, j = e % N;
+        A[i * LDA + j] = 2.0 * pre->v[u];
+        if (i == j) G2d[i] = 2.0 * pre->v[u];
       }
+    }
+  } else {
+    for (int e = tid; e < N * N; e += 256) {
+      const int i = e / N, j = e % N;
+      const double v = 2.0 * lm_og(gog, N, i, j);
+      A[i * LDA + j] = v;
+      if (i == j) G2d[i] = v;
     }
   }
   __syncthreads();
@@ -706,18 +714,16 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
   // LDL^T elimination over the whole workgroup (lower triangle): step k
   // subtracts A_ik A_jk / A_kk from every (i, j), k < j <= i; D_k = A_kk
   bool ok = true;
-  // (column j = k + 1 + lane, rows i = k + 1 + wid + 4 s >= j: the same
-  // update per entry as an e -> (i, j) enumeration, without its divisions;
+  // (one or two entries per thread: every load of a step in flight at once;
   // the upper triangle stays 2 G for the exact loss change below)
   for (int k = 0; k < N; ++k) {
     const double akk = A[k * LDA + k];
     ok = ok && akk > 0.0;
     const double inv = lm_rcp(akk);
-    const int j = k + 1 + lane;
-    if (j < N) {
-      const double ajk = A[j * LDA + k];
-      for (int i = k + 1 + wid; i < N; i += 4)
-        if (j <= i) A[i * LDA + j] -= (A[i * LDA + k] * ajk) * inv;
+    const int m = N - k - 1;
+    for (int e = tid; e < m * m; e += 256) {
+      const int i = k + 1 + e / m, j = k + 1 + e % m;
+      if (j <= i) A[i * LDA + j] -= (A[i * LDA + k] * A[j * LDA + k]) * inv;
     }
     __syncthreads();
   }
@@ -726,7 +732,7 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
     // 1 / D_i (v_rcp_f64 + one Newton step, as lm_rcp)
     const double di = lane < N ? A[lane * LDA + lane] : 1.0;
     const double ri = lm_rcp(di);
-    const double gi = lane < N ? g[o0 + lane] : 0.0;
+    const double gi = lane < N ? (pre != nullptr ? pre->gi : g[o0 + lane]) : 0.0;
     double b = -gi;
     for (int k = 0; k < N; ++k) {
       const double zk = lmc_readlane(b, k) * lmc_readlane(ri, k);  // L_ik z_k = A_ik (z_k / D_k)
@@ -756,6 +762,114 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
   return ok;
 }
 
+// lm_out_newton for the net's own N = NU <= 22 output parameters with the
+// prologue's prefetched entries: the same arithmetic in the same order
+// (bitwise the same step), but after the workgroup-wide fill ONE wave does
+// the elimination (wave-synchronous LDS, a wavefront fence per column instead
+// of a workgroup barrier; compile-time N, every step's loads in flight at
+// once) and the triangular solves with each lane's row / column of the
+// factor loaded up front (readlane + fma chains only).  Every thread calls it.
+template <int P, int N>
+RPH_INLINE bool lm_out_newton_w1(const LmOgPre& pre, const float ridge, const float mu, double* A, double* out,
+                                 double* dl) {
+#pragma clang fp contract(off)
+  static_assert(N >= 1 && N * N <= 512, "prefetched output step: N * N <= 512");
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int LDA = 65;
+  __shared__ int s_ok;
+  double* const G2d = out + 64;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + 256 * u;
+    if (e < N * N) {
+      const int i = e / N, j = e % N;
+      A[i * LDA + j] = 2.0 * pre.v[u];
+      if (i == j) G2d[i] = 2.0 * pre.v[u];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    double dg = lane < N ? A[lane * LDA + lane] : 0.0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dg += __shfl_xor(dg, o, 64);
+    const double rid = (double)ridge * dg / (double)N;
+    if (lane < N) {
+      const double a = A[lane * LDA + lane];
+      A[lane * LDA + lane] = (a + a * (double)mu) + rid;
+    }
+    lmc_wave_sync();
+    bool ok = true;
+    lm_static_for<N>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int MK = N - k - 1;                 // trailing rows / columns
+      constexpr int NT = (MK * MK + 63) / 64;       // square slots per lane (c > r skipped)
+      const double akk = A[k * LDA + k];
+      double aik[NT > 0 ? NT : 1], ajk[NT > 0 ? NT : 1], aij[NT > 0 ? NT : 1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int e = lane + 64 * t < MK * MK ? lane + 64 * t : 0;
+        const int i = k + 1 + e / MK, j = k + 1 + e % MK;
+        aik[t] = A[i * LDA + k];
+        ajk[t] = A[j * LDA + k];
+        aij[t] = A[i * LDA + j];
+      }
+      ok = ok && akk > 0.0;
+      const double inv = lm_rcp(akk);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int e = lane + 64 * t;
+        if (e < MK * MK) {
+          const int i = k + 1 + e / MK, j = k + 1 + e % MK;
+          if (j <= i) A[i * LDA + j] = aij[t] - (aik[t] * ajk[t]) * inv;
+        }
+      }
+      lmc_wave_sync();
+    });
+    // L z = b, z / D, L^T d = z (lm_out_newton's order): this lane's row and
+    // column of the factor first
+    const int li = lane < N ? lane : 0;
+    double rw[N], cl[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      rw[k] = A[li * LDA + k];
+      cl[k] = A[k * LDA + li];
+    }
+    const double di = lane < N ? A[lane * LDA + lane] : 1.0;
+    const double ri = lm_rcp(di);
+    const double gi = lane < N ? pre.gi : 0.0;
+    double b = -gi;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const double zk = lmc_readlane(b, k) * lmc_readlane(ri, k);
+      if (lane > k && lane < N) b -= rw[k] * zk;
+    }
+    b *= ri;
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
+      const double dk = lmc_readlane(b, k);
+      if (lane < k) b -= (cl[k] * ri) * dk;
+    }
+    if (lane >= N) b = 0.0;
+    if (lane < N) out[lane] = b;
+    // exact loss change: g.d + d.G d (G undamped: A's upper triangle, G2d)
+    double gd = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double gj = lane < N ? (lane == j ? G2d[li] : (lane < j ? rw[j] : cl[j])) : 0.0;
+      gd += (0.5 * gj) * lmc_readlane(b, j);
+    }
+    double t = b * (gi + gd);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) {
+      *dl = t;
+      s_ok = ok ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
 // Solve kernel, LM_SPEC workgroups.  Every workgroup takes the same
 // accept / reject decision from the same inputs (the scalar slot of this
 // pass's parity, which no workgroup of this launch writes: workgroup 0
@@ -767,7 +881,7 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
 //    system at the damping after m further consecutive rejections (m = 0 is
 //    this solve's own step) — the same arithmetic a later serial solve would
 //    do, so the results are bitwise those of one-solve-per-pass.
-template <int P, int R>
+template <int P, int R, int NU>
 __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDesc lm, const double* __restrict__ red_new,
                                                   const int pass) {
   // no implicit fma contraction: every workgroup (own step or a speculative
@@ -831,6 +945,28 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     ds_new[k] = lmc_gram<TileGrid<P>::NBG>(red_new, i, i);
     ds_old[k] = lmc_gram<TileGrid<P>::NBG>(best_red, i, i);
   }
+  // final pass: the output step's inputs for either outcome (the trial's and
+  // the best point's packed output Gram, its marker and gradient entries)
+  // with the rest of the prologue - a dependent round trip each otherwise
+  const bool final_pass = pass == lm.passes;
+  constexpr bool OG_PRE = NU * NU <= 512;
+  LmOgPre og_pre[2];  // [trial block, best block]
+  double ogm_new = -1.0, ogm_old = -1.0;
+  if constexpr (OG_PRE) {
+    if (final_pass && m == 0 && lm.out_gram && lm.out_n == NU) {
+      ogm_new = red_new[LM_RED_OUTG];
+      ogm_old = best_red[LM_RED_OUTG];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u < NU * NU ? tid + 256 * u : 0;
+        og_pre[0].v[u] = lm_og(red_new + LM_RED_OUTG, NU, e / NU, e % NU);
+        og_pre[1].v[u] = lm_og(best_red + LM_RED_OUTG, NU, e / NU, e % NU);
+      }
+      const int gl = P - NU + (lane < NU ? lane : 0);
+      og_pre[0].gi = red_new[LM_GBLK_MAX + gl];
+      og_pre[1].gi = best_red[LM_GBLK_MAX + gl];
+    }
+  }
   const int best_old = pass == 0 ? 1 : (int)sv_best;
   const int trial = 1 - best_old;
   const double Lt = t_loss / fmax(cnt, 1.0);
@@ -860,7 +996,6 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
   } else {
     lam = fmin(lam * lm.lam_up, (double)lm.lam_max);
   }
-  const bool final_pass = pass == lm.passes;
   // a rejection whose step the last full solve precomputed (same damping,
   // same best point: rejections do not move it)
   double sl = 0.0, so = 0.0, sq = 0.0;
@@ -936,24 +1071,30 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     // the best point when it was accepted, else at the rejected last trial -
     // published when trial + step beats the best point (its loss change is
     // exact: the trial's own full-batch Gram and gradient)
-    const bool have_og = on_ok && src[LM_RED_OUTG] >= 0.0;
-    bool out_ok = have_og && lm_out_newton<P>(src + LM_RED_OUTG, g, on, lm.ridge, lm.out_mu, lds,
-                                              lds + 64 * 65, &s_dl);
+    const bool pre_ok = OG_PRE && on == NU;  // (the prologue loaded both candidates)
+    const bool have_og = on_ok && (pre_ok ? (accept ? ogm_new : ogm_old) : src[LM_RED_OUTG]) >= 0.0;
+    auto newton = [&](const double* gog, const double* gg, const LmOgPre* pr) {
+      if constexpr (OG_PRE) {
+        if (pre_ok) return lm_out_newton_w1<P, NU>(*pr, lm.ridge, lm.out_mu, lds, lds + 64 * 65, &s_dl);
+      }
+      return lm_out_newton<P>(gog, gg, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65, &s_dl, pre_ok ? pr : nullptr);
+    };
+    bool out_ok = have_og && newton(src + LM_RED_OUTG, g, &og_pre[accept ? 0 : 1]);
     bool use_trial = false;
     // (only for a trial within 2x the best loss: the step must then remove
     // little more than Lt - Lb, and its predicted change, exact up to the
     // Gram's ~1e-5 rounding, is a reliable decision - a far-off trial's
     // Lt + dl would cancel catastrophically)
-    if (!have_og && !stopped && !accept && on_ok && red_new[LM_RED_OUTG] >= 0.0 && Lt == Lt && Lt < 2.0 * Lb) {
-      const bool ok_t = lm_out_newton<P>(red_new + LM_RED_OUTG, red_new + LM_GBLK_MAX, on, lm.ridge, lm.out_mu,
-                                         lds, lds + 64 * 65, &s_dl);
+    if (!have_og && !stopped && !accept && on_ok && (pre_ok ? ogm_new : red_new[LM_RED_OUTG]) >= 0.0 && Lt == Lt &&
+        Lt < 2.0 * Lb) {
+      const bool ok_t = newton(red_new + LM_RED_OUTG, red_new + LM_GBLK_MAX, &og_pre[0]);
       use_trial = ok_t && Lt == Lt && Lt + s_dl < Lb;
       out_ok = use_trial;
     }
     __syncthreads();
     const int pub_pt = use_trial ? trial : best;  // the point the published weights start from
     for (int i = tid; i < P; i += 256) {
-      double wd = st[LMS_W + pub_pt * LM_NPMAX + i];
+      double wd = pub_pt == 0 ? w_slot0 : w_slot1;  // (the prologue's loads: i = tid < P <= 256)
       if (out_ok) {
         if (i >= P - on) wd += lds[64 * 65 + i - (P - on)];
       } else if (i == lm.bias_index) {
@@ -1515,7 +1656,7 @@ extern "C" int rph_lm_solve(const TrainDesc* d, const LmDesc* lm, const double* 
     const int bytes = K::smem();                                                                       \
     static bool attr = false;                                                                          \
     if (!attr) {                                                                                       \
-      hipError_t e = hipFuncSetAttribute((const void*)k_lm_solve<K::S::P, K::S::R>,                   \
+      hipError_t e = hipFuncSetAttribute((const void*)k_lm_solve<K::S::P, K::S::R, K::Body::NU>,                   \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, bytes);           \
       if (e != hipSuccess) {                                                                           \
         (void)hipGetLastError(); /* do not leave the error for the next runtime call */                \
@@ -1523,7 +1664,7 @@ extern "C" int rph_lm_solve(const TrainDesc* d, const LmDesc* lm, const double* 
       }                                                                                                \
       attr = true;                                                                                     \
     }                                                                                                  \
-    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R>), dim3(LM_SPEC, lm->inst), dim3(256), bytes, s, *d, *lm, \
+    hipLaunchKernelGGL((k_lm_solve<K::S::P, K::S::R, K::Body::NU>), dim3(LM_SPEC, lm->inst), dim3(256), bytes, s, *d, *lm, \
                        red_new, pass);                                                                 \
     return (int)hipGetLastError();                                                                     \
   }

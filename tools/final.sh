@@ -2,7 +2,7 @@
 # Round-end rehearsal on one GPU: smoke, the GPU suite, the euro30 bench and a
 # rocprofv3 kernel-stats run of it; outputs under gpurun_out/final/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/final
+OUT=${1:-gpurun_out/final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail -5 $OUT/smoke.log; exit 1; }
