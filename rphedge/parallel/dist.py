@@ -259,19 +259,34 @@ def _probe_xgmi_local(info: DistInfo, mb, lmb, lm: bool) -> tuple[bool, torch.Te
     # corrupts the fused LM sum itself (rank W-1 dropped on every rank)
     inj = os.environ.get("RPH_PROBE_FAIL", "")
     inj_rank = os.environ.get("RPH_PROBE_FAIL_RANK")
-    if inj and (inj == "both" or inj == ("lm" if lm else "packet")) and (
-            inj_rank is None or int(inj_rank) == info.rank):
+    injected = bool(inj and (inj == "both" or inj == ("lm" if lm else "packet")) and (
+        inj_rank is None or int(inj_rank) == info.rank))
+    if injected and not (lm and inj_rank is not None):
         return False, None, rec
-    try:
-        if lm:
-            fault = 1 if os.environ.get("RPH_PROBE_FAULT", "") == "lm_drop" else 0
-            wv, fused, clean = _probe_lm_fit(info, mb, lmb=lmb, fault=fault)
+    if lm:
+        # the fused fit, then - on EVERY rank, whatever the fused fit did (a
+        # raising rank must not skip the reference fit's collectives) - the
+        # reference fit over the process group
+        fault = 1 if os.environ.get("RPH_PROBE_FAULT", "") == "lm_drop" else 0
+        wv = wr = None
+        fused = clean = False
+        if not injected:  # (a one-rank injection still joins the reference fit's collectives)
+            try:
+                wv, fused, clean = _probe_lm_fit(info, mb, lmb=lmb, fault=fault)
+            except Exception as e:
+                rec["exception"] = f"{type(e).__name__}: {e}"[:200]
+        try:
             wr, _, _ = _probe_lm_fit(info, mb, lm_comm=TorchComm(info.device))
-            dev = float((wv - wr).abs().max().item() / max(float(wr.abs().max().item()), 1e-30))
-            rec = {"fused": fused, "clean": clean, "max_rel_dev_vs_allreduce": dev, "rtol": PROBE_RTOL,
-                   "fault_injected": bool(fault)}
-            ok = fused and clean and bool(torch.isfinite(wv).all()) and dev <= PROBE_RTOL
-            return ok, wv, rec
+        except Exception as e:
+            rec["exception_reference"] = f"{type(e).__name__}: {e}"[:200]
+        if wv is None or wr is None:
+            return False, wv, rec
+        dev = float((wv - wr).abs().max().item() / max(float(wr.abs().max().item()), 1e-30))
+        rec.update({"fused": fused, "clean": clean, "max_rel_dev_vs_allreduce": dev, "rtol": PROBE_RTOL,
+                    "fault_injected": bool(fault)})
+        ok = fused and clean and bool(torch.isfinite(wv).all()) and dev <= PROBE_RTOL
+        return ok, wv, rec
+    try:
         n = 1 << 12
         g = torch.Generator().manual_seed(100 + info.rank)          # different data per rank
         x = (torch.rand(n, generator=g) * 0.6 + 0.7).to(info.device)
