@@ -199,6 +199,8 @@ def parse(argv=None):
                     help="LM fits end with the exact Newton step on the whole output layer")
     ap.add_argument("--lm-out-mu", type=float, default=None, help="relative damping of the output-layer step")
     ap.add_argument("--lm-ridge", type=float, default=None, help="LM systems: + this x the mean diagonal")
+    ap.add_argument("--lm-out-tr", type=float, default=None,
+                    help="output-layer step trust region: ||d|| <= this x ||w_o|| (0: off)")
     ap.add_argument("--lm-renorm", type=int, default=None, choices=[0, 1],
                     help="later dates: warm start re-expressed for the date's input standardisation")
     ap.add_argument("--lm-explore-passes", type=int, default=None, help="trial points of every exploration fit")
@@ -233,7 +235,7 @@ def parse(argv=None):
                     ("lm_stop_tol", 0.0), ("lm_stop_min", 2), ("lm_lam0_rest", 0.0), ("lm_lam0_first", 0.0),
                     ("lm_lam_carry", 0.0),
                     ("lm_starts", 1), ("lm_explore_passes", 45), ("lm_explore_log2", 16), ("lm_explore_one", 0), ("lm_renorm", 0), ("lm_out_fix", 0),
-                    ("lm_out_mu", 1e-5), ("lm_ridge", 1e-10), ("lm_leaf_paths", -1)):
+                    ("lm_out_mu", 1e-5), ("lm_out_tr", 0.0), ("lm_ridge", 1e-10), ("lm_leaf_paths", -1)):
         if getattr(a, k) is None:
             setattr(a, k, pre.get(k, dflt))
     if pre.get("cpu"):
@@ -259,7 +261,7 @@ def build_run(a, world: int):
                         lm_lam_carry=a.lm_lam_carry, lm_starts=a.lm_starts, lm_explore_passes=a.lm_explore_passes,
                         lm_explore_log2=a.lm_explore_log2, lm_explore_one=bool(a.lm_explore_one),
                         lm_renorm=bool(a.lm_renorm), lm_out_fix=bool(a.lm_out_fix),
-                        lm_out_mu=a.lm_out_mu, lm_ridge=a.lm_ridge, lm_leaf_paths=a.lm_leaf_paths)
+                        lm_out_mu=a.lm_out_mu, lm_out_tr=a.lm_out_tr, lm_ridge=a.lm_ridge, lm_leaf_paths=a.lm_leaf_paths)
     model = pre["model"]
     kw = dict(Y=100.0, K=100.0, T=1.0, mu=0.08, r=0.08, sigma=0.15, rebalancing=1.0 / a.dates,
               dt=1.0 / (a.dates * a.substeps), n_paths=a.paths_log2 + int(math.log2(world)),

@@ -753,10 +753,16 @@ RPH_INLINE bool lm_out_newton(const double* gog, const double* g, const int N, c
       const double gj = lane < N ? (lane == j ? G2d[lane] : A[lo * LDA + hi]) : 0.0;
       gd += (0.5 * gj) * lmc_readlane(b, j);
     }
-    double t = b * (gi + gd);
+    double t = b * (gi + gd), tl = b * gi;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
-    if (lane == 0) *dl = t;
+    for (int o = 32; o >= 1; o >>= 1) {
+      t += __shfl_xor(t, o, 64);
+      tl += __shfl_xor(tl, o, 64);
+    }
+    if (lane == 0) {
+      *dl = t;
+      dl[1] = tl;  // g.d (the linear part; the quadratic part d.G d = dl - g.d)
+    }
   }
   __syncthreads();
   return ok;
@@ -858,11 +864,15 @@ RPH_INLINE bool lm_out_newton_w1(const LmOgPre& pre, const float ridge, const fl
       const double gj = lane < N ? (lane == j ? G2d[li] : (lane < j ? rw[j] : cl[j])) : 0.0;
       gd += (0.5 * gj) * lmc_readlane(b, j);
     }
-    double t = b * (gi + gd);
+    double t = b * (gi + gd), tl = b * gi;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    for (int o = 32; o >= 1; o >>= 1) {
+      t += __shfl_xor(t, o, 64);
+      tl += __shfl_xor(tl, o, 64);
+    }
     if (lane == 0) {
       *dl = t;
+      dl[1] = tl;
       s_ok = ok ? 1 : 0;
     }
   }
@@ -1065,7 +1075,8 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     // full-batch output Gram (when the best point's pass built it), else on
     // the bond bias alone
     const int on = lm.out_n;
-    __shared__ double s_dl;
+    __shared__ double s_dl2[2];  // the step's exact loss change, its linear part g.d
+    double& s_dl = s_dl2[0];
     const bool on_ok = on > 0 && on <= LM_OG_MAX && on <= P && lm.out_gram;
     // the last evaluation (this pass) built the output Gram: the out step at
     // the best point when it was accepted, else at the rejected last trial -
@@ -1075,11 +1086,45 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     const bool have_og = on_ok && (pre_ok ? (accept ? ogm_new : ogm_old) : src[LM_RED_OUTG]) >= 0.0;
     auto newton = [&](const double* gog, const double* gg, const LmOgPre* pr) {
       if constexpr (OG_PRE) {
-        if (pre_ok) return lm_out_newton_w1<P, NU>(*pr, lm.ridge, lm.out_mu, lds, lds + 64 * 65, &s_dl);
+        if (pre_ok) return lm_out_newton_w1<P, NU>(*pr, lm.ridge, lm.out_mu, lds, lds + 64 * 65, s_dl2);
       }
-      return lm_out_newton<P>(gog, gg, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65, &s_dl, pre_ok ? pr : nullptr);
+      return lm_out_newton<P>(gog, gg, on, lm.ridge, lm.out_mu, lds, lds + 64 * 65, s_dl2, pre_ok ? pr : nullptr);
+    };
+    // trust region (lm.out_tr > 0): ||d|| <= out_tr x max(||w_o||, 1e-3
+    // sqrt(on)) for the output weights w_o of point pt; a longer step is
+    // scaled onto the boundary and its exact loss change (a g.d + a^2 d.G d,
+    // the loss is quadratic along d) replaces s_dl - before any decision on it
+    __shared__ double s_nrm[2][4];
+    auto trust = [&](const int pt) {
+      if (!(lm.out_tr > 0.f)) return;
+      double dd = 0.0, ww = 0.0;
+      if (tid < P && tid >= P - on) {
+        const double di = lds[64 * 65 + tid - (P - on)], wi = pt == 0 ? w_slot0 : w_slot1;
+        dd = di * di;
+        ww = wi * wi;
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        dd += __shfl_xor(dd, o, 64);
+        ww += __shfl_xor(ww, o, 64);
+      }
+      if (lane == 0) {
+        s_nrm[0][wid] = dd;
+        s_nrm[1][wid] = ww;
+      }
+      __syncthreads();
+      const double nd = sqrt((s_nrm[0][0] + s_nrm[0][1]) + (s_nrm[0][2] + s_nrm[0][3]));
+      const double nw = sqrt((s_nrm[1][0] + s_nrm[1][1]) + (s_nrm[1][2] + s_nrm[1][3]));
+      const double rad = (double)lm.out_tr * fmax(nw, 1e-3 * sqrt((double)on));
+      if (nd > rad) {
+        const double a = rad / nd;
+        if (tid < on) lds[64 * 65 + tid] *= a;
+        if (tid == 0) s_dl2[0] = a * s_dl2[1] + a * a * (s_dl2[0] - s_dl2[1]);
+      }
+      __syncthreads();
     };
     bool out_ok = have_og && newton(src + LM_RED_OUTG, g, &og_pre[accept ? 0 : 1]);
+    if (out_ok) trust(best);
     bool use_trial = false;
     // (only for a trial within 2x the best loss: the step must then remove
     // little more than Lt - Lb, and its predicted change, exact up to the
@@ -1088,11 +1133,13 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
     if (!have_og && !stopped && !accept && on_ok && (pre_ok ? ogm_new : red_new[LM_RED_OUTG]) >= 0.0 && Lt == Lt &&
         Lt < 2.0 * Lb) {
       const bool ok_t = newton(red_new + LM_RED_OUTG, red_new + LM_GBLK_MAX, &og_pre[0]);
+      if (ok_t) trust(trial);
       use_trial = ok_t && Lt == Lt && Lt + s_dl < Lb;
       out_ok = use_trial;
     }
     __syncthreads();
     const int pub_pt = use_trial ? trial : best;  // the point the published weights start from
+
     for (int i = tid; i < P; i += 256) {
       double wd = pub_pt == 0 ? w_slot0 : w_slot1;  // (the prologue's loads: i = tid < P <= 256)
       if (out_ok) {

@@ -313,7 +313,11 @@ struct LmDesc {
   // 1: the last LM_OUTG_TAIL passes accumulate the full-batch output-layer
   // Gram matrix (slab_o -> red[LM_RED_OUTG]); the output step then uses it
   int out_gram;
-  int pad3;
+  // > 0: trust region of the output step - ||d|| <= out_tr x max(||w_o||,
+  // 1e-3 sqrt(out_n)) (w_o the output weights it starts from); a longer step
+  // is scaled back onto the boundary (its exact loss change follows: the
+  // loss is quadratic along d).  0: off
+  float out_tr;
   float* slab_o;                 // [num_wgs][3][1024] per-workgroup output-layer Gram tiles (MFMA layout)
   // 1: the Gram subsample is read from gfeat / gprice ([ns] per feature /
   // traded asset, slot order = the global subsample, simulated identically on

@@ -295,7 +295,7 @@ class HedgeRun:
                            lm_leaf_paths=int(getattr(tr, "lm_leaf_paths", -1)),
                            lm_lam0=float(tr.lm_lam0), lm_lam_up=float(tr.lm_lam_up),
                            lm_lam_down=float(tr.lm_lam_down), lm_out_fix=bool(tr.lm_out_fix),
-                           lm_out_mu=float(tr.lm_out_mu),
+                           lm_out_mu=float(tr.lm_out_mu), lm_out_tr=float(getattr(tr, "lm_out_tr", 0.0)),
                            lm_ridge=float(getattr(tr, "lm_ridge", 1e-10)),
                            lm_diag_floor=float(tr.lm_diag_floor))
         if int(tr.variant) >= 0:

@@ -120,6 +120,7 @@ class TrainingParams:
                                      # ~1e-5 of its scale are rounding noise of the bf16 hi/lo products - and
                                      # the net's own collinear directions (an exact fp32 Gram at 1e-7 blew up
                                      # basket5 seeds: BENCHMARKS.md round 5)
+    lm_out_tr: float = 0.0           # ... its trust region: ||d|| <= lm_out_tr x max(||w_o||, 1e-3 sqrt(n_o)) (0: off)
     lm_ridge: float = 1e-10          # LM systems (the fit's and the output step's): + this x the mean diagonal
     lm_renorm: bool = False          # later dates: the warm start's first layer re-expressed for the date's input
                                      # standardisation (the previous hedge as a function of the raw state)

@@ -194,6 +194,7 @@ class TrainConfig:
     # Gram's condition number reaches 1e9+; below ~1e-5 of its scale the
     # fp32-accumulated matrix is rounding noise, tools/og_precision.py)
     lm_out_mu: float = 1e-5
+    lm_out_tr: float = 0.0  # output step trust region: ||d|| <= this x max(||w_o||, 1e-3 sqrt(n_o)) (0: off)
     # run the data-parallel LM sequence (pass + reduce -> all-reduce of the
     # reduced block -> solve, one launch each) even on one rank: the test hook
     # that exercises the RCCL / mailbox exchange path at world size 1
@@ -733,6 +734,7 @@ class HipBackend:
             # (pinball fits: no output-layer / bias Newton step - the loss is not quadratic)
             lm.bias_index = -1 if pin else _lm_bias_index(self.spec, t)
             lm.out_n, lm.out_mu = (0 if pin else _lm_out_n(self.spec, t)), float(t.lm_out_mu)
+            lm.out_tr = float(t.lm_out_tr)
             lm.out_gram = 1 if lm.out_n > 0 else 0
             lm.damping = 1 if str(t.lm_damping).lower() == "nielsen" else 0
             lm.gram_skip = int(os.environ.get("RPH_LM_GRAM_SKIP", t.lm_gram_skip))  # (env: tuning sweeps)

@@ -98,7 +98,7 @@ class LmDesc(C.Structure):
         ("damping", C.c_int), ("stop_min", C.c_int), ("stop_tol", C.c_float), ("gram_skip", C.c_int),
         ("inst", C.c_int), ("explore", C.c_int), ("lam_carry", C.c_float), ("diag_floor", C.c_float), ("w0", VP),
         ("renorm", C.c_int), ("pad1", C.c_int), ("ren_mu", C.c_float * MAXIN), ("ren_isd", C.c_float * MAXIN),
-        ("out_n", C.c_int), ("out_mu", C.c_float), ("out_gram", C.c_int), ("pad3", C.c_int),
+        ("out_n", C.c_int), ("out_mu", C.c_float), ("out_gram", C.c_int), ("out_tr", C.c_float),
         ("slab_o", VP),
         ("gfeat", VP * MAXIN), ("gprice", VP * MAXIN), ("gram_side", C.c_int), ("q_delta", C.c_float), ("q_kappa", C.c_float),
         ("dp", LmDpDesc), ("dp_fused", C.c_int), ("leaf_blocks", C.c_int), ("gtarget", VP),
