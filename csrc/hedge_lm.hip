@@ -131,7 +131,12 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   // (the output-Gram instantiation does not fit twice on a CU: its Gram tiles
   // stay in the path workgroups)
   const int gram_base = B::OGM ? 0 : lm.gram_base;
-  const typename B::Sched sc = B::sched(d, lm.num_wgs, gram_base > 0 ? 0 : lm.gram_wgs, lm.gram_skip, lm.leaf_blocks);
+  // the final evaluation builds no Gram tile: its solve only accepts / rejects
+  // and takes the output-layer (or bias) Newton step, which read g, the
+  // statistics and the output Gram - so its path schedule is the even one
+  const bool fin = pass == lm.passes;
+  const typename B::Sched sc =
+      B::sched(d, lm.num_wgs, (gram_base > 0 || fin) ? 0 : lm.gram_wgs, lm.gram_skip, lm.leaf_blocks);
   if (path_wg) B::load(d, 0, perm, sc.b0 * 128, lane, pre);
   for (int i = tid; i < P; i += 256) {
     float w;
@@ -209,7 +214,7 @@ __global__ __launch_bounds__(256, B::WAVES_PER_SIMD) void k_lm_pass(const TrainD
   }
   RPH_STAMPP(2);
   const int gtile = (int)blockIdx.x - gram_base;  // this workgroup's Gram tile
-  if (gtile < 0 || gtile >= lm.gram_wgs) return;
+  if (fin || gtile < 0 || gtile >= lm.gram_wgs) return;
   // ---- Gram tile of 64 subsample paths (matrix cores) ------------------------
   if (wid == 0) {
     const long long slot = (long long)gtile * LM_TILE + lane;
@@ -396,7 +401,8 @@ __host__ __device__ constexpr int lm_pk_red_wgs(int R, int num_wgs, int dp_fused
 
 
 template <int P, int R, int NU>
-__global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass) {
+__global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __restrict__ red, const int pass,
+                                                 const int wg0) {
   using LS = LmShape<P>;
   constexpr int NG = LS::NBLK * 1024;
   __shared__ double part[1024];
@@ -408,13 +414,15 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
   const float* const slab_g = lm.slab_g + (size_t)inst * lm.gram_wgs * NG;
   const float* const slab_b = lm.slab_b + (size_t)inst * lm.num_wgs * R;
   const int tid = threadIdx.x;
+  // (wg0: the final evaluation's launch starts past the Gram workgroups)
+  const int bx = (int)blockIdx.x + wg0;
   const int NGW = lm_gram_red_wgs(NG, lm.gram_wgs);       // Gram workgroups
   const int NPW = lm_pk_red_wgs(R, lm.num_wgs, lm.dp_fused);  // packet workgroups
-  if ((int)blockIdx.x >= NGW + NPW) {
+  if (bx >= NGW + NPW) {
     // full-batch output-layer Gram (packed upper triangle, mean over every
     // path); a pass that did not build it marks entry 0 with -1
     const bool og_pass = lm.out_gram && pass > lm.passes - LM_OUTG_TAIL;
-    const int ob = blockIdx.x - (NGW + NPW);
+    const int ob = bx - (NGW + NPW);
     if (!og_pass) {
       if (ob == 0 && tid == 0) red[LM_RED_OUTG] = -1.0;
       return;
@@ -531,10 +539,10 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       if (lo < hi && hi < P) red[LmTPack<P>::OFF + TG::tidx(hi >> 4, lo >> 4) * 256 + tg_off(hi & 15, lo & 15)] = 2.0 * v;
     }
   };
-  if (NGW == NG / 1024 && (int)blockIdx.x < NGW) {
+  if (NGW == NG / 1024 && bx < NGW) {
     // <= 16 slabs: thread = entry, the 16 "group" partial sums (slab g or 0)
     // combined in the LDS form's order: even groups, odd groups, their sum
-    const int e = blockIdx.x * 1024 + tid;
+    const int e = bx * 1024 + tid;
     const float* col = slab_g + e;
     double a = 0.0, b = 0.0;
 #pragma unroll
@@ -549,13 +557,13 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     tpack(e, v);
     return;
   }
-  if ((int)blockIdx.x < NGW) {
+  if (bx < NGW) {
     // Gram: workgroup handles entries [64 b, 64 b + 64); thread (g, l) sums
     // the slabs g, g + 16, ... of entry 64 b + l (every load of a 64-slab
     // reduction in flight at once: 4 per thread), the 16 partial sums
     // combined in LDS in fixed order
     const int l = tid & 63, g = tid >> 6;
-    const int e = blockIdx.x * 64 + l;
+    const int e = bx * 64 + l;
     const float* col = slab_g + e;
     double s0 = 0.0, s1 = 0.0;
     int w = g;
@@ -607,7 +615,7 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     }
     return;
   }
-  const int pw = blockIdx.x - NGW;
+  const int pw = bx - NGW;
   const int k = tid & 3, grp = tid >> 2;
   const int i = pw * 4 + k;
   const int row = (int)(__builtin_bitreverse32((unsigned)grp) >> 24);
@@ -1396,7 +1404,8 @@ static int lm_pass_launch(const TrainDesc* d, const LmDesc* lm, int pass, const 
   using K = LmKernels<A, B, C, E>;
   // path workgroups + Gram-only workgroups past them (Gram subsample > 64 x path grid)
   const bool og = lm->out_gram && pass > lm->passes - LM_OUTG_TAIL;
-  const int gend = (og && K::BodyOG::OGM ? 0 : lm->gram_base) + lm->gram_wgs;
+  // (the final evaluation builds no Gram tile: the path grid alone)
+  const int gend = pass == lm->passes ? 0 : (og && K::BodyOG::OGM ? 0 : lm->gram_base) + lm->gram_wgs;
   const unsigned grid = (unsigned)(gend > lm->num_wgs ? gend : lm->num_wgs);
   if constexpr (K::BodyOG::OGM) {
     // the last LM_OUTG_TAIL evaluations of an lm_out_fix fit build the output Gram
@@ -1684,10 +1693,12 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK, K::Body::NU)) return rc; \
     if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    const int rg = lm_gram_red_wgs(LmShape<K::S::P>::NBLK * 1024, lm->gram_wgs) +                   \
-                   lm_pk_red_wgs(K::S::R, lm->num_wgs, lm->dp_fused) + lm_og_wgs(K::Body::NU);             \
+    const int ngw = lm_gram_red_wgs(LmShape<K::S::P>::NBLK * 1024, lm->gram_wgs);               \
+    /* the final evaluation built no Gram: its reduce starts past the Gram workgroups */       \
+    const int wg0 = pass == lm->passes ? ngw : 0;                                               \
+    const int rg = ngw + lm_pk_red_wgs(K::S::R, lm->num_wgs, lm->dp_fused) + lm_og_wgs(K::Body::NU) - wg0; \
     hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R, K::Body::NU>), dim3(rg, lm->inst), dim3(1024), 0, s, \
-                       *lm, red_new, pass);                                                     \
+                       *lm, red_new, pass, wg0);                                                \
     return (int)hipGetLastError();                                                              \
   }
   RPH_LM_SHAPES(X)
