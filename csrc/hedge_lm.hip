@@ -452,13 +452,25 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       const int lane = tid & 63, w = tid >> 6, le = lane & 15, k = lane >> 4;
       const int e = ob * 16 + le;
       const float* const so = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024 + slab_off(e);
-      double r[4];
+      double v;
+      if (lm.num_wgs > 256) {
+        // (<= 512 rows: rows 32 w + 8 k + [0, 8), the same tree one level deeper)
+        double r[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int row = 16 * w + 4 * k + u;
-        r[u] = (e < NPK && row < lm.num_wgs) ? (double)so[(size_t)row * 3 * 1024] : 0.0;
+        for (int u = 0; u < 8; ++u) {
+          const int row = 32 * w + 8 * k + u;
+          r[u] = (e < NPK && row < lm.num_wgs) ? (double)so[(size_t)row * 3 * 1024] : 0.0;
+        }
+        v = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      } else {
+        double r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int row = 16 * w + 4 * k + u;
+          r[u] = (e < NPK && row < lm.num_wgs) ? (double)so[(size_t)row * 3 * 1024] : 0.0;
+        }
+        v = (r[0] + r[1]) + (r[2] + r[3]);
       }
-      double v = (r[0] + r[1]) + (r[2] + r[3]);
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       if (k == 0) part[w * 16 + le] = v;
@@ -494,18 +506,25 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
     }
     const float* const slab_o = lm.slab_o + (size_t)inst * lm.num_wgs * 3 * 1024 + off;
     // rows [16 g, 16 g + 16) by a pairwise tree, then the 16 groups by a
-    // pairwise tree: a contiguous-halves tree over the (<= 256) rows
-    double r[16];
+    // pairwise tree: a contiguous-halves tree over the (<= 256) rows (<= 512:
+    // rows [32 g, 32 g + 32) in two halves, one level deeper)
+    const int RPG = lm.num_wgs > 256 ? 32 : 16;
+    double h[2];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int w = 16 * g + u;
-      r[u] = (e < NPK && w < lm.num_wgs) ? (double)slab_o[(size_t)w * 3 * 1024] : 0.0;
+    for (int hh = 0; hh < 2; ++hh) {
+      double r[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int w = RPG * g + 16 * hh + u;
+        r[u] = (e < NPK && w < lm.num_wgs && (hh == 0 || RPG == 32)) ? (double)slab_o[(size_t)w * 3 * 1024] : 0.0;
+      }
+#pragma unroll
+      for (int st = 1; st < 16; st <<= 1)
+#pragma unroll
+        for (int u = 0; u < 16; u += 2 * st) r[u] += r[u + st];
+      h[hh] = r[0];
     }
-#pragma unroll
-    for (int st = 1; st < 16; st <<= 1)
-#pragma unroll
-      for (int u = 0; u < 16; u += 2 * st) r[u] += r[u + st];
-    part[tid] = r[0];
+    part[tid] = RPG == 32 ? h[0] + h[1] : h[0];
     __syncthreads();
     if (g == 0) {
       double v = 0.0;
@@ -619,7 +638,17 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
   const int k = tid & 3, grp = tid >> 2;
   const int i = pw * 4 + k;
   const int row = (int)(__builtin_bitreverse32((unsigned)grp) >> 24);
-  part[tid] = row < lm.num_wgs ? (double)slab_b[(size_t)row * R + i] : 0.0;
+  if (lm.num_wgs > 256) {
+    // (<= 512 rows: position grp holds rows bitrev9(grp) = 2 bitrev8(grp) and
+    // bitrev9(grp + 256) = 2 bitrev8(grp) + 1 - the first level of the
+    // contiguous-halves tree over 512 rows; the LDS tree below is the rest)
+    const int r0 = 2 * row;
+    const double a = r0 < lm.num_wgs ? (double)slab_b[(size_t)r0 * R + i] : 0.0;
+    const double b = r0 + 1 < lm.num_wgs ? (double)slab_b[(size_t)(r0 + 1) * R + i] : 0.0;
+    part[tid] = a + b;
+  } else {
+    part[tid] = row < lm.num_wgs ? (double)slab_b[(size_t)row * R + i] : 0.0;
+  }
   __syncthreads();
 #pragma unroll
   for (int st = 128; st >= 1; st >>= 1) {
@@ -1336,8 +1365,8 @@ __global__ __launch_bounds__(256) void k_lm_solve(const TrainDesc d, const LmDes
 // ---------------------------------------------------------------------------
 template <int NIN, int H, int NO, int HEAD>
 struct LmKernels {
-  // one pass workgroup per CU, two paths per lane, packed fp32 (two
-  // workgroups per CU spill: BENCHMARKS.md round 4)
+  // two paths per lane, packed fp32; one or two pass workgroups per CU
+  // (Body::WAVES_PER_SIMD: two where the plain body fits 256 VGPRs)
   using Body = NarrowPairBody<NIN, H, NO, HEAD>;
   // the same body + the full-batch output-layer Gram on the matrix cores (the
   // last LM_OUTG_TAIL passes of an lm_out_fix fit)
@@ -1352,8 +1381,8 @@ static int lm_validate(const TrainDesc* d, const LmDesc* lm, int P, int R, int n
   if (int rc = validate_train(d, 3 /* no schedule buffers */, "rph_lm")) return rc;
   if (!lm->state || !lm->slab_b || !lm->slab_g) return rph_report("rph_lm", "null LM buffer");
   if (d->batch != d->n_local || d->steps_per_epoch != 1) return rph_report("rph_lm", "LM fits are full batch");
-  if (lm->num_wgs < 1 || lm->num_wgs > 256 || lm->passes < 0 || lm->passes >= MAXHIST)
-    return rph_report("rph_lm", "bad num_wgs (1..256) / passes");
+  if (lm->num_wgs < 1 || lm->num_wgs > LM_PASS_WGS_MAX || lm->passes < 0 || lm->passes >= MAXHIST)
+    return rph_report("rph_lm", "bad num_wgs (1..512) / passes");
   if (lm->leaf_blocks < 0 || (lm->leaf_blocks > 0 && (long long)lm->leaf_blocks * 128 * 4 * lm->num_wgs < d->batch))
     return rph_report("rph_lm", "leaf_blocks: the waves' leaves must cover the shard");
   if (lm->gram_wgs < 1 || lm->gram_wgs > 65535) return rph_report("rph_lm", "bad Gram workgroup count");
@@ -1684,6 +1713,32 @@ extern "C" int rph_lm_shape(int nin, int h, int nout, int head, int* p, int* r, 
   return -1;
 }
 
+// Pass workgroups per CU the shape's plain pass body allows (1 or 2): the
+// host sizes the pass grid up to 256 x that (engine.lm_pass_wgs).
+extern "C" int rph_lm_pass_wps(int nin, int h, int nout, int head) {
+#define X(A, B, C, E)                                        \
+  if (shape_is(nin, h, nout, head, A, B, C, E)) {            \
+    return LmKernels<A, B, C, E>::Body::WAVES_PER_SIMD;      \
+  }
+  RPH_LM_SHAPES(X)
+#undef X
+  return 1;
+}
+
+// The descriptor of one pass: the output-Gram pass body fits once per CU
+// (80 KB of LDS), so where the plain passes run two workgroups per CU (more
+// than 256: the cyclic schedule only) that pass takes 256 - one round of
+// workgroups instead of two, and a 256-row output-Gram reduction
+template <class K>
+static LmDesc lm_pass_desc(const LmDesc& lm, const int pass) {
+  LmDesc lp = lm;
+  const bool og = lm.out_gram && pass > lm.passes - LM_OUTG_TAIL;
+  if (og && K::BodyOG::WAVES_PER_SIMD == 1 && lm.leaf_blocks == 0 && lm.gram_base == 0 && lm.num_wgs > 256 &&
+      pass == lm.passes)
+    lp.num_wgs = 256;
+  return lp;
+}
+
 // One pass = pass kernel + reduce kernel (into red_new); the caller all-reduces
 // red_new when data parallel, then launches rph_lm_solve.
 extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new, int pass, void* stream) {
@@ -1692,13 +1747,14 @@ extern "C" int rph_lm_eval(const TrainDesc* d, const LmDesc* lm, double* red_new
   if (shape_is(d->nin, d->h, d->nout, d->head, A, B, C, E)) {                                  \
     using K = LmKernels<A, B, C, E>;                                                            \
     if (int rc = lm_validate(d, lm, K::S::P, K::S::R, LmShape<K::S::P>::NBLK, K::Body::NU)) return rc; \
-    if (int rc = lm_pass_launch<A, B, C, E>(d, lm, pass, red_new, s)) return rc;                \
-    const int ngw = lm_gram_red_wgs(LmShape<K::S::P>::NBLK * 1024, lm->gram_wgs);               \
+    const LmDesc lp = lm_pass_desc<K>(*lm, pass);                                               \
+    if (int rc = lm_pass_launch<A, B, C, E>(d, &lp, pass, red_new, s)) return rc;               \
+    const int ngw = lm_gram_red_wgs(LmShape<K::S::P>::NBLK * 1024, lp.gram_wgs);                \
     /* the final evaluation built no Gram: its reduce starts past the Gram workgroups */       \
-    const int wg0 = pass == lm->passes ? ngw : 0;                                               \
-    const int rg = ngw + lm_pk_red_wgs(K::S::R, lm->num_wgs, lm->dp_fused) + lm_og_wgs(K::Body::NU) - wg0; \
-    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R, K::Body::NU>), dim3(rg, lm->inst), dim3(1024), 0, s, \
-                       *lm, red_new, pass, wg0);                                                \
+    const int wg0 = pass == lp.passes ? ngw : 0;                                                \
+    const int rg = ngw + lm_pk_red_wgs(K::S::R, lp.num_wgs, lp.dp_fused) + lm_og_wgs(K::Body::NU) - wg0; \
+    hipLaunchKernelGGL((k_lm_reduce<K::S::P, K::S::R, K::Body::NU>), dim3(rg, lp.inst), dim3(1024), 0, s, \
+                       lp, red_new, pass, wg0);                                                 \
     return (int)hipGetLastError();                                                              \
   }
   RPH_LM_SHAPES(X)

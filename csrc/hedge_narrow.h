@@ -227,7 +227,13 @@ RPH_INLINE nb_bf16x8 nb_img_frag(const unsigned char* img, int s, int ub, int la
 
 template <int NIN, int H, int NO, int HEAD, bool OG = false>
 struct NarrowPairBody {
-  static constexpr int WAVES_PER_SIMD = 1;  // one pass workgroup per CU (256 VGPRs + AGPRs per lane)
+  // pass workgroups per CU: two for the 1- and 2-input free-head nets without
+  // the output Gram (their body fits 256 VGPRs and 46 KB of LDS, so two waves
+  // share each SIMD and fill each other's dependency stalls), else one (the
+  // output-Gram body needs 80 KB of LDS; aliased onto the Gram tile's image
+  // and capped at 256 VGPRs (4 spills) it gained 0.4 % and the bench P&L went
+  // wrong, cause not isolated: reverted, BENCHMARKS.md round 6)
+  static constexpr int WAVES_PER_SIMD = (!OG && NIN <= 2 && HEAD == HEAD_FREE && NO <= 2) ? 2 : 1;
   static constexpr int NIN_ = NIN, H_ = H, NO_ = NO, HEAD_ = HEAD;
   using S = NetShape<NIN, H, NO, HEAD>;
   static constexpr int P = S::P;

@@ -191,6 +191,7 @@ constexpr int LM_OUTG = 64 * 65 / 2;
 constexpr int LM_OUTG_TAIL = 1;  // evaluations of an lm_out_fix fit that carry it: the last one (passes)
 constexpr int LM_RED_OUTG = LM_GBLK_MAX + LM_NPMAX + 8;
 constexpr int LM_RED = LM_RED_OUTG + LM_OUTG;
+constexpr int LM_PASS_WGS_MAX = 512;  // LM pass workgroups (two per CU for the small nets; k_lm_reduce trees)
 constexpr int LM_OG_MAX = 64;    // output-layer parameters of the full-batch Gram (two 32-row MFMA blocks)
 // k_lm_solve workgroups of a full solve: workgroup m factorises the system at
 // the damping that m consecutive rejections would reach, so a rejection's

@@ -310,20 +310,22 @@ def gram_subsample(n_total: int, lm_gram_paths: int) -> tuple[int, int, int]:
     return ns, ns // nb, n_total // nb
 
 
-def lm_pass_wgs(n_local: int) -> int:
+def lm_pass_wgs(n_local: int, wps: int = 1) -> int:
     """Workgroups of the LM pass kernel (HipBackend._lm_buffers; the torch
-    oracle derives its Gram subsample from the same number): one per CU (256),
-    at most one per 256 local paths."""
-    return int(max(1, min(256, n_local // 256)))
+    oracle derives its Gram subsample from the same number): ``wps`` per CU
+    (256 CUs; 2 for the nets whose plain pass body fits twice on a CU,
+    native.lm_pass_wps), at most one per 256 local paths."""
+    return int(max(1, min(256 * max(1, min(int(wps), L.LM_PASS_WGS_MAX // 256)), n_local // 256)))
 
 
-def lm_pass_schedule(n_local: int, leaf_paths: int = 0) -> tuple[int, int]:
+def lm_pass_schedule(n_local: int, leaf_paths: int = 0, wps: int = 1) -> tuple[int, int]:
     """(pass workgroups, leaf blocks) of an LM pass over ``n_local`` paths
     (TrainConfig.lm_leaf_paths): auto (0) = lm_pass_wgs workgroups, the shard
     split into 4 x that many contiguous leaves; > 0 = leaves of that many
-    paths (the workgroups to cover them, at most 256); < 0 = the cyclic
+    paths (the workgroups to cover them, at most 256 x wps); < 0 = the cyclic
     schedule (leaf 0)."""
-    nw = lm_pass_wgs(n_local)
+    nw = lm_pass_wgs(n_local, wps)
+    nmax = lm_pass_wgs(1 << 40, wps)
     nblk = (int(n_local) + 127) // 128
     if leaf_paths < 0:
         return nw, 0
@@ -336,9 +338,9 @@ def lm_pass_schedule(n_local: int, leaf_paths: int = 0) -> tuple[int, int]:
         if int(n_local) % leaf_paths:
             raise ValueError(f"lm_leaf_paths {leaf_paths} does not divide the {n_local}-path shard")
         lb = leaf_paths // 128
-        nw = int(min(256, max(1, -(-nblk // (4 * lb)))))
+        nw = int(min(nmax, max(1, -(-nblk // (4 * lb)))))
         if 4 * nw * lb < nblk:
-            raise ValueError(f"{leaf_paths}-path leaves need more than 256 pass workgroups for {n_local} paths")
+            raise ValueError(f"{leaf_paths}-path leaves need more than {nmax} pass workgroups for {n_local} paths")
         if nw & (nw - 1):
             raise ValueError(f"lm_leaf_paths {leaf_paths} gives {nw} pass workgroups for {n_local} paths; world "
                              "invariance needs a power of two (choose a power-of-two shard and leaf size)")
@@ -699,7 +701,9 @@ class HipBackend:
                 raise ValueError(f"no Levenberg-Marquardt solver for net {self.spec} (8-unit nets up to 174 parameters)")
             P, R, nblk = shp
             t = self.tcfg
-            nw, leaf = lm_pass_schedule(self.n_local, int(os.environ.get("RPH_LM_LEAF", t.lm_leaf_paths)))  # (env: A/B)
+            wps = self.native.lm_pass_wps(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+            wps = int(os.environ.get("RPH_LM_WPS", wps))  # (env: A/B)
+            nw, leaf = lm_pass_schedule(self.n_local, int(os.environ.get("RPH_LM_LEAF", t.lm_leaf_paths)), wps)
             W = max(self.world, 1)
             # the global Gram subsample (every rank: gw = ns / 64 Gram workgroups,
             # past the path grid where it is larger)
@@ -893,7 +897,9 @@ class HipBackend:
             t, dev = self.tcfg, self.device
             # K instances in one launch: at most 256 / K pass workgroups each, so
             # the whole grid is co-resident (one workgroup per CU) and a pass
-            # costs one round of workgroups, not K
+            # costs one round of workgroups, not K (two per CU where the body
+            # allows it measured slower: the 32-row packet reductions cost more
+            # than the passes gain, BENCHMARKS.md round 6)
             nw, leaf = lm_pass_schedule(nsub, 0 if int(t.lm_leaf_paths) >= 0 else -1)
             if K > 1:
                 nw = max(1, min(nw, 256 // K))

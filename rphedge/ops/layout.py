@@ -67,6 +67,7 @@ LM_OUTG = 64 * 65 // 2               # full-batch output-layer Gram, packed uppe
 LM_OUTG_TAIL = 1                     # the last evaluation of an lm_out_fix fit carries it
 LM_RED_OUTG = LM_GBLK_MAX + LM_NPMAX + 8
 LM_RED = LM_RED_OUTG + LM_OUTG
+LM_PASS_WGS_MAX = 512               # LM pass workgroups (csrc/rph_types.h)
 LM_OG_MAX = 64
 LMS_W = 0
 LMS_RED = 2 * LM_NPMAX

@@ -194,6 +194,7 @@ def _bind(lib):
         "rph_eval": (C.c_int, [C.POINTER(EvalDesc), VP]),
         "rph_pnl": (C.c_int, [C.POINTER(PnlDesc), VP]),
         "rph_lm_shape": (C.c_int, [C.c_int] * 4 + [C.POINTER(C.c_int)] * 3),
+        "rph_lm_pass_wps": (C.c_int, [C.c_int] * 4),
         "rph_lm_eval": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_solve": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, C.c_int, VP]),
         "rph_lm_fit": (C.c_int, [C.POINTER(TrainDesc), C.POINTER(LmDesc), VP, VP]),
@@ -348,6 +349,12 @@ def lm_shape(nin: int, h: int, nout: int, head: int):
     if lib.rph_lm_shape(nin, h, nout, head, *[C.byref(x) for x in v]) != 0:
         return None
     return tuple(int(x.value) for x in v)
+
+
+def lm_pass_wps(nin: int, h: int, nout: int, head: int) -> int:
+    """Pass workgroups per CU of the shape's plain LM pass body (1 or 2;
+    csrc/hedge_narrow.h NarrowPairBody::WAVES_PER_SIMD)."""
+    return int(load(required=True).rph_lm_pass_wps(nin, h, nout, head))
 
 
 def lm_eval(desc: TrainDesc, lm: LmDesc, red_new: torch.Tensor, pass_: int, stream=None):

@@ -51,14 +51,15 @@ def _setup(shape, n, dev, seed=0):
     return spec, feats, pr, y, data, w0
 
 
-@pytest.mark.parametrize("shape", SHAPES)
-def test_lm_pass_block_matches_fp64(shape):
+@pytest.mark.parametrize("shape,n", [(s, 1 << 15) for s in SHAPES] + [((1, 8, 2, 0), 1 << 17), ((2, 8, 2, 0), 1 << 18)])
+def test_lm_pass_block_matches_fp64(shape, n):
+    """(2^17+ paths on the nets with two pass workgroups per CU: a 512-row
+    packet reduction)"""
     from rphedge.engine import FitConfig, HipBackend, TrainConfig
     from rphedge.models.hedge_mlp import torch_forward
     from rphedge.ops import layout as L
 
     dev = torch.device("cuda", 0)
-    n = 1 << 15
     spec, feats, pr, y, data, w0 = _setup(shape, n, dev)
     be = HipBackend(spec, n, TrainConfig(batch_size=n, lm_gram_paths=4096), device=dev)
     b = be._lm_buffers()
@@ -67,6 +68,9 @@ def test_lm_pass_block_matches_fp64(shape):
     d.batch, d.steps_per_epoch, d.shuffle, d.inv_batch = n, 1, 0, 1.0 / n
     lm = b["desc"]
     lm.passes = 1
+    if n >= 1 << 17:
+        wps = be.native.lm_pass_wps(*shape)
+        assert wps == 2 and lm.num_wgs == 512
     be.native.lm_eval(d, lm, b["red"], 0, None)
     torch.cuda.synchronize()
     red = b["red"].cpu().numpy()

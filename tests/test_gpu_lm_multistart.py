@@ -174,10 +174,13 @@ def test_renorm_reexpresses_the_warm_start():
     np.testing.assert_array_equal(got[o_["W1"]:o_["W2"]], current_weights(spec, wc)[o_["W1"]:o_["W2"]])
 
 
-@pytest.mark.parametrize("shape,fitted", [((1, 8, 2, 0), True), ((5, 8, 6, 0), True), ((2, 8, 2, 0), True),
-                                          ((1, 8, 1, 1), True), ((3, 8, 2, 0), True),
-                                          ((1, 8, 2, 0), False), ((2, 8, 2, 0), False)])
-def test_output_newton_step_matches_torch(shape, fitted):
+@pytest.mark.parametrize("shape,fitted,n", [((1, 8, 2, 0), True, 1 << 13), ((5, 8, 6, 0), True, 1 << 13),
+                                            ((2, 8, 2, 0), True, 1 << 13), ((1, 8, 1, 1), True, 1 << 13),
+                                            ((3, 8, 2, 0), True, 1 << 13), ((1, 8, 2, 0), False, 1 << 13),
+                                            ((2, 8, 2, 0), False, 1 << 13),
+                                            # 512 pass workgroups: the 512-row output-Gram reduction
+                                            ((1, 8, 2, 0), True, 1 << 17)])
+def test_output_newton_step_matches_torch(shape, fitted, n):
     """lm_out_fix: the last solve's Newton step on the output layer with the
     FULL-BATCH output Gram matrix (built on the matrix cores by the pass,
     bf16 operands, fp32 accumulation): only the output layer moves, the
@@ -190,7 +193,6 @@ def test_output_newton_step_matches_torch(shape, fitted):
     from rphedge.ops import layout as L
 
     dev = torch.device("cuda", 0)
-    n = 1 << 13
     spec, feats, pr, y, data, w_init = _setup(shape, n, dev, seed=7)
     w0 = w_init
     if fitted:

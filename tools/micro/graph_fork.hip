@@ -52,32 +52,36 @@ int main() {
   CK(hipMalloc(&out, 4096 * sizeof(float)));
   const unsigned long long T = 2000;  // 20 us at 100 MHz
   const int NK = 20;                   // kernel pairs per graph
-  for (int grid_main : {1, 256}) {
-    for (int variant = 0; variant < 2; ++variant) {
+  for (const unsigned long long T2 : {500ull, 1500ull}) {
+  for (int grid_main : {256}) {
+    for (int variant = 0; variant < 3; ++variant) {
       hipGraph_t g;
       hipGraphExec_t ge;
       CK(hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal));
       for (int k = 0; k < NK; ++k) {
         if (variant == 0) {
           hipLaunchKernelGGL(k_spin, dim3(grid_main), dim3(256), 0, s0, T, out);
-          hipLaunchKernelGGL(k_spin, dim3(1), dim3(256), 0, s0, T, out + 2048);
+          hipLaunchKernelGGL(k_spin, dim3(1), dim3(256), 0, s0, T2, out + 2048);
         } else {
           CK(hipEventRecord(fork, s0));
           CK(hipStreamWaitEvent(s1, fork, 0));
-          hipLaunchKernelGGL(k_spin, dim3(1), dim3(256), 0, s1, T, out + 2048);
+          hipLaunchKernelGGL(k_spin, dim3(1), dim3(256), 0, s1, T2, out + 2048);
           hipLaunchKernelGGL(k_spin, dim3(grid_main), dim3(256), 0, s0, T, out);
-          CK(hipEventRecord(join, s1));
-          CK(hipStreamWaitEvent(s0, join, 0));
+          if (variant == 1 || k == NK - 1) {  // variant 2: one join at the end (fork cost alone)
+            CK(hipEventRecord(join, s1));
+            CK(hipStreamWaitEvent(s0, join, 0));
+          }
         }
       }
       CK(hipStreamEndCapture(s0, &g));
       CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
       const double us = replay_us(ge, s0, 20);
-      std::printf("main grid %3d, %s: %.1f us per pair (%d pairs of 20 us kernels)\n", grid_main,
-                  variant == 0 ? "serial  " : "forked  ", us / NK, NK);
+      std::printf("main grid %3d (20 us), side %4.1f us, %s: %.1f us per pair (%d pairs)\n", grid_main,
+                  T2 / 100.0, variant == 0 ? "serial" : variant == 1 ? "fork+join" : "fork only", us / NK, NK);
       CK(hipGraphExecDestroy(ge));
       CK(hipGraphDestroy(g));
     }
+  }
   }
   CK(hipFree(out));
   return 0;
