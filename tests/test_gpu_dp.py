@@ -272,6 +272,40 @@ def test_lm_strong_scaling_rehearsal_is_bitwise(world):
         assert ss[r] == f"{st['accepted']} {st['chol_failures']}"
 
 
+@pytest.mark.parametrize("leaf", [0, 256])
+def test_lm_512_pass_workgroups_two_ranks(leaf):
+    """The two-workgroups-per-CU pass grid under data parallelism: 2^19 global
+    paths, so one rank runs 512 pass workgroups (512-row packet reduce; in
+    leaf mode also the 512-row output-Gram reduce) and each of two ranks 512
+    (cyclic) or 256 (256-path leaves).  The replicas agree bit for bit; in
+    leaf mode they are the one-rank fit bit for bit (the 512-row trees are the
+    contiguous-halves trees the rank tree completes), cyclic to 1e-4."""
+    from rphedge.engine import lm_pass_schedule
+
+    n, passes, world = 1 << 19, 6, 2
+    assert lm_pass_schedule(n, leaf, 2)[0] == 512
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "w")
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_worker_lm, args=(r, world, port, n, passes, out, True, leaf, True))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+        w0, w1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+        s0, s1 = open(out + ".0.txt").read(), open(out + ".1.txt").read()
+    assert np.array_equal(w0, w1) and s0 == s1
+    ref, st = _lm_fit(0, 1, n, passes, torch.device("cuda", 0), side=True, leaf=leaf, out_fix=True)
+    if leaf:
+        assert np.array_equal(w0, ref), np.abs(w0 - ref).max()
+        assert s0 == f"{st['accepted']} {st['chol_failures']}"
+    else:
+        np.testing.assert_allclose(w0, ref, rtol=1e-4, atol=1e-6)
+
+
 def test_lm_gram_side_one_rank_is_bitwise_the_shard_gram():
     """One rank: the Gram subsample read from simulated subsample data
     (LmDesc.gram_side) or from the shard (the same global paths) gives the
