@@ -394,9 +394,12 @@ constexpr int lm_og_wgs(int NU) { return NU <= LM_OG_MAX ? (NU * (NU + 1) / 2 + 
 constexpr int LM_TPE_MAX = 16;
 __host__ __device__ constexpr int lm_gram_red_wgs(int ng, int gram_wgs) { return gram_wgs <= LM_TPE_MAX ? ng / 1024 : ng / 64; }
 // the gradient packet likewise, for <= 16 packet rows (no fused exchange):
-// one workgroup, thread = entry, the rows' contiguous-halves tree in registers
+// one workgroup, thread = entry, the rows' contiguous-halves tree in registers;
+// <= 32 rows (the exploration's instances at two workgroups per CU): 32
+// entries per workgroup
+constexpr int LM_PK_C_MAX = 32;
 __host__ __device__ constexpr int lm_pk_red_wgs(int R, int num_wgs, int dp_fused) {
-  return (num_wgs <= LM_TPE_MAX && !dp_fused) ? 1 : R / 4;
+  return dp_fused ? R / 4 : num_wgs <= LM_TPE_MAX ? 1 : num_wgs <= LM_PK_C_MAX ? R / 32 : R / 4;
 }
 
 
@@ -632,6 +635,23 @@ __global__ __launch_bounds__(1024) void k_lm_reduce(const LmDesc lm, double* __r
       const int e = i < P ? i : LM_NPMAX + i - P;
       red[LM_GBLK_MAX + e] = a[0] + 0.0;
     }
+    return;
+  }
+  if (lm.num_wgs <= LM_PK_C_MAX && !lm.dp_fused) {
+    // 32 entries x 32 row positions: position q holds row bitrev5(q), and the
+    // LDS tree adds q + st to q for st = 16 .. 1 - the contiguous-halves tree
+    const int pw = bx - NGW;
+    const int k = tid & 31, q = tid >> 5;
+    const int i = pw * 32 + k;
+    const int row = (int)(__builtin_bitreverse32((unsigned)q) >> 27);
+    part[tid] = row < lm.num_wgs ? (double)slab_b[(size_t)row * R + i] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int st = 16; st >= 1; st >>= 1) {
+      if (q < st) part[tid] += part[tid + 32 * st];
+      __syncthreads();
+    }
+    if (tid < 32 && i < P + 4) red[LM_GBLK_MAX + (i < P ? i : LM_NPMAX + i - P)] = part[tid];
     return;
   }
   const int pw = bx - NGW;

@@ -895,17 +895,21 @@ class HipBackend:
         def make():
             _, R, nblk = self.native.lm_shape(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
             t, dev = self.tcfg, self.device
-            # K instances in one launch: at most 256 / K pass workgroups each, so
-            # the whole grid is co-resident (one workgroup per CU) and a pass
-            # costs one round of workgroups, not K (two per CU where the body
-            # allows it measured slower: the 32-row packet reductions cost more
-            # than the passes gain, BENCHMARKS.md round 6)
-            nw, leaf = lm_pass_schedule(nsub, 0 if int(t.lm_leaf_paths) >= 0 else -1)
+            # K instances in one launch: at most 256 x wps / K pass workgroups
+            # each, so the whole grid is co-resident (wps workgroups per CU) and
+            # a pass costs one round of workgroups, not K
+            wps = self.native.lm_pass_wps(self.spec.nin, self.spec.hidden, self.spec.nout, self.spec.head)
+            wps = int(os.environ.get("RPH_LM_EXPLORE_WPS", wps))  # (env: A/B)
+            nw, leaf = lm_pass_schedule(nsub, 0 if int(t.lm_leaf_paths) >= 0 else -1, wps)
+            nw1 = lm_pass_schedule(nsub, 0 if int(t.lm_leaf_paths) >= 0 else -1)[0]
             if K > 1:
-                nw = max(1, min(nw, 256 // K))
+                nw = max(1, min(nw, 256 * wps // K))
+                nw1 = max(1, min(nw1, 256 // K))
                 if leaf > 0:
                     leaf = -(-((nsub + 127) // 128) // (4 * nw))
-            gw = int(max(1, min(max(L.LM_TILE, min(int(t.lm_gram_paths), nsub)) // L.LM_TILE, nw)))
+            # (the Gram subsample: one 64-path tile per workgroup of a one-per-CU
+            # grid - the same subsample whatever wps)
+            gw = int(max(1, min(max(L.LM_TILE, min(int(t.lm_gram_paths), nsub)) // L.LM_TILE, nw1)))
             w0 = torch.zeros(K, L.LM_NPMAX, dtype=torch.float32)
             rows = np.asarray(fcfg.lm_w0s, dtype=np.float32)[:K, :P]
             w0[:, :P] = torch.from_numpy(np.ascontiguousarray(rows))
