@@ -231,3 +231,28 @@ def test_pension_lm_preset_cpu():
     for d in r.induction.dates:
         h = d.fit_q99["history"]
         assert len(h) > 1 and math.isfinite(d.fit_q99["best_loss"]) and d.fit_q99["best_loss"] <= h[0]
+
+
+def test_lm_pass_grid_sizes():
+    """LM pass grid (engine.lm_pass_wgs / lm_pass_schedule): one workgroup per
+    CU (256), or two (512) for the bodies that fit twice (native.lm_pass_wps),
+    at most one per 256 local paths; contiguous leaves keep 4 per workgroup,
+    a power-of-two workgroup count and whole leaves per shard."""
+    import pytest
+
+    from rphedge.engine import lm_pass_schedule, lm_pass_wgs
+
+    assert lm_pass_wgs(1 << 20) == 256 and lm_pass_wgs(1 << 20, 2) == 512
+    assert lm_pass_wgs(1 << 16, 2) == 256 and lm_pass_wgs(1 << 10, 2) == 4 and lm_pass_wgs(100, 2) == 1
+    assert lm_pass_wgs(1 << 20, 4) == 512  # (capped at LM_PASS_WGS_MAX)
+    assert lm_pass_schedule(1 << 20, -1, 2) == (512, 0)       # cyclic
+    assert lm_pass_schedule(1 << 20, 0, 2) == (512, 4)        # auto leaves: 512 paths
+    assert lm_pass_schedule(1 << 20, 1024, 2) == (256, 8)     # fixed leaves: 1024 paths
+    assert lm_pass_schedule(1 << 20, 512, 2) == (512, 4)
+    assert lm_pass_schedule(1 << 19, 256, 2) == (512, 2)
+    with pytest.raises(ValueError):
+        lm_pass_schedule(1 << 20, 256, 2)  # 1024 workgroups needed
+    with pytest.raises(ValueError):
+        lm_pass_schedule(1 << 20, 256, 1)
+    with pytest.raises(ValueError):
+        lm_pass_schedule(3 * (1 << 16), 1024, 2)  # 48 workgroups: not a power of two
