@@ -135,12 +135,12 @@ PRESETS = {
     "basket5": dict(model="basket", dates=252, substeps=1, paths_log2=23, epochs_first=32, epochs_rest=2,
                     batch_log2=18, lr=2e-2, lr_rest=2e-3,
                     extra=dict(mu=0.05, r=0.05, sigma=0.2, n_assets=5, basket_corr=0.5),
-                    optimizer="lm", lm_passes_first=80, lm_passes_rest=3, lm_lam_carry=2.0, lm_out_fix=1,
+                    optimizer="lm", lm_passes_first=80, lm_passes_rest=4, lm_lam_carry=2.0, lm_out_fix=1,
                     # first date: 40 passes on the 2^16-path prefix, then 80 on every path
                     # (2 seeds: 333 vs 340 ms, P&L 0.359 vs 0.374 mean; profiles/r4/presets_explore_one.jsonl);
                     # round 6 (16 seeds, profiles/r6/basket5/): 80 instead of 40 polish passes,
-                    # the output-step trust region 0.5, damping carry x2 and 3 passes per later
-                    # date: 1.157 -> 1.089 x Levy, worst 1.501 -> 1.198 x, 352 -> 425 ms
+                    # the output-step trust region 0.5, damping carry x2 and 4 passes per later
+                    # date: 1.157 -> 1.071 x Levy, worst 1.501 -> 1.131 x, 352 -> 493 ms
                     lm_out_tr=0.5,
                     lm_explore_one=1, lm_explore_passes=40, lm_explore_log2=16,
                     # (round 6: neither spread breakpoints - 16 seeds 1.165 x Levy, worst 1.358 x,

@@ -15,11 +15,12 @@ the learnt hedge's self-financing P&L std / the analytic hedge's.
   euro30    1.0087 / 1.0297 (14)                        1 2 13 14      1.035
   heston30  1.0071 / 1.0132 (5)                         1 2 5 13       1.015
   euro252   1.0412 / 1.0984 (4), residual <= 0.0749     1 2 4 12       1.12, residual 0.08
-  basket5   1.089 / 1.198 (13)                          1 3 4 13       1.22
+  basket5   1.071 / 1.131 (3)                           1 3 4 13       1.15
 
-basket5 misses the round-5 verdict's target (mean <= 1.08 x, worst <= 1.15 x
-the Levy hedge): test_basket5_verdict_target keeps that gap visible as an
-expected failure instead of absorbing it into the bound."""
+basket5 meets the round-5 verdict's target (16 seeds: mean <= 1.08 x, worst
+<= 1.15 x the Levy hedge) since the round-6 preset (4 passes per later date,
+damping carry x2, 80 first-date polish passes, output-step trust region):
+its bound IS the target."""
 import json
 import math
 import os
@@ -55,7 +56,7 @@ def _seeds(preset, seeds, extra=()):
     ("euro30", (1, 2, 13, 14), 1.035, None, 0.01),
     ("heston30", (1, 2, 5, 13), 1.015, None, 0.02),
     ("euro252", (1, 2, 4, 12), 1.12, 0.08, 0.01),
-    ("basket5", (1, 3, 4, 13), 1.22, None, None),
+    ("basket5", (1, 3, 4, 13), 1.15, None, None),
 ])
 def test_preset_pnl_within_anchor(preset, seeds, ratio, resid_max, price_tol):
     for r in _seeds(preset, seeds):
@@ -70,8 +71,7 @@ def test_preset_pnl_within_anchor(preset, seeds, ratio, resid_max, price_tol):
             assert abs(r["V0"] - r["hedge_price"]) < 0.02 * r["hedge_price"], (preset, s, r["V0"], r["hedge_price"])
 
 
-@pytest.mark.xfail(reason="basket5 misses the verdict target (16 seeds: 1.089 x mean, 1.198 x worst, seed 13)",
-                   strict=False)
 def test_basket5_verdict_target():
-    r = _seeds("basket5", (13,))[0]
+    """The round-5 verdict's basket target on its worst seed of the 16 (seed 3)."""
+    r = _seeds("basket5", (3,))[0]
     assert r["pnl"] <= 1.15 * r["anchor_pnl"], r["pnl"] / r["anchor_pnl"]
